@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Build the rocfm native extensions in-tree (gfx950 only).
+
+Two Python extension modules are produced next to the package sources:
+
+* ``rocfm/_rocfm_hip``  – every HIP kernel (csrc/kernels/*.hip, hipcc --offload-arch=gfx950)
+  plus pybind11 launch bindings (csrc/hip_module.cpp).  No torch headers: ops take raw device
+  pointers + the current HIP stream, so the module compiles in seconds and its launches are
+  captured by torch.cuda.CUDAGraph.
+* ``rocfm/_rocfm_io``   – the host-only C++ runtime (TFRecord reader/writer, CRC32C,
+  fixed-schema Example decoder, multi-threaded prefetching batch loader, libsvm converter).
+  Built with g++ so it works on CPU-only machines too.
+
+Usage: ``python build.py [--force] [-j N]``.  Incremental: objects are rebuilt only when a source
+or any header under csrc/ is newer.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "deepfm-tensorflow-distributed-training-on-amazon-sagemaker_amd")
+BUILD = os.path.join(ROOT, "build", "obj")
+CSRC = os.path.join(ROOT, "csrc")
+ARCH = os.environ.get("ROCFM_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes():
+    import pybind11
+
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def _newest_header():
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    hs += glob.glob(os.path.join(CSRC, "**", "*.inc"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _stale(obj, src, hdr_time):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return t < os.path.getmtime(src) or t < hdr_time
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n$ " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    return r.stderr
+
+
+def hip_objects(force, jobs):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + [os.path.join(CSRC, "hip_module.cpp")]
+    hdr = _newest_header()
+    os.makedirs(BUILD, exist_ok=True)
+    base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", CSRC,
+            "-Wno-unused-result", "-munsafe-fp-atomics"]
+    todo, objs = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, "hip_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, s, hdr):
+            extra = []
+            if s.endswith(".cpp"):
+                extra = ["-x", "hip"] + sum((["-I", p] for p in _py_includes()), [])
+            todo.append(base + extra + ["-c", s, "-o", o])
+    with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
+        for err in ex.map(_run, todo):
+            if err and "warning" in err:
+                sys.stderr.write(err)
+    return objs
+
+
+def io_objects(force, jobs):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "io", "*.cpp")))
+    hdr = _newest_header()
+    os.makedirs(BUILD, exist_ok=True)
+    base = [CXX, "-O3", "-fPIC", "-std=c++17", "-msse4.2", "-pthread", "-I", CSRC]
+    base += sum((["-I", p] for p in _py_includes()), [])
+    todo, objs = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, "io_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, s, hdr):
+            todo.append(base + ["-c", s, "-o", o])
+    with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
+        list(ex.map(_run, todo))
+    return objs
+
+
+def link(objs, out, hip):
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(o) for o in objs):
+        return out
+    if hip:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+    else:
+        cmd = [CXX, "-shared", "-fPIC", "-pthread", "-o", out] + objs
+    _run(cmd)
+    return out
+
+
+def build(force=False, jobs=None, hip=True, io=True):
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    outs = []
+    if io and glob.glob(os.path.join(CSRC, "io", "*.cpp")):
+        outs.append(link(io_objects(force, jobs), os.path.join(PKG, "_rocfm_io" + EXT), hip=False))
+    if hip:
+        outs.append(link(hip_objects(force, jobs), os.path.join(PKG, "_rocfm_hip" + EXT), hip=True))
+    return outs
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--no-hip", action="store_true")
+    a = ap.parse_args()
+    for o in build(a.force, a.j, hip=not a.no_hip):
+        print("built", os.path.relpath(o, ROOT))

@@ -1,0 +1,110 @@
+// rocfm — common device/host helpers for the gfx950 (CDNA4) kernels.
+//
+// Every kernel in csrc/kernels is written for MI355X only: wave64, MFMA bf16 tiles,
+// 160 KiB LDS per CU.  Launch wrappers take raw device pointers plus a hipStream_t so
+// they can be captured into HIP graphs by the Python engine (rocfm/models/fused.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+#define ROCFM_HIP_CHECK(expr)                                                        \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));     \
+  } while (0)
+
+#define ROCFM_REQUIRE(cond, msg)                                   \
+  do {                                                            \
+    if (!(cond)) throw std::invalid_argument(std::string(msg));   \
+  } while (0)
+
+namespace rocfm {
+
+constexpr int kWave = 64;
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (4 VGPR), raw bits
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16;  // 32x32 MFMA accumulator
+
+// D = A(16x32) · B(32x16) + C.  Lane l holds A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15];
+// C/D element i of lane l is (row (l>>4)*4+i, col l&15).
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+// D = A(32x16) · B(16x32) + C.  Lane l holds A[l&31][8(l>>5)+j] and B[8(l>>5)+j][l&31];
+// C/D register r of lane l is (row (r&3)+8(r>>2)+4(l>>5), col l&31).
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+
+// f32 -> bf16, round-to-nearest-even.  NaN stays NaN (cdna guide: avoid the integer trick for NaN).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
+
+// Wave-wide reductions (64 lanes).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG (dropout masks).  Keyed by (seed, step); counter by
+// (row, column-group).  The same (seed, step, row, col) always yields the same mask, so the
+// backward pass and the eager oracle (rocfm/ops/reference.py) can regenerate it exactly.
+// ---------------------------------------------------------------------------------------
+struct Philox4 {
+  uint32_t x, y, z, w;
+};
+__host__ __device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+__host__ __device__ __forceinline__ Philox4 philox4x32_10(Philox4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(0xD2511F53u, c.x, &hi0);
+    uint32_t lo1 = mulhilo(0xCD9E8D57u, c.z, &hi1);
+    Philox4 n;
+    n.x = hi1 ^ c.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ c.w ^ k1;
+    n.w = lo0;
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+// Dropout keep decisions for the 4 rows 4*rg .. 4*rg+3 of column `col` of hidden layer `layer`.
+// u = (philox lane >> 8) / 2^24; keep iff u < keep.  rocfm/ops/reference.py replicates this.
+__host__ __device__ __forceinline__ Philox4 dropout_bits(uint64_t seed, uint32_t layer, uint32_t step,
+                                                         uint32_t rg, uint32_t col) {
+  Philox4 c{rg, col, layer, step};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__host__ __device__ __forceinline__ bool keep_from_bits(uint32_t v, float keep) {
+  return (float)(v >> 8) * (1.0f / 16777216.0f) < keep;
+}
+
+}  // namespace rocfm

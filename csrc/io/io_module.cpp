@@ -1,0 +1,194 @@
+// pybind11 bindings for the host runtime (module rocfm._rocfm_io).  Host-only: builds and runs on
+// CPU-only machines (tests) and feeds pinned buffers on the GPU box.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "loader.h"
+#include "tfrecord.h"
+
+namespace py = pybind11;
+using namespace rocfm::io;
+
+static Schema make_schema(int field_size, const std::string& label_key, const std::string& ids_key,
+                          const std::string& vals_key) {
+  Schema s;
+  s.field_size = field_size;
+  s.label_key = label_key;
+  s.ids_key = ids_key;
+  s.vals_key = vals_key;
+  return s;
+}
+
+PYBIND11_MODULE(_rocfm_io, m) {
+  m.doc() = "rocfm host runtime: TFRecord/Example codec, CRC32C, batch loader, libsvm converter";
+
+  m.def("crc32c", [](py::bytes b) {
+    std::string s = b;
+    return crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  m.def("masked_crc32c", [](py::bytes b) {
+    std::string s = b;
+    return mask_crc(crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
+  });
+
+  m.def(
+      "encode_example",
+      [](float label, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
+         py::array_t<float, py::array::c_style | py::array::forcecast> vals, const std::string& label_key,
+         const std::string& ids_key, const std::string& vals_key) {
+        if (ids.size() != vals.size()) throw std::invalid_argument("ids/vals length mismatch");
+        Schema s = make_schema((int)ids.size(), label_key, ids_key, vals_key);
+        std::string out;
+        encode_example(s, label, ids.data(), vals.data(), (int)ids.size(), &out);
+        return py::bytes(out);
+      },
+      py::arg("label"), py::arg("ids"), py::arg("vals"), py::arg("label_key") = "label", py::arg("ids_key") = "ids",
+      py::arg("vals_key") = "values");
+
+  m.def(
+      "decode_example",
+      [](py::bytes payload, int field_size, int64_t max_id, const std::string& label_key, const std::string& ids_key,
+         const std::string& vals_key) {
+        std::string p = payload;
+        Schema s = make_schema(field_size, label_key, ids_key, vals_key);
+        float label = 0;
+        py::array_t<int32_t> ids(field_size);
+        py::array_t<float> vals(field_size);
+        int st = decode_example(reinterpret_cast<const uint8_t*>(p.data()), p.size(), s, &label,
+                                ids.mutable_data(), vals.mutable_data(), max_id);
+        return py::make_tuple(st, label, ids, vals);
+      },
+      py::arg("payload"), py::arg("field_size"), py::arg("max_id") = 0, py::arg("label_key") = "label",
+      py::arg("ids_key") = "ids", py::arg("vals_key") = "values");
+
+  // Write a whole batch of Examples as a TFRecord file (synthetic data generation, tests).
+  m.def(
+      "write_tfrecord",
+      [](const std::string& path, py::array_t<float, py::array::c_style | py::array::forcecast> labels,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
+         py::array_t<float, py::array::c_style | py::array::forcecast> vals, bool append) {
+        if (ids.ndim() != 2 || vals.ndim() != 2 || ids.shape(0) != labels.size() || vals.shape(0) != labels.size() ||
+            ids.shape(1) != vals.shape(1))
+          throw std::invalid_argument("write_tfrecord: expects labels[N], ids[N,F], vals[N,F]");
+        const int64_t N = labels.size();
+        const int F = (int)ids.shape(1);
+        Schema s = make_schema(F, "label", "ids", "values");
+        std::string out, ex;
+        out.reserve((size_t)N * (16 + 12 * F + 64));
+        {
+          py::gil_scoped_release nogil;
+          for (int64_t i = 0; i < N; ++i) {
+            ex.clear();
+            encode_example(s, labels.data()[i], ids.data() + i * F, vals.data() + i * F, F, &ex);
+            frame_record(reinterpret_cast<const uint8_t*>(ex.data()), ex.size(), &out);
+          }
+        }
+        FILE* f = fopen(path.c_str(), append ? "ab" : "wb");
+        if (!f) throw std::runtime_error("cannot open " + path);
+        size_t w = fwrite(out.data(), 1, out.size(), f);
+        fclose(f);
+        if (w != out.size()) throw std::runtime_error("short write " + path);
+        return N;
+      },
+      py::arg("path"), py::arg("labels"), py::arg("ids"), py::arg("vals"), py::arg("append") = false);
+
+  m.def(
+      "decode_file",
+      [](const std::string& path, int field_size, int64_t max_id, bool verify_crc, bool skip_bad) {
+        Schema s = make_schema(field_size, "label", "ids", "values");
+        std::vector<float> labels, vals;
+        std::vector<int32_t> ids;
+        size_t n;
+        {
+          py::gil_scoped_release nogil;
+          n = decode_file(path, s, max_id, verify_crc, skip_bad, &labels, &ids, &vals);
+        }
+        py::array_t<float> L((py::ssize_t)n);
+        py::array_t<int32_t> I({(py::ssize_t)n, (py::ssize_t)field_size});
+        py::array_t<float> V({(py::ssize_t)n, (py::ssize_t)field_size});
+        std::copy(labels.begin(), labels.end(), L.mutable_data());
+        std::copy(ids.begin(), ids.end(), I.mutable_data());
+        std::copy(vals.begin(), vals.end(), V.mutable_data());
+        return py::make_tuple(L, I, V);
+      },
+      py::arg("path"), py::arg("field_size"), py::arg("max_id") = 0, py::arg("verify_crc") = true,
+      py::arg("skip_bad") = false);
+
+  m.def(
+      "scan_file",
+      [](const std::string& path, bool verify_crc, bool skip_bad) {
+        // returns (num_records, bad_records, list of payload lengths)
+        FILE* f = fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("cannot open " + path);
+        std::string buf;
+        char tmp[1 << 16];
+        size_t g;
+        while ((g = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.append(tmp, g);
+        fclose(f);
+        std::vector<RecordRef> recs;
+        size_t bad = 0;
+        scan_records(reinterpret_cast<const uint8_t*>(buf.data()), buf.size(), verify_crc, skip_bad, &recs, &bad);
+        std::vector<uint32_t> lens;
+        for (auto& r : recs) lens.push_back(r.len);
+        return py::make_tuple(recs.size(), bad, lens);
+      },
+      py::arg("path"), py::arg("verify_crc") = true, py::arg("skip_bad") = false);
+
+  m.def(
+      "convert_libsvm",
+      [](const std::string& in_path, const std::string& out_path, int num_threads) {
+        Schema s = make_schema(0, "label", "ids", "values");
+        py::gil_scoped_release nogil;
+        return convert_libsvm(in_path, out_path, s, num_threads);
+      },
+      py::arg("in_path"), py::arg("out_path"), py::arg("num_threads") = 4);
+
+  py::class_<BatchLoader>(m, "BatchLoader")
+      .def(py::init([](std::vector<std::string> files, int field_size, int64_t max_id, int batch_size,
+                       bool drop_remainder, int num_epochs, int shard_count, int shard_index, int num_threads,
+                       int num_slots, bool verify_crc, bool skip_bad, int shuffle_buffer, uint64_t seed,
+                       bool stream_mode) {
+             LoaderOptions o;
+             o.files = std::move(files);
+             o.schema.field_size = field_size;
+             o.max_id = max_id;
+             o.batch_size = batch_size;
+             o.drop_remainder = drop_remainder;
+             o.num_epochs = num_epochs;
+             o.shard_count = shard_count;
+             o.shard_index = shard_index;
+             o.num_threads = num_threads;
+             o.num_slots = num_slots;
+             o.verify_crc = verify_crc;
+             o.skip_bad = skip_bad;
+             o.shuffle_buffer = shuffle_buffer;
+             o.seed = seed;
+             o.stream_mode = stream_mode;
+             return new BatchLoader(o);
+           }),
+           py::arg("files"), py::arg("field_size"), py::arg("max_id") = 0, py::arg("batch_size") = 1024,
+           py::arg("drop_remainder") = true, py::arg("num_epochs") = 1, py::arg("shard_count") = 1,
+           py::arg("shard_index") = 0, py::arg("num_threads") = 4, py::arg("num_slots") = 4,
+           py::arg("verify_crc") = true, py::arg("skip_bad") = false, py::arg("shuffle_buffer") = 0,
+           py::arg("seed") = 0, py::arg("stream_mode") = false)
+      .def("set_slot",
+           [](BatchLoader& L, int i, uintptr_t ids, uintptr_t vals, uintptr_t labels) {
+             L.set_slot(i, reinterpret_cast<int32_t*>(ids), reinterpret_cast<float*>(vals),
+                        reinterpret_cast<float*>(labels));
+           })
+      .def("start", &BatchLoader::start)
+      .def("next",
+           [](BatchLoader& L) {
+             int rows = 0, epoch = 0, slot;
+             {
+               py::gil_scoped_release nogil;
+               slot = L.next(&rows, &epoch);
+             }
+             return py::make_tuple(slot, rows, epoch);
+           })
+      .def("release", &BatchLoader::release)
+      .def("stop", &BatchLoader::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("bad_records", &BatchLoader::bad_records)
+      .def_property_readonly("records_seen", &BatchLoader::records_seen);
+}

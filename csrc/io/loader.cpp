@@ -1,0 +1,444 @@
+// rocfm host runtime: multi-threaded TFRecord batch loader (see loader.h).
+#include "loader.h"
+
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <fstream>
+#include <random>
+#include <sstream>
+#include <stdexcept>
+
+namespace rocfm {
+namespace io {
+
+struct BatchLoader::Chunk {
+  const uint8_t* data = nullptr;
+  size_t size = 0;
+  void* map = nullptr;
+  std::string arena;  // stream mode
+  ~Chunk() {
+    if (map && map != MAP_FAILED) munmap(map, size);
+  }
+};
+
+namespace {
+std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path);
+}
+
+BatchLoader::BatchLoader(const LoaderOptions& opt) : opt_(opt) {
+  if (opt_.batch_size <= 0) throw std::invalid_argument("batch_size must be > 0");
+  if (opt_.shard_count <= 0 || opt_.shard_index < 0 || opt_.shard_index >= opt_.shard_count)
+    throw std::invalid_argument("bad shard spec");
+  if (opt_.num_slots < 2) opt_.num_slots = 2;
+  if (opt_.num_threads < 1) opt_.num_threads = 1;
+  slots_.resize(opt_.num_slots);
+  slot_state_.assign(opt_.num_slots, 0);
+  slot_seq_.resize(opt_.num_slots);
+  for (int i = 0; i < opt_.num_slots; ++i) slot_seq_[i] = i;
+  slot_rows_.assign(opt_.num_slots, 0);
+  slot_epoch_.assign(opt_.num_slots, 0);
+}
+
+BatchLoader::~BatchLoader() { stop(); }
+
+void BatchLoader::set_slot(int i, int32_t* ids, float* vals, float* labels) {
+  if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot");
+  slots_[i] = Slot{ids, vals, labels};
+}
+
+void BatchLoader::start() {
+  if (started_) return;
+  for (auto& s : slots_)
+    if (!s.ids || !s.vals || !s.labels) throw std::runtime_error("all slots must be set before start()");
+  started_ = true;
+  reader_ = std::thread(&BatchLoader::reader_main, this);
+  for (int i = 0; i < opt_.num_threads; ++i) workers_.emplace_back(&BatchLoader::worker_main, this);
+}
+
+void BatchLoader::stop() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (reader_.joinable()) reader_.join();
+  for (auto& t : workers_)
+    if (t.joinable()) t.join();
+  workers_.clear();
+}
+
+void BatchLoader::fail(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (error_.empty()) error_ = msg;
+    stop_ = true;
+  }
+  cv_.notify_all();
+}
+
+void BatchLoader::push_job(Job&& j) {
+  std::unique_lock<std::mutex> lk(mu_);
+  // bound the queue: at most 2 × slots outstanding jobs
+  cv_.wait(lk, [&] { return stop_ || (int)jobs_.size() < 2 * opt_.num_slots; });
+  if (stop_) return;
+  jobs_.push_back(std::move(j));
+  lk.unlock();
+  cv_.notify_all();
+}
+
+namespace {
+
+std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path) {
+  auto c = std::make_shared<BatchLoader::Chunk>();
+  int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + path + ": " + strerror(errno));
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    ::close(fd);
+    throw std::runtime_error("cannot stat " + path);
+  }
+  c->size = (size_t)st.st_size;
+  if (c->size) {
+    c->map = mmap(nullptr, c->size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (c->map == MAP_FAILED) {
+      ::close(fd);
+      throw std::runtime_error("mmap failed for " + path);
+    }
+    madvise(c->map, c->size, MADV_SEQUENTIAL | MADV_WILLNEED);
+    c->data = static_cast<const uint8_t*>(c->map);
+  }
+  ::close(fd);
+  return c;
+}
+
+// Read TFRecord frames from a stream (FIFO / stdin) into an arena of ≈arena_bytes.
+bool read_stream_chunk(FILE* f, size_t arena_bytes, bool verify, bool skip_bad, BatchLoader::Chunk* c,
+                       std::vector<RecordRef>* recs, size_t* bad) {
+  std::string& a = c->arena;
+  a.clear();
+  std::vector<std::pair<size_t, uint32_t>> offs;
+  while (a.size() < arena_bytes) {
+    uint8_t hdr[12];
+    size_t got = fread(hdr, 1, 12, f);
+    if (got == 0) break;
+    if (got != 12) throw std::runtime_error("TFRecord stream: truncated header");
+    uint64_t len;
+    memcpy(&len, hdr, 8);
+    uint32_t lcrc;
+    memcpy(&lcrc, hdr + 8, 4);
+    if (verify && mask_crc(crc32c(hdr, 8)) != lcrc) throw std::runtime_error("TFRecord stream: corrupt length CRC");
+    size_t off = a.size();
+    a.resize(off + len + 4);
+    if (fread(&a[off], 1, len + 4, f) != len + 4) throw std::runtime_error("TFRecord stream: truncated record");
+    bool ok = true;
+    if (verify) {
+      uint32_t dcrc;
+      memcpy(&dcrc, &a[off + len], 4);
+      ok = mask_crc(crc32c(reinterpret_cast<const uint8_t*>(&a[off]), len)) == dcrc;
+      if (!ok && !skip_bad) throw std::runtime_error("TFRecord stream: corrupt data CRC");
+    }
+    if (ok)
+      offs.emplace_back(off, (uint32_t)len);
+    else
+      ++*bad;
+  }
+  c->data = reinterpret_cast<const uint8_t*>(a.data());
+  c->size = a.size();
+  for (auto& o : offs) recs->push_back(RecordRef{c->data + o.first, o.second});
+  return !offs.empty();
+}
+
+}  // namespace
+
+void BatchLoader::reader_main() {
+  try {
+    int64_t seq = 0;
+    std::mt19937_64 rng(opt_.seed);
+    const int B = opt_.batch_size;
+    for (int epoch = 0; opt_.num_epochs < 0 || epoch < opt_.num_epochs; ++epoch) {
+      Job cur;
+      cur.epoch = epoch;
+      std::vector<RecordRef> shuf;  // shuffle buffer
+      std::vector<std::shared_ptr<Chunk>> shuf_keep;
+      int64_t ridx = 0;  // record index across the concatenated file list (Dataset.shard)
+      auto emit = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
+        if (cur.keep.empty() || cur.keep.back() != keep) cur.keep.push_back(keep);
+        cur.recs.push_back(r);
+        if ((int)cur.recs.size() == B) {
+          cur.seq = seq++;
+          push_job(std::move(cur));
+          cur = Job();
+          cur.epoch = epoch;
+        }
+      };
+      auto take = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
+        ++seen_;
+        if ((ridx++ % opt_.shard_count) != opt_.shard_index) return;
+        if (opt_.shuffle_buffer > 0) {
+          shuf.push_back(r);
+          shuf_keep.push_back(keep);
+          if ((int)shuf.size() >= opt_.shuffle_buffer) {
+            size_t k = rng() % shuf.size();
+            emit(shuf[k], shuf_keep[k]);
+            shuf[k] = shuf.back();
+            shuf_keep[k] = shuf_keep.back();
+            shuf.pop_back();
+            shuf_keep.pop_back();
+          }
+        } else {
+          emit(r, keep);
+        }
+      };
+      for (const auto& path : opt_.files) {
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (stop_) return;
+        }
+        if (opt_.stream_mode) {
+          FILE* f = (path == "-") ? stdin : fopen(path.c_str(), "rb");
+          if (!f) throw std::runtime_error("cannot open stream " + path);
+          while (true) {
+            auto c = std::make_shared<Chunk>();
+            std::vector<RecordRef> recs;
+            size_t bad = 0;
+            bool any = read_stream_chunk(f, (size_t)8 << 20, opt_.verify_crc, opt_.skip_bad, c.get(), &recs, &bad);
+            bad_ += bad;
+            for (auto& r : recs) take(r, c);
+            if (!any) break;
+            std::lock_guard<std::mutex> g(mu_);
+            if (stop_) break;
+          }
+          if (f != stdin) fclose(f);
+        } else {
+          auto c = map_file(path);
+          std::vector<RecordRef> recs;
+          size_t bad = 0;
+          scan_records(c->data, c->size, opt_.verify_crc, opt_.skip_bad, &recs, &bad);
+          bad_ += bad;
+          for (auto& r : recs) take(r, c);
+        }
+      }
+      // drain the shuffle buffer
+      while (!shuf.empty()) {
+        size_t k = rng() % shuf.size();
+        emit(shuf[k], shuf_keep[k]);
+        shuf[k] = shuf.back();
+        shuf_keep[k] = shuf_keep.back();
+        shuf.pop_back();
+        shuf_keep.pop_back();
+      }
+      if (!cur.recs.empty() && !opt_.drop_remainder) {
+        cur.seq = seq++;
+        push_job(std::move(cur));
+      }
+      if (opt_.stream_mode && opt_.num_epochs < 0) break;  // a pipe cannot be rewound
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      jobs_total_ = seq;
+    }
+    cv_.notify_all();
+  } catch (const std::exception& e) {
+    fail(e.what());
+  }
+}
+
+void BatchLoader::worker_main() {
+  const int F = opt_.schema.field_size;
+  while (true) {
+    Job job;
+    int slot;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+      if (stop_) return;
+      job = std::move(jobs_.front());
+      jobs_.pop_front();
+      cv_.notify_all();
+      slot = (int)(job.seq % opt_.num_slots);
+      cv_.wait(lk, [&] { return stop_ || (slot_state_[slot] == 0 && slot_seq_[slot] == job.seq); });
+      if (stop_) return;
+      slot_state_[slot] = 1;
+    }
+    Slot& s = slots_[slot];
+    int n = (int)job.recs.size();
+    std::string err;
+    for (int r = 0; r < n; ++r) {
+      int st = decode_example(job.recs[r].data, job.recs[r].len, opt_.schema, s.labels + r,
+                              s.ids + (size_t)r * F, s.vals + (size_t)r * F, opt_.max_id);
+      if (st != kOk) {
+        static const char* names[] = {"ok", "malformed Example protobuf", "missing feature",
+                                      "wrong feature length (FixedLenFeature expects field_size values)",
+                                      "id out of range [0, feature_size)"};
+        err = std::string("decode error in batch ") + std::to_string(job.seq) + " record " + std::to_string(r) +
+              ": " + names[st];
+        break;
+      }
+    }
+    if (!err.empty()) {
+      fail(err);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      slot_rows_[slot] = n;
+      slot_epoch_[slot] = job.epoch;
+      slot_state_[slot] = 2;
+    }
+    cv_.notify_all();
+  }
+}
+
+int BatchLoader::next(int* nrows, int* epoch) {
+  std::unique_lock<std::mutex> lk(mu_);
+  int slot = (int)(next_consume_ % opt_.num_slots);
+  cv_.wait(lk, [&] {
+    return !error_.empty() || (slot_state_[slot] == 2 && slot_seq_[slot] == next_consume_) ||
+           (jobs_total_ >= 0 && next_consume_ >= jobs_total_) || (stop_ && error_.empty());
+  });
+  if (!error_.empty()) throw std::runtime_error(error_);
+  if (slot_state_[slot] == 2 && slot_seq_[slot] == next_consume_) {
+    *nrows = slot_rows_[slot];
+    *epoch = slot_epoch_[slot];
+    ++next_consume_;
+    return slot;
+  }
+  return -1;
+}
+
+void BatchLoader::release(int slot) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (slot < 0 || slot >= opt_.num_slots || slot_state_[slot] != 2) return;
+    slot_state_[slot] = 0;
+    slot_seq_[slot] += opt_.num_slots;
+  }
+  cv_.notify_all();
+}
+
+size_t decode_file(const std::string& path, const Schema& s, int64_t max_id, bool verify_crc, bool skip_bad,
+                   std::vector<float>* labels, std::vector<int32_t>* ids, std::vector<float>* vals) {
+  auto c = map_file(path);
+  std::vector<RecordRef> recs;
+  size_t bad = 0;
+  scan_records(c->data, c->size, verify_crc, skip_bad, &recs, &bad);
+  const int F = s.field_size;
+  labels->resize(recs.size());
+  ids->resize(recs.size() * (size_t)F);
+  vals->resize(recs.size() * (size_t)F);
+  size_t out = 0;
+  for (size_t r = 0; r < recs.size(); ++r) {
+    int st = decode_example(recs[r].data, recs[r].len, s, labels->data() + out, ids->data() + out * F,
+                            vals->data() + out * F, max_id);
+    if (st != kOk) {
+      if (skip_bad) continue;
+      throw std::runtime_error("decode error in " + path + " record " + std::to_string(r) + " (status " +
+                               std::to_string(st) + ")");
+    }
+    ++out;
+  }
+  labels->resize(out);
+  ids->resize(out * (size_t)F);
+  vals->resize(out * (size_t)F);
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------------
+// libsvm → TFRecord
+// ------------------------------------------------------------------------------------------------
+namespace {
+bool parse_libsvm_line(const char* p, const char* end, float* label, std::vector<int64_t>* ids,
+                       std::vector<float>* vals) {
+  ids->clear();
+  vals->clear();
+  while (p < end && (*p == ' ' || *p == '\t')) ++p;
+  if (p >= end) return false;
+  char* q;
+  *label = strtof(p, &q);
+  if (q == p) return false;
+  p = q;
+  while (p < end) {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+    if (p >= end) break;
+    long long id = strtoll(p, &q, 10);
+    if (q == p || q >= end || *q != ':') return false;
+    p = q + 1;
+    float v = strtof(p, &q);
+    if (q == p) return false;
+    p = q;
+    ids->push_back(id);
+    vals->push_back(v);
+  }
+  return true;
+}
+}  // namespace
+
+size_t convert_libsvm(const std::string& in_path, const std::string& out_path, const Schema& s, int num_threads) {
+  auto c = map_file(in_path);
+  const char* base = reinterpret_cast<const char*>(c->data);
+  size_t n = c->size;
+  if (num_threads < 1) num_threads = 1;
+  // split on line boundaries
+  std::vector<size_t> cuts{0};
+  for (int t = 1; t < num_threads; ++t) {
+    size_t pos = n * t / num_threads;
+    while (pos < n && base[pos] != '\n') ++pos;
+    if (pos < n) ++pos;
+    if (pos > cuts.back()) cuts.push_back(pos);
+  }
+  cuts.push_back(n);
+  int parts = (int)cuts.size() - 1;
+  std::vector<std::string> outs(parts);
+  std::vector<size_t> counts(parts, 0);
+  std::vector<std::string> errs(parts);
+  std::vector<std::thread> th;
+  for (int t = 0; t < parts; ++t) {
+    th.emplace_back([&, t] {
+      std::vector<int64_t> ids;
+      std::vector<float> vals;
+      std::string ex;
+      const char* p = base + cuts[t];
+      const char* end = base + cuts[t + 1];
+      while (p < end) {
+        const char* nl = (const char*)memchr(p, '\n', end - p);
+        const char* le = nl ? nl : end;
+        float label;
+        if (parse_libsvm_line(p, le, &label, &ids, &vals)) {
+          ex.clear();
+          encode_example(s, label, ids.data(), vals.data(), (int)ids.size(), &ex);
+          frame_record(reinterpret_cast<const uint8_t*>(ex.data()), ex.size(), &outs[t]);
+          ++counts[t];
+        } else {
+          const char* q = p;
+          while (q < le && (*q == ' ' || *q == '\t' || *q == '\r')) ++q;
+          if (q < le && errs[t].empty()) errs[t] = std::string("cannot parse libsvm line: ") + std::string(p, le);
+        }
+        p = le + 1;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
+  FILE* f = fopen(out_path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot write " + out_path);
+  size_t total = 0;
+  for (int t = 0; t < parts; ++t) {
+    if (fwrite(outs[t].data(), 1, outs[t].size(), f) != outs[t].size()) {
+      fclose(f);
+      throw std::runtime_error("short write to " + out_path);
+    }
+    total += counts[t];
+  }
+  fclose(f);
+  return total;
+}
+
+}  // namespace io
+}  // namespace rocfm

@@ -1,0 +1,109 @@
+// rocfm host runtime: multi-threaded TFRecord batch loader (replaces the tf.data C++ runtime the
+// reference's input_fn drives: PS:112-169, HVD:104-161).
+//
+// Pipeline (per epoch, like the reference's shard → batch(drop_remainder) → parse → repeat):
+//   reader thread : mmap file (or read a FIFO/stdin in pipe mode) → walk TFRecord framing +
+//                   CRC32C → keep every shard_count-th record starting at shard_index (record
+//                   index runs over the concatenated file list, = Dataset.shard) → optional
+//                   shuffle buffer → cut batches of batch_size (tail dropped per epoch when
+//                   drop_remainder) → job queue
+//   N workers     : decode a job's records straight into output slot (seq % num_slots)
+//   consumer      : next() returns slots strictly in sequence order; release() recycles them.
+// Output slots are caller-provided host buffers (Python passes pinned torch tensors so the H2D copy
+// is a true async DMA on a side HIP stream).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tfrecord.h"
+
+namespace rocfm {
+namespace io {
+
+struct LoaderOptions {
+  std::vector<std::string> files;
+  Schema schema;
+  int64_t max_id = 0;  // ids must be < max_id (0 = unchecked)
+  int batch_size = 1024;
+  bool drop_remainder = true;
+  int num_epochs = 1;  // < 0 → forever
+  int shard_count = 1;
+  int shard_index = 0;
+  int num_threads = 4;
+  int num_slots = 4;
+  bool verify_crc = true;
+  bool skip_bad = false;
+  int shuffle_buffer = 0;  // records; 0 = no record shuffle (reference default, Q6)
+  uint64_t seed = 0;
+  bool stream_mode = false;  // pipe mode: files are FIFOs / "-" for stdin, read sequentially
+};
+
+struct Slot {
+  int32_t* ids = nullptr;
+  float* vals = nullptr;
+  float* labels = nullptr;
+};
+
+class BatchLoader {
+ public:
+  explicit BatchLoader(const LoaderOptions& opt);
+  ~BatchLoader();
+  void set_slot(int i, int32_t* ids, float* vals, float* labels);
+  void start();
+  // Blocks until the next batch is decoded.  Returns slot index and fills nrows/epoch; returns -1
+  // at end of data.  Throws on decode/framing errors.
+  int next(int* nrows, int* epoch);
+  void release(int slot);
+  void stop();
+  size_t bad_records() const { return bad_.load(); }
+  size_t records_seen() const { return seen_.load(); }
+
+  struct Chunk;  // owns the bytes (mmap or arena)
+
+ private:
+  struct Job {
+    int64_t seq;
+    int epoch;
+    std::vector<RecordRef> recs;
+    std::vector<std::shared_ptr<Chunk>> keep;
+  };
+  void reader_main();
+  void worker_main();
+  void push_job(Job&& j);
+  void fail(const std::string& msg);
+
+  LoaderOptions opt_;
+  std::vector<Slot> slots_;
+  std::vector<int> slot_state_;    // 0 free, 1 filling, 2 ready
+  std::vector<int64_t> slot_seq_;  // seq the slot currently holds / will hold
+  std::vector<int> slot_rows_, slot_epoch_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> jobs_;
+  int64_t next_consume_ = 0;
+  int64_t jobs_total_ = -1;  // set when reader finishes
+  bool stop_ = false;
+  std::string error_;
+  std::thread reader_;
+  std::vector<std::thread> workers_;
+  std::atomic<size_t> bad_{0}, seen_{0};
+  bool started_ = false;
+};
+
+// Decode an entire TFRecord file (small files: validation sets, tests).
+size_t decode_file(const std::string& path, const Schema& s, int64_t max_id, bool verify_crc, bool skip_bad,
+                   std::vector<float>* labels, std::vector<int32_t>* ids, std::vector<float>* vals);
+
+// libsvm ("label id:val id:val ...") → TFRecord, multi-threaded, output order = input order.
+// Mirrors tools/libsvm_to_tfrecord.py:22-61 (one Example per line, every pair kept).
+// Returns number of records written.
+size_t convert_libsvm(const std::string& in_path, const std::string& out_path, const Schema& s, int num_threads);
+
+}  // namespace io
+}  // namespace rocfm

@@ -1,0 +1,86 @@
+// Parameter blocks shared by the DeepFM row-tile kernel and its host launcher.
+#pragma once
+#include "../common.h"
+#include "optim.h"
+
+namespace rocfm {
+
+constexpr int kMaxHidden = 6;  // hidden MLP layers supported by the fused engine
+constexpr int kRowTile = 16;   // rows per workgroup = one 16-row MFMA M tile
+constexpr int kRowThreads = 256;
+
+struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
+  int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32;
+  int lda[kMaxHidden + 1];  // bf16 row stride of each activation tile
+  int ldz;                  // bf16 row stride of the dz ping-pong tiles
+  int total;
+};
+
+struct RowsParams {
+  // inputs
+  const int32_t* ids;   // [B][F]
+  const float* vals;    // [B][F]
+  const float* labels;  // [B]
+  const float* emb;     // [V][Kp]: cols 0..K-1 = fm_v row, col K = fm_w, rest 0
+  const float* fm_bias;
+  const float* w_out;  // [dims[nl]] f32 (deep_out/weights)
+  const float* b_out;  // [1]
+  const uint16_t* WT[kMaxHidden];  // layer l: [dims[l+1]][dims[l]] bf16 (forward B operand)
+  const uint16_t* Wb[kMaxHidden];  // layer l: [dims[l]][dims[l+1]] bf16 (backward B operand)
+  const float* bias[kMaxHidden];   // layer l: [dims[l+1]]
+  float keep[kMaxHidden];
+  int dims[kMaxHidden + 1];  // dims[0] = round_up(F*K, 32); dims[l>0] = hidden width padded to 32
+  int nl, F, K, Kp, B, Bp;   // B valid rows; Bp = padded rows = leading dim of actT/dzT
+  float inv_scale;           // dL/dy scale (1/B_local)
+  int train, loss_type;      // loss_type 0 log_loss, 1 square_loss
+  uint64_t seed;
+  const int64_t* step;  // device global_step (dropout key)
+  // outputs
+  float* prob;       // [B]
+  float* loss_rows;  // [B] (nullable)
+  float* g_out;      // [Bp] dL/dy
+  float* contrib;    // [B*F][Kp] per-lookup gradient rows (train)
+  uint16_t* actT[kMaxHidden + 1];  // [dims[a]][Bp] bf16, a = 0..nl (train)
+  uint16_t* dzT[kMaxHidden + 1];   // [dims[a]][Bp] bf16, a = 1..nl (train)
+  RowsLds lds;
+};
+
+struct WgradParams {
+  const uint16_t* actT[kMaxHidden + 1];
+  const uint16_t* dzT[kMaxHidden + 1];
+  const float* g;  // [Bp] dL/dy
+  int dims[kMaxHidden + 1];
+  int nl, Bp;
+  float* params;  // flat dense buffer
+  float* grads;   // flat grad buffer (fuse_opt == 0)
+  float* s0;
+  float* s1;
+  int offW[kMaxHidden], offb[kMaxHidden], off_wout, off_bout, off_fmb;
+  uint16_t* WT[kMaxHidden];
+  uint16_t* Wb[kMaxHidden];
+  int tile_start[kMaxHidden + 1];  // prefix sums of 32×32 tiles per layer
+  int bias_start[kMaxHidden + 1];  // prefix sums of 32-column bias blocks per layer
+  int fuse_opt;
+  OptParams opt;
+  const int64_t* step;
+  float grad_scale;
+};
+
+struct DenseApplyParams {
+  float* params;
+  const float* grads;
+  float* s0;
+  float* s1;
+  int n;
+  int nl;
+  int dims[kMaxHidden + 1];
+  int offW[kMaxHidden];
+  uint16_t* WT[kMaxHidden];
+  uint16_t* Wb[kMaxHidden];
+  int apply;
+  OptParams opt;
+  const int64_t* step;
+  float grad_scale;
+};
+
+}  // namespace rocfm

@@ -1,0 +1,47 @@
+// Parameter blocks of the embedding-update kernels (emb_update.hip).
+#pragma once
+#include "../common.h"
+#include "optim.h"
+
+namespace rocfm {
+
+struct EmbUpdateParams {
+  const uint32_t* skeys;  // [n] sorted ids
+  const uint32_t* svals;  // [n] lookup index into contrib
+  int n;
+  const float* contrib;  // [*][Kp]
+  int K1;                // real columns: K + 1 (fm_v row + fm_w)
+  int Kp;                // row stride (multiple of 4, <= 64)
+  float* emb;            // [V][Kp]
+  float* s0;
+  float* s1;
+  float l2;
+  float grad_scale;
+  OptParams opt;
+  const int64_t* step;
+  int mode;
+  float* dense_grad;   // mode 1: [V][Kp]
+  uint32_t* out_keys;  // mode 2
+  float* out_rows;     // mode 2: [cap][Kp]
+  int* out_count;      // mode 2
+  int id_offset;       // subtracted from keys before indexing emb (row-shard local index)
+  int id_stride;       // keys are mapped to local rows by (key - id_offset) / id_stride
+};
+
+struct EmbDenseParams {
+  float* emb;
+  float* s0;
+  float* s1;
+  float* dense_grad;
+  long long n4;  // number of float4 in the table
+  int Kp, K1;
+  float l2;
+  OptParams opt;
+  const int64_t* step;
+};
+
+void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream);
+void launch_emb_dense_update(EmbDenseParams p, hipStream_t stream);
+void launch_emb_sumsq(const float* emb, long long n4, int Kp, int K1, float* partial, int nblocks, hipStream_t stream);
+
+}  // namespace rocfm

@@ -1,0 +1,187 @@
+// MLP weight gradients (+ fused optimizer) and dense-parameter maintenance kernels.
+//
+// dW_l = h_lᵀ · dz_{l+1} reduces over the batch, the one cross-example reduction of the MLP.
+// The row kernel (deepfm_rows.hip) leaves h and dz transposed ([feature][batch], bf16), so both
+// MFMA operands are 16-B contiguous per lane:
+//   A[i][b] = actT[i][b], B[b][o] = dzT[o][b]  →  v_mfma_f32_32x32x16_bf16, f32 accumulate.
+// One workgroup owns one 32×32 tile of one layer's dW (no atomics, no split-K seam): its 4 waves
+// take a quarter of the batch each and combine through LDS; the tile's epilogue then applies the
+// optimizer to the f32 master weights and re-emits both bf16 copies (Wᵀ for the forward, W for
+// the backward) — single-GPU steps need no separate optimizer launch.  In data-parallel mode the
+// epilogue writes the gradient instead, RCCL all-reduces it, and dense_apply_kernel finishes.
+// Bias and output-layer gradients (Σ_b dz, hᵀ·g, Σ g) run in extra workgroups of the same grid.
+#include "deepfm_rows.h"
+
+namespace rocfm {
+
+namespace {
+
+__device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, int idx, float g) {
+  if (p.fuse_opt) {
+    float w = p.params[idx], a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
+    opt_apply(p.opt, st, w, g, a, b);
+    p.params[idx] = w;
+    if (p.s0) p.s0[idx] = a;
+    if (p.s1) p.s1[idx] = b;
+  } else {
+    p.grads[idx] = g;
+  }
+}
+
+__device__ __forceinline__ float sum_bf16x8(uint4 v) {
+  return bf2f(v.x & 0xffff) + bf2f(v.x >> 16) + bf2f(v.y & 0xffff) + bf2f(v.y >> 16) + bf2f(v.z & 0xffff) +
+         bf2f(v.z >> 16) + bf2f(v.w & 0xffff) + bf2f(v.w >> 16);
+}
+__device__ __forceinline__ float dot_bf16x8_f32(uint4 v, const float* g) {
+  return bf2f(v.x & 0xffff) * g[0] + bf2f(v.x >> 16) * g[1] + bf2f(v.y & 0xffff) * g[2] + bf2f(v.y >> 16) * g[3] +
+         bf2f(v.z & 0xffff) * g[4] + bf2f(v.z >> 16) * g[5] + bf2f(v.w & 0xffff) * g[6] + bf2f(v.w >> 16) * g[7];
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
+  __shared__ __attribute__((aligned(16))) float s_red[3 * 16 * 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int bid = blockIdx.x;
+  const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
+  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  const int Bp = p.Bp;
+
+  if (bid < n_tiles) {
+    int li = 0;
+    while (bid >= p.tile_start[li + 1]) ++li;
+    const int Din = p.dims[li], Dout = p.dims[li + 1];
+    const int local = bid - p.tile_start[li];
+    const int nto = Dout >> 5;
+    const int ti = local / nto, to = local % nto;
+    const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
+    const uint16_t* Bm = p.dzT[li + 1] + (size_t)(to * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
+    const int q = Bp >> 2;  // batch quarter per wave (Bp % 64 == 0)
+    f32x16 acc = {};
+    int b = wave * q;
+    const int be = b + q;
+#pragma unroll 4
+    for (; b < be; b += 16)
+      acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(A + b), *reinterpret_cast<const bf16x8*>(Bm + b), acc);
+    if (wave > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s_red[((wave - 1) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float g = (acc[r] + s_red[(0 * 16 + r) * 64 + lane] + s_red[(1 * 16 + r) * 64 + lane] +
+                         s_red[(2 * 16 + r) * 64 + lane]) *
+                        p.grad_scale;
+        const int i = ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int o = to * 32 + (lane & 31);
+        const int idx = p.offW[li] + i * Dout + o;
+        emit(p, st, idx, g);
+        if (p.fuse_opt) {
+          const uint16_t w = f2bf(p.params[idx]);
+          p.WT[li][(size_t)o * Din + i] = w;
+          p.Wb[li][(size_t)i * Dout + o] = w;
+        }
+      }
+    }
+    return;
+  }
+  if (bid < n_tiles + n_bias) {  // bias gradients: Σ_b dz[o][b] for 32 columns
+    const int lb = bid - n_tiles;
+    int li = 0;
+    while (lb >= p.bias_start[li + 1]) ++li;
+    const int cb = lb - p.bias_start[li];
+    const int o = cb * 32 + (t >> 3), sub = t & 7;
+    const uint16_t* row = p.dzT[li + 1] + (size_t)o * Bp;
+    float s = 0.f;
+    for (int b = sub * 8; b < Bp; b += 64) s += sum_bf16x8(*reinterpret_cast<const uint4*>(row + b));
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (sub == 0) emit(p, st, p.offb[li] + o, s * p.grad_scale);
+    return;
+  }
+  // output layer: dW_out[c] = Σ_b h[c][b]·g[b]; d b_out = d fm_bias = Σ_b g[b]
+  {
+    const int Dn = p.dims[p.nl];
+    const uint16_t* H = p.actT[p.nl];
+    for (int c0 = 0; c0 < Dn; c0 += 32) {
+      const int c = c0 + (t >> 3), sub = t & 7;
+      float s = 0.f;
+      if (c < Dn) {
+        const uint16_t* row = H + (size_t)c * Bp;
+        for (int b = sub * 8; b < Bp; b += 64) s += dot_bf16x8_f32(*reinterpret_cast<const uint4*>(row + b), p.g + b);
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (sub == 0 && c < Dn) emit(p, st, p.off_wout + c, s * p.grad_scale);
+    }
+    float s = 0.f;
+    for (int b = t; b < Bp; b += 256) s += p.g[b];
+    s = wave_sum(s);
+    if (lane == 0) s_red[wave] = s;
+    __syncthreads();
+    if (t == 0) {
+      const float tot = (s_red[0] + s_red[1] + s_red[2] + s_red[3]) * p.grad_scale;
+      emit(p, st, p.off_bout, tot);
+      emit(p, st, p.off_fmb, tot);
+    }
+  }
+}
+
+void launch_mlp_wgrad(WgradParams p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.Bp % 64 == 0, "mlp_wgrad: Bp must be a multiple of 64");
+  p.tile_start[0] = 0;
+  p.bias_start[0] = 0;
+  for (int l = 0; l < p.nl; ++l) {
+    ROCFM_REQUIRE(p.dims[l] % 32 == 0 && p.dims[l + 1] % 32 == 0, "mlp_wgrad: dims must be padded to 32");
+    p.tile_start[l + 1] = p.tile_start[l] + (p.dims[l] / 32) * (p.dims[l + 1] / 32);
+    p.bias_start[l + 1] = p.bias_start[l] + p.dims[l + 1] / 32;
+  }
+  for (int l = p.nl + 1; l <= kMaxHidden; ++l) {
+    p.tile_start[l] = p.tile_start[p.nl];
+    p.bias_start[l] = p.bias_start[p.nl];
+  }
+  const int grid = p.tile_start[p.nl] + p.bias_start[p.nl] + 1;
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(grid), dim3(256), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// dense_apply_kernel: elementwise optimizer over the flat dense buffer (after the DP all-reduce),
+// or (apply == 0) just refresh the bf16 weight copies from the f32 masters (init / restore).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dense_apply_kernel(const DenseApplyParams p) {
+  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < p.n; idx += gridDim.x * 256) {
+    float w = p.params[idx];
+    if (p.apply) {
+      float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
+      opt_apply(p.opt, st, w, p.grads[idx] * p.grad_scale, a, b);
+      p.params[idx] = w;
+      if (p.s0) p.s0[idx] = a;
+      if (p.s1) p.s1[idx] = b;
+    }
+    for (int l = 0; l < p.nl; ++l) {
+      const int sz = p.dims[l] * p.dims[l + 1];
+      if (idx >= p.offW[l] && idx < p.offW[l] + sz) {
+        const int k = idx - p.offW[l];
+        const int i = k / p.dims[l + 1], o = k % p.dims[l + 1];
+        const uint16_t h = f2bf(w);
+        p.WT[l][(size_t)o * p.dims[l] + i] = h;
+        p.Wb[l][(size_t)i * p.dims[l + 1] + o] = h;
+      }
+    }
+  }
+}
+
+void launch_dense_apply(DenseApplyParams p, hipStream_t stream) {
+  const int grid = std::min(cdiv(p.n, 256), 2048);
+  if (grid <= 0) return;
+  hipLaunchKernelGGL(dense_apply_kernel, dim3(grid), dim3(256), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rocfm

@@ -1,0 +1,69 @@
+// Device-side optimizer updates with the TF 1.x formulas of rocfm/optim/tf_optim.py
+// (reference: PS:292-307 / HVD:281-297).  One element at a time; callers vectorise.
+#pragma once
+#include "../common.h"
+
+namespace rocfm {
+
+enum OptType : int { kAdam = 0, kAdagrad = 1, kMomentum = 2, kFtrl = 3, kGD = 4 };
+
+struct OptParams {
+  int type = kAdam;
+  float lr = 5e-4f;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+  float momentum = 0.95f;
+  float ftrl_lr_power = -0.5f, ftrl_l1 = 0.f, ftrl_l2 = 0.f;
+};
+
+// Step-dependent scalars, computed once per thread from the device step counter (t = step+1).
+struct OptStep {
+  float lr_t;  // Adam: lr·√(1−β2ᵗ)/(1−β1ᵗ); others: lr
+};
+
+__device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
+  OptStep s;
+  if (o.type == kAdam) {
+    double t = (double)(step + 1);
+    s.lr_t = (float)((double)o.lr * sqrt(1.0 - pow((double)o.beta2, t)) / (1.0 - pow((double)o.beta1, t)));
+  } else {
+    s.lr_t = o.lr;
+  }
+  return s;
+}
+
+// In-place update of param p and slots s0/s1 with gradient g.
+__device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st, float& p, float g, float& s0,
+                                          float& s1) {
+  switch (o.type) {
+    case kAdam: {
+      s0 = o.beta1 * s0 + (1.f - o.beta1) * g;
+      s1 = o.beta2 * s1 + (1.f - o.beta2) * g * g;
+      p -= st.lr_t * s0 / (sqrtf(s1) + o.eps);
+      break;
+    }
+    case kAdagrad: {
+      s0 += g * g;
+      p -= o.lr * g * rsqrtf(s0);
+      break;
+    }
+    case kMomentum: {
+      s0 = o.momentum * s0 + g;
+      p -= o.lr * s0;
+      break;
+    }
+    case kFtrl: {
+      float pw = -o.ftrl_lr_power;
+      float acc_new = s0 + g * g;
+      float sigma = (powf(acc_new, pw) - powf(s0, pw)) / o.lr;
+      s1 += g - sigma * p;
+      float quad = powf(acc_new, pw) / o.lr + 2.f * o.ftrl_l2;
+      p = fabsf(s1) > o.ftrl_l1 ? (copysignf(o.ftrl_l1, s1) - s1) / quad : 0.f;
+      s0 = acc_new;
+      break;
+    }
+    default:
+      p -= o.lr * g;
+  }
+}
+
+}  // namespace rocfm

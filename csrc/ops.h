@@ -1,0 +1,34 @@
+// Host-side launch entry points of the rocfm HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "kernels/deepfm_rows.h"
+#include "kernels/emb_update.h"
+#include "kernels/optim.h"
+
+namespace rocfm {
+
+// probe.hip
+void launch_probe(float* out, int n, hipStream_t stream);
+
+// deepfm_rows.hip
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K);
+void launch_deepfm_rows(RowsParams p, hipStream_t stream);
+
+// mlp_wgrad.hip
+void launch_mlp_wgrad(WgradParams p, hipStream_t stream);
+void launch_dense_apply(DenseApplyParams p, hipStream_t stream);
+
+// emb_update.hip (declared in kernels/emb_update.h)
+
+// sort.hip
+size_t sort_pairs_temp_bytes(int n, int end_bit);
+void sort_pairs_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_out,
+                     int n, int end_bit, hipStream_t stream);
+size_t sort_pairs_vals_temp_bytes(int n, int end_bit);
+void sort_pairs_vals(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                     const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit, hipStream_t stream);
+
+}  // namespace rocfm

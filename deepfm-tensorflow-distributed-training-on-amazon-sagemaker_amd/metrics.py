@@ -1,0 +1,101 @@
+"""Evaluation metrics.
+
+* ``TFStreamingAUC``: the reference's ``tf.metrics.auc(labels, pred)`` (PS:282, HVD:271) —
+  ``num_thresholds=200``, thresholds ``[-1e-7, 1/199, …, 198/199, 1+1e-7]``, confusion counts
+  accumulated over batches, trapezoidal ROC area with the 1e-7 guards TF uses [ext].  The
+  accumulators are plain per-threshold counts, so ranks all-reduce them (fixes Q7: every rank
+  evaluates its shard and the counts are summed).
+* ``exact_auc``: rank-based ROC AUC (ties get average rank) — the unbiased number.
+* ``LossMean``: running mean of the per-batch loss, as Estimator.evaluate reports it.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+_EPS = 1e-7
+
+
+def tf_thresholds(num_thresholds: int = 200) -> np.ndarray:
+    t = [(i + 1) * 1.0 / (num_thresholds - 1) for i in range(num_thresholds - 2)]
+    return np.asarray([0.0 - _EPS] + t + [1.0 + _EPS], dtype=np.float64)
+
+
+class TFStreamingAUC:
+    def __init__(self, num_thresholds: int = 200):
+        self.thr = tf_thresholds(num_thresholds)
+        self.tp = np.zeros(num_thresholds, np.float64)
+        self.fp = np.zeros(num_thresholds, np.float64)
+        self.tn = np.zeros(num_thresholds, np.float64)
+        self.fn = np.zeros(num_thresholds, np.float64)
+
+    def update(self, labels, preds) -> None:
+        labels = _np(labels).astype(bool).reshape(-1)
+        preds = np.clip(_np(preds).astype(np.float64).reshape(-1), 0.0, 1.0)
+        # pred > thr counts via a sorted search: for each threshold, #preds strictly greater
+        pos = np.sort(preds[labels])
+        neg = np.sort(preds[~labels])
+        gt_pos = len(pos) - np.searchsorted(pos, self.thr, side="right")
+        gt_neg = len(neg) - np.searchsorted(neg, self.thr, side="right")
+        self.tp += gt_pos
+        self.fn += len(pos) - gt_pos
+        self.fp += gt_neg
+        self.tn += len(neg) - gt_neg
+
+    def state(self) -> np.ndarray:
+        return np.stack([self.tp, self.fp, self.tn, self.fn])
+
+    def load_state(self, s: np.ndarray) -> None:
+        self.tp, self.fp, self.tn, self.fn = [np.array(x, np.float64) for x in s]
+
+    def result(self) -> float:
+        tpr = (self.tp + _EPS) / (self.tp + self.fn + _EPS)
+        fpr = self.fp / (self.fp + self.tn + _EPS)
+        return float(np.sum((fpr[:-1] - fpr[1:]) * (tpr[:-1] + tpr[1:]) / 2.0))
+
+
+def exact_auc(labels, preds) -> float:
+    y = _np(labels).astype(bool).reshape(-1)
+    p = _np(preds).astype(np.float64).reshape(-1)
+    n_pos = int(y.sum())
+    n_neg = len(y) - n_pos
+    if n_pos == 0 or n_neg == 0:
+        return float("nan")
+    order = np.argsort(p, kind="mergesort")
+    ps = p[order]
+    ranks = np.empty(len(p), np.float64)
+    # average ranks for ties
+    i = 0
+    n = len(ps)
+    r = np.arange(1, n + 1, dtype=np.float64)
+    # vectorised tie handling
+    uniq, start, counts = np.unique(ps, return_index=True, return_counts=True)
+    avg = start + (counts + 1) / 2.0
+    ranks[order] = np.repeat(avg, counts)
+    del i, r, uniq
+    return float((ranks[y].sum() - n_pos * (n_pos + 1) / 2.0) / (n_pos * n_neg))
+
+
+def logloss(labels, preds, eps: float = 1e-7) -> float:
+    y = _np(labels).astype(np.float64).reshape(-1)
+    p = np.clip(_np(preds).astype(np.float64).reshape(-1), eps, 1 - eps)
+    return float(-np.mean(y * np.log(p) + (1 - y) * np.log(1 - p)))
+
+
+class LossMean:
+    def __init__(self):
+        self.total = 0.0
+        self.count = 0
+
+    def update(self, loss: float, n: int = 1) -> None:
+        self.total += float(loss) * n
+        self.count += n
+
+    def result(self) -> float:
+        return self.total / max(self.count, 1)
+
+
+def _np(x) -> np.ndarray:
+    if isinstance(x, torch.Tensor):
+        return x.detach().float().cpu().numpy()
+    return np.asarray(x)

@@ -1,0 +1,432 @@
+"""Fused MI355X training engine for DeepFM (the HIP path).
+
+One training step on one GPU is four kernels (plus a step-counter bump), captured once into a HIP
+graph and replayed:
+
+    side stream : sort_pairs      — radix sort of the batch's (id, lookup) pairs (sort.hip)
+    main stream : deepfm_rows     — gather + FM + MLP fwd + head + MLP bwd + FM bwd (deepfm_rows.hip)
+                  mlp_wgrad       — dW/db on MFMA + fused optimizer + bf16 weight refresh (mlp_wgrad.hip)
+                  emb_rows_update — sorted segment-sum of lookup grads + row optimizer (emb_update.hip)
+
+which replaces the reference's per-step TF graph (PS:172-313 ≡ HVD:164-303 forward/backward +
+ApplyAdam ×11 variables).  ``embedding_update='exact'`` keeps the reference semantics of the
+full-table L2 (dense gradient, every row's optimizer slots move every step) by
+writing the summed lookup gradients into a dense table and running one dense update kernel.
+
+State layout (device):
+  emb   [V, Kp] f32 — fm_v in columns 0..K-1, fm_w in column K, zero padding (Kp = 4·⌈(K+1)/4⌉)
+  dense [P] f32     — MLP weights/biases (dims padded to 32), deep_out, fm_bias (DenseLayout)
+  WT/Wb             — bf16 copies of each hidden layer's W (forward / backward MFMA operands)
+  slots             — optimizer state with the same layouts (Adam m,v; Adagrad acc; …)
+  step  [1] int64   — global_step, read by the kernels (Adam bias correction, dropout keys)
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import torch
+
+from ..optim import OPT_ID, OptHParams, init_slots, slot_names
+from ..ops import require_hip
+from .deepfm import ModelSpec, init_params, mlp_names
+
+
+def _r32(x: int) -> int:
+    return (x + 31) // 32 * 32
+
+
+class DenseLayout:
+    """Flat f32 layout of every non-embedding parameter."""
+
+    def __init__(self, spec: ModelSpec):
+        self.spec = spec
+        real = [spec.deep_in] + list(spec.layers)
+        self.real = real
+        self.dims = [_r32(d) for d in real]
+        self.nl = len(spec.layers)
+        off = 0
+        self.offW, self.offb = [], []
+        for l in range(self.nl):
+            self.offW.append(off)
+            off += self.dims[l] * self.dims[l + 1]
+            self.offb.append(off)
+            off += self.dims[l + 1]
+        self.off_wout = off
+        off += self.dims[self.nl]
+        self.off_bout = off
+        off += 1
+        self.off_fmb = off
+        off += 1
+        self.total = (off + 3) // 4 * 4
+
+    def views(self, flat: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+        """TF-named views (unpadded) into a flat buffer (params or any slot)."""
+        v: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        v["fm_bias"] = flat[self.off_fmb:self.off_fmb + 1]
+        for l, (wn, bn) in enumerate(mlp_names(self.spec)[:-1]):
+            W = flat[self.offW[l]:self.offW[l] + self.dims[l] * self.dims[l + 1]].view(self.dims[l], self.dims[l + 1])
+            v[wn] = W[: self.real[l], : self.real[l + 1]]
+            v[bn] = flat[self.offb[l]:self.offb[l] + self.real[l + 1]]
+        wn, bn = mlp_names(self.spec)[-1]
+        v[wn] = flat[self.off_wout:self.off_wout + self.real[self.nl]].view(-1, 1)
+        v[bn] = flat[self.off_bout:self.off_bout + 1]
+        return v
+
+    def pack(self, P: Dict[str, torch.Tensor], flat: torch.Tensor) -> None:
+        flat.zero_()
+        for name, view in self.views(flat).items():
+            view.copy_(P[name].reshape(view.shape))
+
+
+class FusedDeepFM:
+    """Device-resident DeepFM state + the fused HIP training/inference steps for one GPU."""
+
+    def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device="cuda",
+                 embedding_update: str = "sparse", seed: int = 1234,
+                 params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
+                 use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None):
+        if spec.batch_norm:
+            raise ValueError("the fused engine does not implement batch_norm; use engine=torch")
+        if len(spec.layers) > 6:
+            raise ValueError("the fused engine supports at most 6 hidden layers")
+        self.H = require_hip()
+        self.spec, self.hp = spec, hp
+        self.device = torch.device(device)
+        self.B = int(batch_size)
+        self.Bp = (self.B + 63) // 64 * 64
+        self.F, self.K = spec.field_size, spec.embedding_size
+        self.K1 = self.K + 1
+        self.Kp = (self.K1 + 3) // 4 * 4
+        if self.Kp > 64:
+            raise ValueError("embedding_size must be <= 63 for the fused engine")
+        self.V = spec.feature_size
+        self.layout = DenseLayout(spec)
+        self.embedding_update = embedding_update
+        self.grad_scale = float(grad_scale)
+        self.use_graph = use_graph
+        self.fuse_dense_opt = fuse_dense_opt
+        self.seed = int(seed if dropout_seed is None else dropout_seed)
+        self.loss_code = 0 if spec.loss_type == "log_loss" else 1
+        dev = self.device
+        L = self.layout
+
+        # ---- parameters + optimizer state ----------------------------------------------------
+        P = params if params is not None else init_params(spec, seed)
+        self.emb = torch.zeros(self.V, self.Kp, dtype=torch.float32, device=dev)
+        self.emb[:, : self.K].copy_(P["fm_v"])
+        self.emb[:, self.K].copy_(P["fm_w"])
+        self.dense = torch.zeros(L.total, dtype=torch.float32, device=dev)
+        L.pack({k: v.to(dev) for k, v in P.items()}, self.dense)
+        self.emb_slots = self._make_slots(self.emb, real_cols=self.K1)
+        self.dense_slots = self._make_slots(self.dense)
+        self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
+        self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        # ---- static step buffers --------------------------------------------------------------
+        B, Bp, F = self.B, self.Bp, self.F
+        self.ids_buf = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
+        self.vals_buf = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
+        self.labels_buf = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.prob = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.loss_rows = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.contrib = torch.zeros(B * F, self.Kp, dtype=torch.float32, device=dev)
+        self.actT = [torch.zeros(L.dims[a], Bp, dtype=torch.bfloat16, device=dev) for a in range(L.nl + 1)]
+        self.dzT = [torch.zeros(L.dims[a], Bp, dtype=torch.bfloat16, device=dev) if a > 0 else None
+                    for a in range(L.nl + 1)]
+        self.n_lookup = B * F
+        self.end_bit = max(1, math.ceil(math.log2(max(self.V, 2))))
+        self.skeys = torch.zeros(self.n_lookup, dtype=torch.int32, device=dev)
+        self.svals = torch.zeros(self.n_lookup, dtype=torch.int32, device=dev)
+        tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
+        self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
+        self.dense_grad = (torch.zeros_like(self.emb) if embedding_update == "exact" else None)
+        self.dense_grads_flat = torch.zeros(L.total, dtype=torch.float32, device=dev)
+        self.sort_stream = torch.cuda.Stream(device=dev) if self.device.type == "cuda" else None
+
+        self._build_params()
+        self.refresh_bf16()
+        self._graph = None
+        self._graph_warm = 0
+
+    # ------------------------------------------------------------------------------------------
+    def _make_slots(self, t: torch.Tensor, real_cols: Optional[int] = None) -> List[torch.Tensor]:
+        hp = self.hp
+        slots = init_slots(hp, t)
+        if real_cols is not None:  # pad columns stay exactly 0 / init so they never move
+            pass
+        return slots
+
+    def _opt(self, lr_scale: float = 1.0):
+        o = self.H.OptParams()
+        hp = self.hp
+        o.type = OPT_ID[hp.name]
+        o.lr = hp.lr * lr_scale
+        o.beta1, o.beta2, o.eps = hp.beta1, hp.beta2, hp.eps
+        o.momentum = hp.momentum
+        o.ftrl_lr_power, o.ftrl_l1, o.ftrl_l2 = hp.ftrl_lr_power, hp.ftrl_l1, hp.ftrl_l2
+        return o
+
+    def _slot_ptrs(self, slots):
+        s0 = slots[0].data_ptr() if len(slots) > 0 else 0
+        s1 = slots[1].data_ptr() if len(slots) > 1 else 0
+        return s0, s1
+
+    def _build_params(self):
+        H, L = self.H, self.layout
+        dense_views = L.views(self.dense)
+        # row kernel
+        rp = H.RowsParams()
+        rp.ids, rp.vals, rp.labels = self.ids_buf.data_ptr(), self.vals_buf.data_ptr(), self.labels_buf.data_ptr()
+        rp.emb = self.emb.data_ptr()
+        rp.fm_bias = dense_views["fm_bias"].data_ptr()
+        rp.w_out = self.dense[L.off_wout:].data_ptr()
+        rp.b_out = self.dense[L.off_bout:].data_ptr()
+        rp.step = self.step.data_ptr()
+        rp.prob, rp.loss_rows, rp.g_out = self.prob.data_ptr(), self.loss_rows.data_ptr(), self.g.data_ptr()
+        rp.contrib = self.contrib.data_ptr()
+        rp.nl, rp.F, rp.K, rp.Kp, rp.B, rp.Bp = L.nl, self.F, self.K, self.Kp, self.B, self.Bp
+        rp.inv_scale = 1.0 / self.B
+        rp.train = 1
+        rp.loss_type = self.loss_code
+        rp.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+        rp.set_dims(L.dims)
+        for l in range(L.nl):
+            rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),
+                         float(self.spec.keep_probs[l]))
+        for a in range(L.nl + 1):
+            rp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
+        self.rows_params = rp
+        if rp.lds_bytes() > 160 * 1024:
+            raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
+        # weight-gradient kernel
+        wp = H.WgradParams()
+        wp.g = self.g.data_ptr()
+        wp.params = self.dense.data_ptr()
+        wp.grads = self.dense_grads_flat.data_ptr()
+        wp.s0, wp.s1 = self._slot_ptrs(self.dense_slots)
+        wp.step = self.step.data_ptr()
+        wp.nl, wp.Bp = L.nl, self.Bp
+        wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
+        wp.fuse_opt = 1 if self.fuse_dense_opt else 0
+        wp.opt = self._opt()
+        wp.grad_scale = 1.0
+        wp.set_dims(L.dims)
+        for a in range(L.nl + 1):
+            wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
+        for l in range(L.nl):
+            wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+        self.wgrad_params = wp
+        # dense apply (DP path / bf16 refresh)
+        dp = H.DenseApplyParams()
+        dp.params = self.dense.data_ptr()
+        dp.grads = self.dense_grads_flat.data_ptr()
+        dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
+        dp.step = self.step.data_ptr()
+        dp.n, dp.nl = L.total, L.nl
+        dp.opt = self._opt()
+        dp.set_dims(L.dims)
+        for l in range(L.nl):
+            dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+        self.dense_apply_params = dp
+        # embedding update
+        ep = H.EmbUpdateParams()
+        ep.skeys, ep.svals = self.skeys.data_ptr(), self.svals.data_ptr()
+        ep.n = self.n_lookup
+        ep.contrib = self.contrib.data_ptr()
+        ep.K1, ep.Kp = self.K1, self.Kp
+        ep.emb = self.emb.data_ptr()
+        ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
+        ep.l2 = float(self.spec.l2_reg)
+        ep.grad_scale = 1.0
+        ep.opt = self._opt()
+        ep.step = self.step.data_ptr()
+        ep.mode = 1 if self.embedding_update == "exact" else 0
+        if self.dense_grad is not None:
+            ep.dense_grad = self.dense_grad.data_ptr()
+        self.emb_params = ep
+        if self.embedding_update == "exact":
+            ed = H.EmbDenseParams()
+            ed.emb = self.emb.data_ptr()
+            ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
+            ed.dense_grad = self.dense_grad.data_ptr()
+            ed.step = self.step.data_ptr()
+            ed.n4 = self.V * self.Kp // 4
+            ed.Kp, ed.K1 = self.Kp, self.K1
+            ed.l2 = float(self.spec.l2_reg)
+            ed.opt = self._opt()
+            self.emb_dense_params = ed
+
+    def set_lr_scale(self, s: float) -> None:
+        """Multiply the learning rate (Horovod's lr × world size, HVD:171)."""
+        o = self._opt(s)
+        self.wgrad_params.opt = o
+        self.dense_apply_params.opt = o
+        self.emb_params.opt = o
+        if self.embedding_update == "exact":
+            self.emb_dense_params.opt = o
+        self._graph = None
+
+    # ------------------------------------------------------------------------------------------
+    @property
+    def stream_ptr(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def refresh_bf16(self) -> None:
+        dp = self.dense_apply_params
+        dp.apply = 0
+        self.H.dense_apply(dp, self.stream_ptr)
+
+    def load_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None) -> None:
+        """Copy a batch into the static (graph-bound) input buffers (async on the current stream)."""
+        n = ids.shape[0]
+        if n != self.B:
+            raise ValueError(f"batch has {n} rows, engine built for {self.B} (drop_remainder semantics)")
+        self.ids_buf[:n].copy_(ids, non_blocking=True)
+        self.vals_buf[:n].copy_(vals, non_blocking=True)
+        if labels is not None:
+            self.labels_buf[:n].copy_(labels, non_blocking=True)
+
+    # ---- the step ------------------------------------------------------------------------------
+    def _enqueue_sort(self):
+        main = torch.cuda.current_stream(self.device)
+        side = self.sort_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.ids_buf.data_ptr(),
+                                   self.skeys.data_ptr(), self.svals.data_ptr(), self.n_lookup, self.end_bit,
+                                   side.cuda_stream)
+        return side
+
+    def _enqueue_forward_backward(self):
+        """rows kernel + (fused or grad-only) wgrad; embedding not yet updated."""
+        s = self.stream_ptr
+        self.rows_params.train = 1
+        self.H.deepfm_rows(self.rows_params, s)
+        self.H.mlp_wgrad(self.wgrad_params, s)
+
+    def _enqueue_emb_update(self, side):
+        main = torch.cuda.current_stream(self.device)
+        main.wait_stream(side)
+        s = self.stream_ptr
+        self.H.emb_rows_update(self.emb_params, s)
+        if self.embedding_update == "exact":
+            self.H.emb_dense_update(self.emb_dense_params, s)
+
+    def _enqueue_step(self):
+        side = self._enqueue_sort()
+        self._enqueue_forward_backward()
+        self._enqueue_emb_update(side)
+        self.step.add_(1)
+
+    def train_step(self) -> None:
+        """One optimisation step on the batch in the static buffers (asynchronous)."""
+        if not self.fuse_dense_opt:
+            raise RuntimeError("train_step() is the single-GPU step; distributed steps live in rocfm.parallel")
+        if not self.use_graph:
+            self._enqueue_step()
+            return
+        if self._graph is None:
+            if self._graph_warm < 2:  # warm up eagerly (allocator, kernel attributes) before capture
+                self._graph_warm += 1
+                self._enqueue_step()
+                return
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(g):
+                self._enqueue_step()
+            self._graph = g
+            # capture recorded the kernels but did not run them
+        self._graph.replay()
+
+    # ---- inference -----------------------------------------------------------------------------
+    @torch.no_grad()
+    def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
+        """Probabilities (and per-row losses) for up to B rows; no dropout, no update."""
+        n = ids.shape[0]
+        if n > self.B:
+            out = [self.predict_batch(ids[i:i + self.B], vals[i:i + self.B],
+                                      None if labels is None else labels[i:i + self.B]) for i in range(0, n, self.B)]
+            return torch.cat([o[0] for o in out]), torch.cat([o[1] for o in out])
+        self.ids_buf[:n].copy_(ids)
+        self.vals_buf[:n].copy_(vals)
+        if labels is not None:
+            self.labels_buf[:n].copy_(labels)
+        else:
+            self.labels_buf.zero_()
+        rp = self.rows_params
+        rp.train = 0
+        saved_B = rp.B
+        rp.B = n
+        self.H.deepfm_rows(rp, self.stream_ptr)
+        rp.B = saved_B
+        rp.train = 1
+        return self.prob[:n].clone(), self.loss_rows[:n].clone()
+
+    # ---- state ----------------------------------------------------------------------------------
+    def l2_value(self) -> float:
+        """λ·(l2_loss(fm_w) + l2_loss(fm_v)) — evaluated on demand (the full-table term of PS:277-278)."""
+        nb = 1024
+        part = torch.zeros(nb, dtype=torch.float32, device=self.device)
+        self.H.emb_sumsq(self.emb.data_ptr(), self.V * self.Kp // 4, self.Kp, self.K1, part.data_ptr(), nb,
+                         self.stream_ptr)
+        return float(self.spec.l2_reg * 0.5 * part.double().sum().item())
+
+    def batch_loss(self, include_l2: bool = True) -> float:
+        loss = float(self.loss_rows[: self.B].double().mean().item())
+        return loss + (self.l2_value() if include_l2 else 0.0)
+
+    def global_step(self) -> int:
+        return int(self.step.item())
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """TF-named variables + optimizer slots + global_step (CPU tensors)."""
+        sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        tf = self._tf_views(self.emb, self.dense)
+        for k, v in tf.items():
+            sd[k] = v.detach().cpu().clone()
+        names = slot_names(self.hp.name)
+        for si, sn in enumerate(names):
+            sv = self._tf_views(self.emb_slots[si], self.dense_slots[si])
+            for k, v in sv.items():
+                sd[f"{k}/{sn}"] = v.detach().cpu().clone()
+        step = self.global_step()
+        sd["global_step"] = torch.tensor(step, dtype=torch.int64)
+        if self.hp.name == "Adam":
+            sd["beta1_power"] = torch.tensor(self.hp.beta1 ** (step + 1), dtype=torch.float32)
+            sd["beta2_power"] = torch.tensor(self.hp.beta2 ** (step + 1), dtype=torch.float32)
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        with torch.no_grad():
+            self._load_views(sd, "", self.emb, self.dense, strict)
+            for si, sn in enumerate(slot_names(self.hp.name)):
+                self._load_views(sd, "/" + sn, self.emb_slots[si], self.dense_slots[si], strict)
+            if "global_step" in sd:
+                self.step.fill_(int(sd["global_step"]))
+        self.refresh_bf16()
+        self._graph = None
+
+    def _tf_views(self, emb_like: torch.Tensor, dense_like: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+        v: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        dv = self.layout.views(dense_like)
+        v["fm_bias"] = dv.pop("fm_bias")
+        v["fm_w"] = emb_like[:, self.K]
+        v["fm_v"] = emb_like[:, : self.K]
+        v.update(dv)
+        return v
+
+    def _load_views(self, sd, suffix, emb_like, dense_like, strict):
+        for k, view in self._tf_views(emb_like, dense_like).items():
+            key = k + suffix
+            if key not in sd:
+                if strict:
+                    raise KeyError(f"checkpoint is missing {key}")
+                continue
+            view.copy_(sd[key].to(view.device).reshape(view.shape))
+
+    def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
+        return OrderedDict((k, v.detach().cpu().clone()) for k, v in self._tf_views(self.emb, self.dense).items())

@@ -1,0 +1,120 @@
+"""Pure-PyTorch/numpy references of the HIP kernels.
+
+Every HIP kernel has an oracle here with the *same* numerics contract (where the kernel rounds to
+bf16, the oracle rounds at the same point), so kernel tests compare against a plain fp32
+PyTorch computation of the same op:
+
+* ``philox4x32_10`` / ``dropout_masks`` — bit-exact replica of ``dropout_bits`` in csrc/common.h
+* ``fused_step_reference`` — deepfm_rows.hip + mlp_wgrad.hip (forward, head, backward, dW/db)
+* ``emb_grad_reference`` — sort + emb_update.hip aggregation (Σ per unique id)
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = 0x9E3779B9, 0xBB67AE85
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
+    """Philox4x32-10 on uint64 numpy arrays holding 32-bit values (vectorised)."""
+    c0, c1, c2, c3 = (np.asarray(x, np.uint64) & MASK32 for x in (c0, c1, c2, c3))
+    k0 = np.uint64(k0 & 0xFFFFFFFF)
+    k1 = np.uint64(k1 & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & MASK32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & MASK32, lo1, (hi0 ^ c3 ^ k1) & MASK32, lo0
+        k0 = (k0 + np.uint64(W0)) & MASK32
+        k1 = (k1 + np.uint64(W1)) & MASK32
+    return c0, c1, c2, c3
+
+
+def dropout_masks(seed: int, layer: int, step: int, rows: int, cols: int, keep: float) -> torch.Tensor:
+    """Keep mask [rows, cols] (bool) exactly as deepfm_rows.hip draws it."""
+    assert rows % 4 == 0
+    rg = np.repeat(np.arange(rows // 4, dtype=np.uint64), cols)
+    cc = np.tile(np.arange(cols, dtype=np.uint64), rows // 4)
+    x, y, z, w = philox4x32_10(rg, cc, np.uint64(layer), np.uint64(step & 0xFFFFFFFF), seed & 0xFFFFFFFF,
+                               (seed >> 32) & 0xFFFFFFFF)
+    lanes = np.stack([x, y, z, w], axis=1).reshape(rows // 4, cols, 4)  # [rg, col, lane]
+    u = (lanes >> np.uint64(8)).astype(np.float64) / 16777216.0
+    keepm = (u.astype(np.float32) < np.float32(keep))
+    return torch.from_numpy(np.ascontiguousarray(keepm.transpose(0, 2, 1).reshape(rows, cols)))
+
+
+def bf16(x: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 (RNE) and back to f32."""
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]], w_out: torch.Tensor,
+                         b_out: float, fm_bias: float, ids: torch.Tensor, vals: torch.Tensor,
+                         labels: torch.Tensor, K: int, keeps: List[float], masks: Optional[List[torch.Tensor]],
+                         inv_scale: float, train: bool = True, loss_type: int = 0):
+    """Forward + backward with the fused kernels' numerics, on unpadded shapes.
+
+    ``emb`` [V, Kp] (cols 0..K-1 fm_v, col K fm_w); ``layers[l]`` = {W [in,out] f32, b [out]}.
+    Returns dict with prob, loss_rows, g, contrib [B*F, K+1], dW/db per layer, dw_out, d_bout.
+    """
+    B, F = ids.shape
+    rows = emb[ids.long()]  # [B,F,Kp]
+    V = rows[..., :K]
+    w = rows[..., K]
+    x = vals
+    e = V * x.unsqueeze(-1)
+    S = e.sum(1)
+    y_lin = fm_bias + (w * x).sum(1) + 0.5 * (S * S - (e * e).sum(1)).sum(1)
+    h = [bf16(e.reshape(B, F * K))]
+    for li, L in enumerate(layers):
+        z = h[-1] @ bf16(L["W"]) + L["b"]
+        a = torch.relu(z)
+        if train and keeps[li] < 1.0:
+            a = torch.where(masks[li], a / keeps[li], torch.zeros_like(a))
+        h.append(bf16(a))
+    y = y_lin + h[-1] @ w_out + b_out
+    p = torch.sigmoid(y)
+    if loss_type == 0:
+        loss = torch.clamp(y, min=0) - y * labels + torch.log1p(torch.exp(-y.abs()))
+        g = (p - labels) * inv_scale
+    else:
+        loss = (p - labels) ** 2
+        g = 2 * (p - labels) * p * (1 - p) * inv_scale
+    out = {"prob": p, "loss_rows": loss, "g": g, "y": y}
+    if not train:
+        return out
+    nl = len(layers)
+    dz = [None] * (nl + 1)
+    dz[nl] = bf16(torch.where(h[nl] > 0, g[:, None] * w_out[None, :] / keeps[nl - 1], torch.zeros_like(h[nl])))
+    dh0 = None
+    for a in range(nl, 0, -1):
+        dh = dz[a] @ bf16(layers[a - 1]["W"]).t()
+        if a - 1 >= 1:
+            dz[a - 1] = bf16(torch.where(h[a - 1] > 0, dh / keeps[a - 2], torch.zeros_like(dh)))
+        else:
+            dh0 = dh
+    de = g[:, None, None] * (S[:, None, :] - e) + dh0.reshape(B, F, K)
+    contrib = torch.cat([x.unsqueeze(-1) * de, (g[:, None] * x).unsqueeze(-1)], dim=-1).reshape(B * F, K + 1)
+    out["contrib"] = contrib
+    out["dW"] = [h[a].t() @ dz[a + 1] for a in range(nl)]
+    out["db"] = [dz[a + 1].sum(0) for a in range(nl)]
+    out["dw_out"] = h[nl].t() @ g
+    out["d_bout"] = g.sum()
+    out["h"] = h
+    out["dz"] = dz
+    return out
+
+
+def emb_grad_reference(ids: torch.Tensor, contrib: torch.Tensor):
+    """Σ of per-lookup gradient rows per unique id → (unique ids, summed rows)."""
+    flat = ids.reshape(-1).long()
+    uniq, inv = torch.unique(flat, return_inverse=True)
+    acc = torch.zeros(len(uniq), contrib.shape[1], dtype=contrib.dtype)
+    acc.index_add_(0, inv, contrib)
+    return uniq, acc
