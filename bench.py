@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""rocfm benchmark: DeepFM training throughput (examples/sec, whole job) on 1..8 MI355X.
+
+Config (BASELINE.json config 2/3): DeepFM on Criteo-shape data — 39 fields (13 numeric with fixed
+ids + 26 categorical), 1M-row hashed vocabulary, embedding_size k=10, deep_layers 128,64,32,
+dropout keep 0.5, Adam lr 5e-4 (× world size, HVD:171), l2 1e-4, per-GPU batch 1024 (the
+reference's per-worker batch, NB-HVD:96), bf16 MFMA MLP with f32 master weights.  Weak scaling:
+every rank trains its own 1024-example batches; N>1 runs one process per GPU over RCCL.
+
+Data is synthetic (rocfm.data.synthetic: Zipf ids with the bundled data's field layout),
+generated once into an HBM-resident pool of batches; each timed step copies its batch into the
+engine's input buffers and runs a FULL optimisation step (forward, backward, MLP + embedding
+optimizer, cross-rank exchange).  Weights are random-init (TF initialisers).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--engine fused|torch]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "examples/sec (whole node) DeepFM Criteo-39-field at 1/2/4/8 MI355X"
+# PyTorch-eager (engine=torch, same semantics, same shapes) measured on one MI355X; see BASELINE.md.
+EAGER_BASELINE = {"sparse": None, "exact": None}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch_size", type=int, default=1024, help="per-GPU batch")
+    ap.add_argument("--feature_size", type=int, default=1_000_000)
+    ap.add_argument("--field_size", type=int, default=39)
+    ap.add_argument("--embedding_size", type=int, default=10)
+    ap.add_argument("--deep_layers", default="128,64,32")
+    ap.add_argument("--dropout", default="0.5,0.5,0.5")
+    ap.add_argument("--optimizer", default="Adam")
+    ap.add_argument("--learning_rate", type=float, default=0.0005)
+    ap.add_argument("--l2_reg", type=float, default=0.0001)
+    ap.add_argument("--engine", default="fused", choices=["fused", "torch"])
+    ap.add_argument("--embedding_update", default="sparse", choices=["sparse", "exact"])
+    ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
+    ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
+    ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--json_out", default="")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus > 1 and world == 1:
+        # re-launch under torch.distributed.run (exec before touching the GPU)
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000), __file__] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rocfm.data.synthetic import SyntheticCriteo
+    from rocfm.models.deepfm import ModelSpec, init_params
+    from rocfm.optim import OptHParams
+
+    layers = [int(x) for x in a.deep_layers.split(",")]
+    keeps = [float(x) for x in a.dropout.split(",")]
+    spec = ModelSpec(a.feature_size, a.field_size, a.embedding_size, layers, keeps, l2_reg=a.l2_reg)
+    hp = OptHParams(name=a.optimizer, lr=a.learning_rate)
+    params = init_params(spec, a.seed)  # identical on every rank (= rank-0 broadcast, HVD:418)
+
+    B = a.batch_size
+    gen = SyntheticCriteo(a.feature_size, a.field_size, seed=a.seed)
+    g = torch.Generator(device=dev).manual_seed(a.seed * 1000 + rank)
+    pool = [gen.batch(B, dev, g) for _ in range(a.pool)]
+    pool_ids = torch.stack([x[0] for x in pool])
+    pool_vals = torch.stack([x[1] for x in pool])
+    pool_labels = torch.stack([x[2] for x in pool])
+
+    parallelism = a.parallelism
+    if parallelism == "auto":
+        parallelism = "dp" if a.embedding_update == "sparse" else "dense_dp"
+    if a.engine == "fused":
+        if world > 1:
+            from rocfm.parallel.dp import FusedDataParallel
+
+            eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
+                                    mode=parallelism, seed=a.seed, use_graph=not a.no_graph)
+        else:
+            from rocfm.models.fused import FusedDeepFM
+
+            eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
+                              use_graph=not a.no_graph)
+
+        eng.attach_pool(pool_ids, pool_vals, pool_labels)
+
+        def step(i):
+            eng.train_step()
+    else:
+        from rocfm.models.torch_engine import TorchDeepFM
+
+        eng = TorchDeepFM(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
+        if world > 1:
+            from rocfm.parallel.dp import attach_torch_dp
+
+            attach_torch_dp(eng, a.embedding_update)
+
+        def step(i):
+            ids, vals, labels = pool[i % len(pool)]
+            eng.train_step(ids, vals, labels)
+
+    if world > 1 and hasattr(eng, "set_lr_scale"):
+        eng.set_lr_scale(float(world))  # Horovod linear LR scaling (HVD:171)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt / a.steps * 1e3
+    value = B * world * a.steps / dt
+    base = EAGER_BASELINE.get(a.embedding_update)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "examples/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / (base * world), 3) if base else None),
+        "dtype": "bf16",
+        "data": "synthetic Criteo-shape (39 fields, Zipf ids, HBM-resident batch pool), random-init weights",
+        "config": {
+            "model": f"DeepFM Criteo-shape (39 fields, {a.feature_size // 1000}K-hash vocab, k={a.embedding_size}, "
+                     f"mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
+            "global_batch": B * world,
+            "seq_len": a.field_size,
+            "parallelism": f"{parallelism}{world}" if world > 1 else "dp1",
+            "engine": a.engine,
+            "embedding_update": a.embedding_update,
+        },
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

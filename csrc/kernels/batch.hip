@@ -1,0 +1,49 @@
+// Batch fetch for graph-replayed steps: copy batch (cursor + advance) of a device-resident pool
+// ([NB][B][F] ids/values, [NB][B] labels — an HBM-resident dataset or the loader's staging ring)
+// into a static input slot, and publish the next step's cursor / global_step.
+//
+// The engine double-buffers everything a step reads (input slot, sorted keys, cursor, step) by
+// step parity, so this kernel runs on a side stream one step AHEAD of the compute (it fetches and
+// the sort orders batch i+1 while step i trains) and never writes a word the concurrent step
+// reads: it reads cursor[p]/step[p] and writes cursor[1-p]/step[1-p].
+#include "batch.h"
+
+namespace rocfm {
+
+__global__ __launch_bounds__(256) void fetch_batch_kernel(const FetchParams p) {
+  const long long nb = p.pool_batches;
+  long long b = (*p.cur_src + p.advance) % nb;
+  if (b < 0) b += nb;
+  const long long n = (long long)p.B * p.F;
+  const int4* si = reinterpret_cast<const int4*>(p.ids_pool + b * n);
+  const int4* sv = reinterpret_cast<const int4*>(p.vals_pool + b * n);
+  int4* di = reinterpret_cast<int4*>(p.ids);
+  int4* dv = reinterpret_cast<int4*>(p.vals);
+  const long long n4 = (n & 3) ? 0 : (n >> 2);  // vector path only when every batch is 16-B aligned
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    di[i] = si[i];
+    dv[i] = sv[i];
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    p.ids[i] = p.ids_pool[b * n + i];
+    p.vals[i] = p.vals_pool[b * n + i];
+  }
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.B; i += (long long)gridDim.x * 256)
+    p.labels[i] = p.labels_pool[b * p.B + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (p.cur_dst) *p.cur_dst = *p.cur_src + p.advance;
+    if (p.step_dst) *p.step_dst = *p.step_src + p.step_advance;
+  }
+}
+
+void launch_fetch_batch(const FetchParams& p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.pool_batches > 0, "fetch_batch: empty pool");
+  ROCFM_REQUIRE(p.cur_dst != p.cur_src && (p.step_dst == nullptr || p.step_dst != p.step_src),
+                "fetch_batch: source and destination counters must differ");
+  const long long n4 = (long long)p.B * p.F / 4;
+  const int grid = (int)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, 256));
+  hipLaunchKernelGGL(fetch_batch_kernel, dim3(grid), dim3(256), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rocfm

@@ -25,6 +25,45 @@ __device__ __forceinline__ uint32_t pick4(const Philox4& b, int i) {
   return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
 }
 
+// acc[j] = A(16 × Kd, LDS bf16, row stride lda) · B(Kd × 16) for the n-tiles nt = nt0 + 4j (j < NTW)
+// owned by this wave.  B fragments come from global/L2: tile nt, k-step ks at
+// Bt + (nt*16 + (lane&15))*ldb + ks + 8*(lane>>4).  Latency-oriented: every batch issues KU k-steps
+// × NTW tiles of 16-B loads before the first MFMA; out-of-range k-steps load a clamped (valid)
+// address and are zeroed on the VALUE (no per-load predication — cdna guide §5 trap (c)).
+template <int NTW, int KU>
+__device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const uint16_t* Bt, int ldb, int ntiles,
+                                             int nt0, int Kd, int lane, f32x4 (&acc)[NTW]) {
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
+  const uint16_t* bp[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = min(nt0 + 4 * j, ntiles - 1);
+    bp[j] = Bt + (size_t)(nt * 16 + (lane & 15)) * ldb + 8 * (lane >> 4);
+  }
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k0 = 0; k0 < Kd; k0 += 32 * KU) {
+    bf16x8 a[KU], b[NTW][KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int ks = min(k0 + 32 * u, Kd - 32);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) b[j][u] = ld_frag(bp[j] + ks);
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int ks = min(k0 + 32 * u, Kd - 32);
+      a[u] = (k0 + 32 * u < Kd) ? ld_frag(ap + ks) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        if (nt0 + 4 * j < ntiles) acc[j] = mfma16x16x32(a[u], b[j][u], acc[j]);
+  }
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
@@ -54,32 +93,45 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   __syncthreads();
 
   // ---- phase A: gather rows, e = V·x (f32 scratch), h0 = bf16(e), w·x ---------------------------
+  // Work items (row, field, float4-column) are flattened so each thread issues up to 8 independent
+  // 16-B row loads before consuming any (one HBM/MALL latency for the whole tile's gather).
   {
     uint16_t* h0 = reinterpret_cast<uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
-    const int r = t >> 4, q = t & 15;
-    for (int f = q; f < F; f += 16) {
-      const int id = s_ids[r * F + f];
-      const float x = s_vals[r * F + f];
-      const float4* row = reinterpret_cast<const float4*>(p.emb + (size_t)id * Kp);
-      float* eo = s_f32 + r * D0p + f * K;
-      uint16_t* ho = h0 + r * lda + f * K;
-      for (int c4 = 0; c4 < (Kp >> 2); ++c4) {
-        const float4 v = row[c4];
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+    const int KP4 = Kp >> 2;
+    const int nitems = kRowTile * F * KP4;
+    const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
+    for (int base = 0; base < nitems; base += kRowThreads * 8) {
+      float4 v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = c4 * 4 + u;
-          const float e = vv[u] * x;
-          if (k < K) {
-            eo[k] = e;
-            ho[k] = f2bf(e);
-          } else if (k == K) {
-            s_wx[r * F + f] = e;
+      for (int u = 0; u < 8; ++u) {
+        const int idx = min(base + u * kRowThreads + t, nitems - 1);
+        const int rf = idx / KP4, c4 = idx - rf * KP4;
+        v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * kRowThreads + t;
+        if (idx < nitems) {
+          const int rf = idx / KP4, c4 = idx - rf * KP4;
+          const int r = rf / F, f = rf - r * F;
+          const float x = s_vals[rf];
+          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int k = c4 * 4 + c;
+            const float e = vv[c] * x;
+            if (k < K) {
+              s_f32[r * D0p + f * K + k] = e;
+              h0[r * lda + f * K + k] = f2bf(e);
+            } else if (k == K) {
+              s_wx[rf] = e;
+            }
           }
         }
       }
     }
+    const int r = t >> 4, q = t & 15;
     for (int c = D0 + q; c < D0p; c += 16) h0[r * lda + c] = 0;
   }
   __syncthreads();
@@ -130,28 +182,32 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const bool drop = p.train && keep < 1.f;
     const float inv_keep = 1.f / keep;
     __syncthreads();  // previous layer's tile (and phase A/B) complete
-    for (int nt = wave; nt < (Dout >> 4); nt += 4) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const uint16_t* bp = W + (size_t)(nt * 16 + (lane & 15)) * Din + 8 * (lane >> 4);
-      const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
-#pragma unroll 4
-      for (int ks = 0; ks < Din; ks += 32) acc = mfma16x16x32(ld_frag(ap + ks), ld_frag(bp + ks), acc);
-      const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
-      const float bc = p.bias[l][c];
-      Philox4 bits{0u, 0u, 0u, 0u};
-      if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
-      float hv[4];
+    const int ntiles = Dout >> 4;
+    for (int nt0 = wave; nt0 < ntiles; nt0 += 8) {
+      f32x4 accs[2];
+      rowtile_gemm<2, 8>(A, lda, W, Din, ntiles, nt0, Din, lane, accs);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float a = fmaxf(acc[i] + bc, 0.f);
-        if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
-        if (row0 + rb + i >= p.B) a = 0.f;
-        hv[i] = a;
-        O[(rb + i) * ldo + c] = f2bf(a);
+      for (int j = 0; j < 2; ++j) {
+        const int nt = nt0 + 4 * j;
+        if (nt >= ntiles) continue;
+        const f32x4 acc = accs[j];
+        const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
+        const float bc = p.bias[l][c];
+        Philox4 bits{0u, 0u, 0u, 0u};
+        if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
+        float hv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float a = fmaxf(acc[i] + bc, 0.f);
+          if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
+          if (row0 + rb + i >= p.B) a = 0.f;
+          hv[i] = a;
+          O[(rb + i) * ldo + c] = f2bf(a);
+        }
+        if (p.train)
+          *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
+              make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
       }
-      if (p.train)
-        *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
-            make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
     }
   }
   __syncthreads();
@@ -221,29 +277,33 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     __syncthreads();
     const int li = a - 1, Dout = p.dims[a], Din = p.dims[li];
     const uint16_t* W = p.Wb[li];  // [Din][Dout]
-    for (int nt = wave; nt < (Din >> 4); nt += 4) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const uint16_t* bp = W + (size_t)(nt * 16 + (lane & 15)) * Dout + 8 * (lane >> 4);
-      const uint16_t* ap = dz_cur + (lane & 15) * ldz + 8 * (lane >> 4);
-#pragma unroll 4
-      for (int ks = 0; ks < Dout; ks += 32) acc = mfma16x16x32(ld_frag(ap + ks), ld_frag(bp + ks), acc);
-      const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
-      if (li >= 1) {
-        const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[li]);
-        const int ldh = L.lda[li];
-        const float inv_keep = 1.f / p.keep[li - 1];
-        float v[4];
+    const int ntiles = Din >> 4;
+    for (int nt0 = wave; nt0 < ntiles; nt0 += 16) {
+      f32x4 accs[4];
+      rowtile_gemm<4, 4>(dz_cur, ldz, W, Dout, ntiles, nt0, Dout, lane, accs);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float h = bf2f(H[(rb + i) * ldh + c]);
-          v[i] = h > 0.f ? acc[i] * inv_keep : 0.f;
-          dz_nxt[(rb + i) * ldz + c] = f2bf(v[i]);
+      for (int j = 0; j < 4; ++j) {
+        const int nt = nt0 + 4 * j;
+        if (nt >= ntiles) continue;
+        const f32x4 acc = accs[j];
+        const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
+        if (li >= 1) {
+          const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[li]);
+          const int ldh = L.lda[li];
+          const float inv_keep = 1.f / p.keep[li - 1];
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float h = bf2f(H[(rb + i) * ldh + c]);
+            v[i] = h > 0.f ? acc[i] * inv_keep : 0.f;
+            dz_nxt[(rb + i) * ldz + c] = f2bf(v[i]);
+          }
+          *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
+              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) s_f32[(rb + i) * D0p + c] = acc[i];
         }
-        *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
-            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s_f32[(rb + i) * D0p + c] = acc[i];
       }
     }
     uint16_t* tmp = dz_cur;
@@ -254,31 +314,35 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 
   // ---- phase F: FM backward → per-lookup gradient rows -----------------------------------------
   {
-    const int r = t >> 4, q = t & 15, gr = row0 + r;
-    if (gr < p.B) {
-      const float g = s_g[r];
-      const float* S = s_S + r * K;
-      for (int f = q; f < F; f += 16) {
-        const int id = s_ids[r * F + f];
-        const float x = s_vals[r * F + f];
-        const float4* row = reinterpret_cast<const float4*>(p.emb + (size_t)id * Kp);
-        float4* out = reinterpret_cast<float4*>(p.contrib + ((size_t)gr * F + f) * Kp);
-        const float* dh = s_f32 + r * D0p + f * K;
-        for (int c4 = 0; c4 < (Kp >> 2); ++c4) {
-          const float4 v = row[c4];
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-          float o[4];
+    const int KP4 = Kp >> 2;
+    const int nitems = kRowTile * F * KP4;
+    const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
+    for (int base = 0; base < nitems; base += kRowThreads * 8) {
+      float4 v[8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int k = c4 * 4 + u;
-            if (k < K) {
-              o[u] = x * (g * (S[k] - vv[u] * x) + dh[k]);
-            } else {
-              o[u] = (k == K) ? g * x : 0.f;
-            }
-          }
-          out[c4] = make_float4(o[0], o[1], o[2], o[3]);
+      for (int u = 0; u < 8; ++u) {
+        const int idx = min(base + u * kRowThreads + t, nitems - 1);
+        const int rf = idx / KP4, c4 = idx - rf * KP4;
+        v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * kRowThreads + t;
+        if (idx >= nitems) continue;
+        const int rf = idx / KP4, c4 = idx - rf * KP4;
+        const int r = rf / F, f = rf - r * F;
+        if (row0 + r >= p.B) continue;
+        const float g = s_g[r], x = s_vals[rf];
+        const float* S = s_S + r * K;
+        const float* dh = s_f32 + r * D0p + f * K;
+        const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k = c4 * 4 + c;
+          o[c] = (k < K) ? x * (g * (S[k] - vv[c] * x) + dh[k]) : ((k == K) ? g * x : 0.f);
         }
+        reinterpret_cast<float4*>(p.contrib + ((size_t)(row0 + r) * F + f) * Kp)[c4] = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
   }

@@ -26,6 +26,10 @@ struct EmbUpdateParams {
   int* out_count;      // mode 2
   int id_offset;       // subtracted from keys before indexing emb (row-shard local index)
   int id_stride;       // keys are mapped to local rows by (key - id_offset) / id_stride
+  uint32_t max_key;    // runs with key >= max_key are skipped (padding sentinels); 0 = no limit
+  int contrib_seg;     // if > 0: lookup j lives at contrib + (j/seg)*seg_stride + (j%seg)*Kp
+  long long contrib_seg_stride;  // floats between segments (per-rank blocks of a gathered buffer)
+  int out_cap;         // mode 2: capacity of out_keys/out_rows (rows past it are dropped, count kept)
 };
 
 struct EmbDenseParams {
@@ -36,6 +40,7 @@ struct EmbDenseParams {
   long long n4;  // number of float4 in the table
   int Kp, K1;
   float l2;
+  float grad_scale;
   OptParams opt;
   const int64_t* step;
 };

@@ -21,14 +21,30 @@ namespace rocfm {
 namespace {
 
 constexpr int kChunk = 256;
-constexpr int kLongRun = 48;
+
+__device__ __forceinline__ const float4* contrib_row4(const EmbUpdateParams& p, uint32_t j) {
+  const float* r = (p.contrib_seg > 0) ? p.contrib + (size_t)(j / (uint32_t)p.contrib_seg) * p.contrib_seg_stride +
+                                             (size_t)(j % (uint32_t)p.contrib_seg) * p.Kp
+                                       : p.contrib + (size_t)j * p.Kp;
+  return reinterpret_cast<const float4*>(r);
+}
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4shfl_up(float4 v, int d) {
+  return make_float4(__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64), __shfl_up(v.z, d, 64), __shfl_up(v.w, d, 64));
+}
+__device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
+  return make_float4(__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64), __shfl_xor(v.z, d, 64), __shfl_xor(v.w, d, 64));
+}
 
 __device__ __forceinline__ void finish_row(const EmbUpdateParams& p, const OptStep& st, uint32_t key, int col,
                                            float g, int out_slot) {
   if (col >= p.K1) return;
   g *= p.grad_scale;
   if (p.mode == 2) {
-    p.out_rows[(size_t)out_slot * p.Kp + col] = g;
+    if (out_slot < p.out_cap) p.out_rows[(size_t)out_slot * p.Kp + col] = g;
     return;
   }
   const size_t row = (size_t)((key - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
@@ -47,48 +63,82 @@ __device__ __forceinline__ void finish_row(const EmbUpdateParams& p, const OptSt
 
 }  // namespace
 
+// One workgroup per 256 consecutive sorted entries.  Every thread loads ONE entry's gradient row
+// (Kp floats, float4 loads) into LDS, so the chunk's rows arrive in one memory latency; run pieces
+// are summed by a wave-level segmented scan (shfl_up, fixed order); each run owned by the chunk
+// (its first entry lies here) adds its ≤4 wave pieces and, for the chunk's last run, the
+// continuation chunks; then one 16-lane group per run applies the optimizer to the table row.
+template <int KP4>
 __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdateParams p) {
+  __shared__ float4 s_rows[kChunk * KP4];
+  __shared__ float4 s_cont[4 * KP4];
   __shared__ int s_head[kChunk + 1];
   __shared__ int s_wcnt[4];
   __shared__ int s_nh, s_last_end, s_out_base;
-  __shared__ float s_part[16][64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c0 = blockIdx.x * kChunk;
+  const int cend = min(c0 + kChunk, p.n);
   const int i = c0 + t;
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
 
-  // 1. run heads inside the chunk, compacted in order
-  uint32_t key = 0;
+  // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
+  uint32_t key = 0xffffffffu;
   bool head = false;
+  float4 v[KP4];
   if (i < p.n) {
     key = p.skeys[i];
     head = (i == 0) || (p.skeys[i - 1] != key);
+    const bool skip = p.max_key && key >= p.max_key;
+    const float4* src = contrib_row4(p, p.svals[i]);
+#pragma unroll
+    for (int u = 0; u < KP4; ++u) v[u] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : src[u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < KP4; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // 2. wave-level segmented inclusive scan (segments: runs, cut at wave boundaries)
+  {
+    const unsigned long long hm = __ballot(head || lane == 0 || i >= p.n);
+    const unsigned long long below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const int seg = 63 - __clzll(hm & below);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+      for (int u = 0; u < KP4; ++u) {
+        const float4 o = f4shfl_up(v[u], d);
+        if (lane - d >= seg) v[u] = f4add(v[u], o);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
+  }
+  // 3. compact the heads in order
   const unsigned long long m = __ballot(head);
   const int before = __popcll(m & ((1ull << lane) - 1ull));
   if (lane == 0) s_wcnt[wave] = __popcll(m);
   __syncthreads();
-  int base = 0;
-  for (int w = 0; w < wave; ++w) base += s_wcnt[w];
-  if (head) s_head[base + before] = i;
+  {
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += s_wcnt[w];
+    if (head) s_head[base + before] = i;
+  }
   if (t == 0) s_nh = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
   __syncthreads();
   const int nh = s_nh;
   if (nh == 0) return;
-
-  // 2. end of the last run (may extend beyond the chunk): wave 0 scans forward
+  // 4. end of the last run; mode 2 reserves output slots
   if (wave == 0) {
     const int last = s_head[nh - 1];
     const uint32_t lk = p.skeys[last];
-    int pos = min(c0 + kChunk, p.n);
+    int pos = cend;
     int end = p.n;
+    if (p.max_key && lk >= p.max_key) pos = p.n;  // sentinel padding sorts last
     while (pos < p.n) {
       const int j = pos + lane;
-      const bool diff = (j < p.n) && (p.skeys[j] != lk);
-      const unsigned long long dm = __ballot(diff || j >= p.n);
+      const bool diff = (j >= p.n) || (p.skeys[j] != lk);
+      const unsigned long long dm = __ballot(diff);
       if (dm) {
-        end = pos + __ffsll((long long)dm) - 1;
-        if (end > p.n) end = p.n;
+        end = min(pos + __ffsll((long long)dm) - 1, p.n);
         break;
       }
       pos += 64;
@@ -99,65 +149,88 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
     }
   }
   __syncthreads();
-  s_head[nh] = s_last_end;
+  if (t == 0) s_head[nh] = min(s_last_end, cend);
+  // 5. continuation of the last run past the chunk: full reductions over following chunks
+  const int last_end = s_last_end;
+  const bool cont = last_end > cend && !(p.max_key && p.skeys[s_head[nh - 1]] >= p.max_key);
+  if (cont) {
+    float4 tot[KP4];
+#pragma unroll
+    for (int u = 0; u < KP4; ++u) tot[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k0 = cend; k0 < last_end; k0 += kChunk) {
+      const int j = k0 + t;
+      float4 w[KP4];
+      if (j < last_end) {
+        const float4* src = contrib_row4(p, p.svals[j]);
+#pragma unroll
+        for (int u = 0; u < KP4; ++u) w[u] = src[u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < KP4; ++u) w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < KP4; ++u) {
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) w[u] = f4add(w[u], f4shfl_xor(w[u], d));
+        tot[u] = f4add(tot[u], w[u]);
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < KP4; ++u) s_cont[wave * KP4 + u] = tot[u];
+    }
+  }
   __syncthreads();
-
-  // 3. short runs: one 16-lane group each, lane = column (Kp <= 64 → 4 columns per lane)
+  // 6. one 16-lane group per owned run: add the wave pieces (+ continuation), apply the optimizer
   const int grp = t >> 4, q = t & 15;
+  const int Kp = KP4 * 4;
   for (int r = grp; r < nh; r += 16) {
-    const int s = s_head[r], e = s_head[r + 1];
-    if (e - s > kLongRun) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = s; k < e; ++k) {
-      const float* src = p.contrib + (size_t)p.svals[k] * p.Kp;
-      a0 += (q < p.Kp) ? src[q] : 0.f;
-      a1 += (q + 16 < p.Kp) ? src[q + 16] : 0.f;
-      a2 += (q + 32 < p.Kp) ? src[q + 32] : 0.f;
-      a3 += (q + 48 < p.Kp) ? src[q + 48] : 0.f;
-    }
+    const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
     const uint32_t kk = p.skeys[s];
+    if (p.max_key && kk >= p.max_key) continue;
     const int slot = (p.mode == 2) ? s_out_base + r : 0;
-    if (p.mode == 2 && q == 0) p.out_keys[slot] = kk;
-    finish_row(p, st, kk, q, a0, slot);
-    finish_row(p, st, kk, q + 16, a1, slot);
-    finish_row(p, st, kk, q + 32, a2, slot);
-    finish_row(p, st, kk, q + 48, a3, slot);
+    if (p.mode == 2 && q == 0 && slot < p.out_cap) p.out_keys[slot] = kk;
+    const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
+    for (int col = q; col < Kp; col += 16) {
+      const int u = col >> 2, comp = col & 3;
+      float g = 0.f;
+      for (int w = w0; w <= w1; ++w) {
+        const int lastw = min(e, c0 + 64 * (w + 1)) - 1 - c0;
+        const float4 x = s_rows[lastw * KP4 + u];
+        g += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
+      }
+      if (cont && r == nh - 1) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float4 x = s_cont[w * KP4 + u];
+          g += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
+        }
+      }
+      finish_row(p, st, kk, col, g, slot);
+    }
   }
+}
 
-  // 4. long runs: the whole workgroup, 16 groups stride the run, combine through LDS
-  for (int r = 0; r < nh; ++r) {
-    const int s = s_head[r], e = s_head[r + 1];
-    if (e - s <= kLongRun) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = s + grp; k < e; k += 16) {
-      const float* src = p.contrib + (size_t)p.svals[k] * p.Kp;
-      a0 += (q < p.Kp) ? src[q] : 0.f;
-      a1 += (q + 16 < p.Kp) ? src[q + 16] : 0.f;
-      a2 += (q + 32 < p.Kp) ? src[q + 32] : 0.f;
-      a3 += (q + 48 < p.Kp) ? src[q + 48] : 0.f;
-    }
-    __syncthreads();
-    s_part[grp][q] = a0;
-    s_part[grp][q + 16] = a1;
-    s_part[grp][q + 32] = a2;
-    s_part[grp][q + 48] = a3;
-    __syncthreads();
-    if (t < 64) {
-      float tot = 0.f;
-      for (int g2 = 0; g2 < 16; ++g2) tot += s_part[g2][t];
-      const uint32_t kk = p.skeys[s];
-      const int slot = (p.mode == 2) ? s_out_base + r : 0;
-      if (p.mode == 2 && t == 0) p.out_keys[slot] = kk;
-      finish_row(p, st, kk, t, tot, slot);
-    }
-  }
+template <int KP4>
+static void launch_rows_update_t(const EmbUpdateParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(emb_rows_update_kernel<KP4>, dim3(cdiv(p.n, kChunk)), dim3(kChunk), 0, stream, p);
 }
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp <= 64 && p.K1 <= p.Kp, "emb_update: Kp must be a multiple of 4 and <= 64");
   if (p.id_stride <= 0) p.id_stride = 1;
   if (p.n <= 0) return;
-  hipLaunchKernelGGL(emb_rows_update_kernel, dim3(cdiv(p.n, kChunk)), dim3(kChunk), 0, stream, p);
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N) \
+  case N:            \
+    launch_rows_update_t<N>(p, stream); \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("emb_update: unsupported Kp");
+  }
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 
@@ -182,7 +255,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
     float* bp = &b.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], gp[u] + p.l2 * wp[u], ap[u], bp[u]);
+      if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], gp[u] * p.grad_scale + p.l2 * wp[u], ap[u], bp[u]);
     E[i] = w;
     G[i] = make_float4(0, 0, 0, 0);
     if (A) A[i] = a;

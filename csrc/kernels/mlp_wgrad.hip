@@ -58,11 +58,22 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
     const uint16_t* Bm = p.dzT[li + 1] + (size_t)(to * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
     const int q = Bp >> 2;  // batch quarter per wave (Bp % 64 == 0)
     f32x16 acc = {};
-    int b = wave * q;
-    const int be = b + q;
-#pragma unroll 4
-    for (; b < be; b += 16)
-      acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(A + b), *reinterpret_cast<const bf16x8*>(Bm + b), acc);
+    const int bs = wave * q, be = bs + q;
+    const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b0 = bs; b0 < be; b0 += 16 * 8) {  // 8 k-steps of loads in flight per batch
+      bf16x8 fa[8], fb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = min(b0 + 16 * u, be - 16);
+        fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
+        fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (b0 + 16 * u >= be) fa[u] = zero;
+        acc = mfma32x32x16(fa[u], fb[u], acc);
+      }
+    }
     if (wave > 0) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) s_red[((wave - 1) * 16 + r) * 64 + lane] = acc[r];
@@ -95,6 +106,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
     const int o = cb * 32 + (t >> 3), sub = t & 7;
     const uint16_t* row = p.dzT[li + 1] + (size_t)o * Bp;
     float s = 0.f;
+#pragma unroll 4
     for (int b = sub * 8; b < Bp; b += 64) s += sum_bf16x8(*reinterpret_cast<const uint4*>(row + b));
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);

@@ -5,6 +5,7 @@
 
 #include "common.h"
 #include "kernels/deepfm_rows.h"
+#include "kernels/batch.h"
 #include "kernels/emb_update.h"
 #include "kernels/optim.h"
 

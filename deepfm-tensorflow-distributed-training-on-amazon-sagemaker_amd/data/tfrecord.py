@@ -1,0 +1,226 @@
+"""TFRecord input pipeline (the reference's ``input_fn``, PS:112-169 / HVD:104-161).
+
+* ``TFRecordDataset`` — batches of (ids int32 [B,F], vals f32 [B,F], labels f32 [B]) decoded by the
+  C++ runtime (csrc/io: mmap + CRC32C + fixed-schema Example decoder + worker pool) into pinned
+  host buffers; ``shard(count, index)`` = ``Dataset.shard``; ``drop_remainder`` and per-epoch
+  repeat like ``batch(drop_remainder=True) … repeat(num_epochs)``; optional record shuffle buffer
+  (the reference has none, Q6); pipe mode reads FIFOs / stdin sequentially (PipeModeDataset).
+* ``read_records`` / ``parse_example`` — a tiny pure-Python reader used as a cross-check oracle in
+  tests and as a fallback when the native module is unavailable.
+* ``discover_files`` — ``glob('{dir}/**/tr*.tfrecords', recursive=True)`` etc. (PS:418-428).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import random
+import struct
+from typing import Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import io as _io_mod
+
+# --------------------------------------------------------------------------------------------
+# file discovery (PS:418-428, HVD:352-361)
+# --------------------------------------------------------------------------------------------
+
+
+def discover_files(data_dir: str, prefix: str, shuffle: bool = False, seed: Optional[int] = None) -> List[str]:
+    if not data_dir:
+        return []
+    files = sorted(glob.glob(os.path.join(data_dir, "**", f"{prefix}*.tfrecords"), recursive=True))
+    if shuffle:  # the reference shuffles the training file order (PS:421)
+        random.Random(seed).shuffle(files)
+    return files
+
+
+# --------------------------------------------------------------------------------------------
+# pure-Python oracle
+# --------------------------------------------------------------------------------------------
+def _crc32c_py(data: bytes) -> int:
+    crc = 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 & -(crc & 1))
+    return crc ^ 0xFFFFFFFF
+
+
+def masked_crc32c_py(data: bytes) -> int:
+    c = _crc32c_py(data)
+    return (((c >> 15) | (c << 17)) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def read_records(path: str, verify: bool = False) -> Iterator[bytes]:
+    with open(path, "rb") as f:
+        while True:
+            hdr = f.read(12)
+            if not hdr:
+                return
+            if len(hdr) < 12:
+                raise ValueError("truncated TFRecord header")
+            (n,) = struct.unpack("<Q", hdr[:8])
+            body = f.read(n)
+            (dcrc,) = struct.unpack("<I", f.read(4))
+            if verify:
+                if masked_crc32c_py(hdr[:8]) != struct.unpack("<I", hdr[8:])[0]:
+                    raise ValueError("bad length crc")
+                if masked_crc32c_py(body) != dcrc:
+                    raise ValueError("bad data crc")
+            yield body
+
+
+def _varint(b: bytes, i: int) -> Tuple[int, int]:
+    v = 0
+    s = 0
+    while True:
+        x = b[i]
+        i += 1
+        v |= (x & 0x7F) << s
+        if not x & 0x80:
+            return v, i
+        s += 7
+
+
+def _fields(b: bytes):
+    i = 0
+    while i < len(b):
+        tag, i = _varint(b, i)
+        fno, wt = tag >> 3, tag & 7
+        if wt == 2:
+            n, i = _varint(b, i)
+            yield fno, wt, b[i:i + n]
+            i += n
+        elif wt == 0:
+            v, i = _varint(b, i)
+            yield fno, wt, v
+        elif wt == 5:
+            yield fno, wt, b[i:i + 4]
+            i += 4
+        elif wt == 1:
+            yield fno, wt, b[i:i + 8]
+            i += 8
+        else:
+            raise ValueError("bad wire type")
+
+
+def parse_example(payload: bytes) -> dict:
+    """Decode a tf.train.Example into {name: list} (float_list → floats, int64_list → ints)."""
+    out = {}
+    for fno, _, feats in _fields(payload):
+        if fno != 1:
+            continue
+        for f2, _, entry in _fields(feats):
+            if f2 != 1:
+                continue
+            key, val = None, None
+            for f3, _, x in _fields(entry):
+                if f3 == 1:
+                    key = x.decode()
+                elif f3 == 2:
+                    val = x
+            values = []
+            for kind, _, lst in _fields(val):
+                for f5, wt, x in _fields(lst):
+                    if kind == 2:  # float_list
+                        if wt == 2:
+                            values += list(struct.unpack(f"<{len(x) // 4}f", x))
+                        else:
+                            values.append(struct.unpack("<f", x)[0])
+                    elif kind == 3:  # int64_list
+                        if wt == 2:
+                            j = 0
+                            while j < len(x):
+                                v, j = _varint(x, j)
+                                values.append(v - (1 << 64) if v >= 1 << 63 else v)
+                        else:
+                            values.append(x - (1 << 64) if x >= 1 << 63 else x)
+                    else:
+                        values.append(x)
+            out[key] = values
+    return out
+
+
+# --------------------------------------------------------------------------------------------
+# native batch loader
+# --------------------------------------------------------------------------------------------
+class TFRecordDataset:
+    """Iterable of host batches decoded by the C++ loader.
+
+    Each yielded batch is a tuple of CPU tensors living in one of ``num_slots`` pinned buffers; the
+    slot is recycled when the NEXT batch is requested, so consumers must copy (e.g. an async H2D
+    copy followed by using the device tensor) before advancing the iterator twice.
+    """
+
+    def __init__(self, files: Sequence[str], field_size: int, batch_size: int, feature_size: int = 0,
+                 num_epochs: int = 1, shard_count: int = 1, shard_index: int = 0, drop_remainder: bool = True,
+                 num_threads: int = 4, num_slots: int = 6, verify_crc: bool = True, skip_bad: bool = False,
+                 shuffle_buffer: int = 0, seed: int = 0, stream_mode: bool = False, pin_memory: Optional[bool] = None):
+        self.files = list(files)
+        self.F = int(field_size)
+        self.B = int(batch_size)
+        self.kw = dict(field_size=self.F, max_id=int(feature_size), batch_size=self.B, drop_remainder=drop_remainder,
+                       num_epochs=int(num_epochs), shard_count=int(shard_count), shard_index=int(shard_index),
+                       num_threads=int(num_threads), num_slots=int(num_slots), verify_crc=verify_crc,
+                       skip_bad=skip_bad, shuffle_buffer=int(shuffle_buffer), seed=int(seed),
+                       stream_mode=stream_mode)
+        self.num_slots = int(num_slots)
+        if pin_memory is None:
+            pin_memory = torch.cuda.is_available()
+        self.pin = pin_memory
+        self.loader = None
+
+    def __iter__(self):
+        io = _io_mod()
+        if io is None:
+            raise RuntimeError("rocfm native IO module missing; run `python build.py`")
+        self.loader = io.BatchLoader(self.files, **self.kw)
+        bufs = []
+        for i in range(self.num_slots):
+            ids = torch.zeros(self.B, self.F, dtype=torch.int32, pin_memory=self.pin)
+            vals = torch.zeros(self.B, self.F, dtype=torch.float32, pin_memory=self.pin)
+            labels = torch.zeros(self.B, dtype=torch.float32, pin_memory=self.pin)
+            self.loader.set_slot(i, ids.data_ptr(), vals.data_ptr(), labels.data_ptr())
+            bufs.append((ids, vals, labels))
+        self.loader.start()
+        prev = None
+        try:
+            while True:
+                slot, rows, epoch = self.loader.next()
+                if prev is not None:
+                    self.loader.release(prev)
+                if slot < 0:
+                    break
+                prev = slot
+                ids, vals, labels = bufs[slot]
+                yield ids[:rows], vals[:rows], labels[:rows]
+        finally:
+            self.loader.stop()
+
+    @property
+    def bad_records(self) -> int:
+        return 0 if self.loader is None else int(self.loader.bad_records)
+
+
+def decode_file(path: str, field_size: int, feature_size: int = 0, verify_crc: bool = True, skip_bad: bool = False):
+    """Whole file → (labels [N], ids [N,F] int32, vals [N,F]) tensors (small files / eval sets)."""
+    io = _io_mod()
+    if io is None:  # pure-Python fallback
+        L, I, V = [], [], []
+        for rec in read_records(path, verify=verify_crc):
+            ex = parse_example(rec)
+            L.append(ex["label"][0])
+            I.append(ex["ids"])
+            V.append(ex["values"])
+        return (torch.tensor(L, dtype=torch.float32), torch.tensor(I, dtype=torch.int32),
+                torch.tensor(V, dtype=torch.float32))
+    L, I, V = io.decode_file(path, field_size, feature_size, verify_crc, skip_bad)
+    return torch.from_numpy(L), torch.from_numpy(I), torch.from_numpy(V)
+
+
+def write_tfrecord(path: str, labels, ids, vals, append: bool = False) -> int:
+    io = _io_mod()
+    return io.write_tfrecord(path, np.asarray(labels, np.float32), np.asarray(ids, np.int64),
+                             np.asarray(vals, np.float32), append)

@@ -1,9 +1,10 @@
 """Fused MI355X training engine for DeepFM (the HIP path).
 
-One training step on one GPU is four kernels (plus a step-counter bump), captured once into a HIP
-graph and replayed:
+One training step on one GPU is three kernels on the critical path plus a side stream that
+prepares the NEXT step's batch, captured once per step parity into a HIP graph and replayed:
 
-    side stream : sort_pairs      — radix sort of the batch's (id, lookup) pairs (sort.hip)
+    side stream : fetch_batch     — copy batch i+1 from the device pool into its input slot (batch.hip)
+                  sort_pairs      — radix sort of its (id, lookup) pairs (sort.hip)
     main stream : deepfm_rows     — gather + FM + MLP fwd + head + MLP bwd + FM bwd (deepfm_rows.hip)
                   mlp_wgrad       — dW/db on MFMA + fused optimizer + bf16 weight refresh (mlp_wgrad.hip)
                   emb_rows_update — sorted segment-sum of lookup grads + row optimizer (emb_update.hip)
@@ -18,7 +19,8 @@ State layout (device):
   dense [P] f32     — MLP weights/biases (dims padded to 32), deep_out, fm_bias (DenseLayout)
   WT/Wb             — bf16 copies of each hidden layer's W (forward / backward MFMA operands)
   slots             — optimizer state with the same layouts (Adam m,v; Adagrad acc; …)
-  step  [1] int64   — global_step, read by the kernels (Adam bias correction, dropout keys)
+  steps [2] int64   — global_step by step parity, read by the kernels (Adam bias correction,
+                      dropout keys); the side-stream fetch of step i publishes step i+1
 """
 from __future__ import annotations
 
@@ -81,7 +83,17 @@ class DenseLayout:
 
 
 class FusedDeepFM:
-    """Device-resident DeepFM state + the fused HIP training/inference steps for one GPU."""
+    """Device-resident DeepFM state + the fused HIP training/inference steps for one GPU.
+
+    Step pipeline (parity p = step % 2; every buffer a step reads is double-buffered):
+
+        side : fetch batch i+1 → input slot 1−p ; radix-sort its ids → keys[1−p]
+        main : deepfm_rows(slot p) → mlp_wgrad → emb_rows_update(keys[p]) ; join side
+
+    so the batch copy and the sort are off the critical path.  Batches come from a device pool
+    ([NB,B,F]): an HBM-resident dataset (``attach_pool``) or a 2-slot staging ring fed with
+    ``push_batch`` one batch ahead (the Estimator's loader path).
+    """
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device="cuda",
                  embedding_update: str = "sparse", seed: int = 1234,
@@ -109,6 +121,7 @@ class FusedDeepFM:
         self.fuse_dense_opt = fuse_dense_opt
         self.seed = int(seed if dropout_seed is None else dropout_seed)
         self.loss_code = 0 if spec.loss_type == "log_loss" else 1
+        self.lr_scale = 1.0
         dev = self.device
         L = self.layout
 
@@ -119,17 +132,18 @@ class FusedDeepFM:
         self.emb[:, self.K].copy_(P["fm_w"])
         self.dense = torch.zeros(L.total, dtype=torch.float32, device=dev)
         L.pack({k: v.to(dev) for k, v in P.items()}, self.dense)
-        self.emb_slots = self._make_slots(self.emb, real_cols=self.K1)
-        self.dense_slots = self._make_slots(self.dense)
+        self.emb_slots = init_slots(hp, self.emb)
+        self.dense_slots = init_slots(hp, self.dense)
         self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
-        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.steps = torch.zeros(2, dtype=torch.int64, device=dev)   # global_step, by parity
+        self.cursor = torch.zeros(2, dtype=torch.int64, device=dev)  # pool batch index, by parity
 
-        # ---- static step buffers --------------------------------------------------------------
+        # ---- static step buffers (double-buffered by parity where the pipeline needs it) -------
         B, Bp, F = self.B, self.Bp, self.F
-        self.ids_buf = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
-        self.vals_buf = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
-        self.labels_buf = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.slot_ids = [torch.zeros(Bp, F, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.slot_vals = [torch.zeros(Bp, F, dtype=torch.float32, device=dev) for _ in range(2)]
+        self.slot_labels = [torch.zeros(Bp, dtype=torch.float32, device=dev) for _ in range(2)]
         self.prob = torch.zeros(Bp, dtype=torch.float32, device=dev)
         self.loss_rows = torch.zeros(Bp, dtype=torch.float32, device=dev)
         self.g = torch.zeros(Bp, dtype=torch.float32, device=dev)
@@ -139,58 +153,64 @@ class FusedDeepFM:
                     for a in range(L.nl + 1)]
         self.n_lookup = B * F
         self.end_bit = max(1, math.ceil(math.log2(max(self.V, 2))))
-        self.skeys = torch.zeros(self.n_lookup, dtype=torch.int32, device=dev)
-        self.svals = torch.zeros(self.n_lookup, dtype=torch.int32, device=dev)
+        self.skeys = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.svals = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
         tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
         self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
         self.dense_grad = (torch.zeros_like(self.emb) if embedding_update == "exact" else None)
         self.dense_grads_flat = torch.zeros(L.total, dtype=torch.float32, device=dev)
-        self.sort_stream = torch.cuda.Stream(device=dev) if self.device.type == "cuda" else None
+        self.sort_stream = torch.cuda.Stream(device=dev)
+        # inference buffers (separate from the training slots)
+        self.pred_ids = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
+        self.pred_vals = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
+        self.pred_labels = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.pred_prob = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        self.pred_loss = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        # default batch source: a 2-slot ring fed by push_batch()
+        self._ring = True
+        self._set_pool(torch.zeros(2, B, F, dtype=torch.int32, device=dev),
+                       torch.zeros(2, B, F, dtype=torch.float32, device=dev),
+                       torch.zeros(2, B, dtype=torch.float32, device=dev))
+        self._pushed = 0
 
+        self._i = 0  # completed steps (host mirror of global_step)
+        self._primed = False
+        self._graphs = [None, None]
+        self._warm = 0
         self._build_params()
         self.refresh_bf16()
-        self._graph = None
-        self._graph_warm = 0
 
     # ------------------------------------------------------------------------------------------
-    def _make_slots(self, t: torch.Tensor, real_cols: Optional[int] = None) -> List[torch.Tensor]:
-        hp = self.hp
-        slots = init_slots(hp, t)
-        if real_cols is not None:  # pad columns stay exactly 0 / init so they never move
-            pass
-        return slots
-
-    def _opt(self, lr_scale: float = 1.0):
+    def _opt(self):
         o = self.H.OptParams()
         hp = self.hp
         o.type = OPT_ID[hp.name]
-        o.lr = hp.lr * lr_scale
+        o.lr = hp.lr * self.lr_scale
         o.beta1, o.beta2, o.eps = hp.beta1, hp.beta2, hp.eps
         o.momentum = hp.momentum
         o.ftrl_lr_power, o.ftrl_l1, o.ftrl_l2 = hp.ftrl_lr_power, hp.ftrl_l1, hp.ftrl_l2
         return o
 
-    def _slot_ptrs(self, slots):
+    @staticmethod
+    def _slot_ptrs(slots):
         s0 = slots[0].data_ptr() if len(slots) > 0 else 0
         s1 = slots[1].data_ptr() if len(slots) > 1 else 0
         return s0, s1
 
-    def _build_params(self):
+    def _rows_params(self, ids, vals, labels, prob, loss_rows, step_ptr, train):
         H, L = self.H, self.layout
-        dense_views = L.views(self.dense)
-        # row kernel
         rp = H.RowsParams()
-        rp.ids, rp.vals, rp.labels = self.ids_buf.data_ptr(), self.vals_buf.data_ptr(), self.labels_buf.data_ptr()
+        rp.ids, rp.vals, rp.labels = ids.data_ptr(), vals.data_ptr(), labels.data_ptr()
         rp.emb = self.emb.data_ptr()
-        rp.fm_bias = dense_views["fm_bias"].data_ptr()
+        rp.fm_bias = self.dense[L.off_fmb:].data_ptr()
         rp.w_out = self.dense[L.off_wout:].data_ptr()
         rp.b_out = self.dense[L.off_bout:].data_ptr()
-        rp.step = self.step.data_ptr()
-        rp.prob, rp.loss_rows, rp.g_out = self.prob.data_ptr(), self.loss_rows.data_ptr(), self.g.data_ptr()
+        rp.step = step_ptr
+        rp.prob, rp.loss_rows, rp.g_out = prob.data_ptr(), loss_rows.data_ptr(), self.g.data_ptr()
         rp.contrib = self.contrib.data_ptr()
         rp.nl, rp.F, rp.K, rp.Kp, rp.B, rp.Bp = L.nl, self.F, self.K, self.Kp, self.B, self.Bp
         rp.inv_scale = 1.0 / self.B
-        rp.train = 1
+        rp.train = 1 if train else 0
         rp.loss_type = self.loss_code
         rp.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         rp.set_dims(L.dims)
@@ -199,76 +219,162 @@ class FusedDeepFM:
                          float(self.spec.keep_probs[l]))
         for a in range(L.nl + 1):
             rp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
-        self.rows_params = rp
         if rp.lds_bytes() > 160 * 1024:
             raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
-        # weight-gradient kernel
-        wp = H.WgradParams()
-        wp.g = self.g.data_ptr()
-        wp.params = self.dense.data_ptr()
-        wp.grads = self.dense_grads_flat.data_ptr()
-        wp.s0, wp.s1 = self._slot_ptrs(self.dense_slots)
-        wp.step = self.step.data_ptr()
-        wp.nl, wp.Bp = L.nl, self.Bp
-        wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
-        wp.fuse_opt = 1 if self.fuse_dense_opt else 0
-        wp.opt = self._opt()
-        wp.grad_scale = 1.0
-        wp.set_dims(L.dims)
-        for a in range(L.nl + 1):
-            wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
-        for l in range(L.nl):
-            wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
-        self.wgrad_params = wp
-        # dense apply (DP path / bf16 refresh)
-        dp = H.DenseApplyParams()
-        dp.params = self.dense.data_ptr()
-        dp.grads = self.dense_grads_flat.data_ptr()
-        dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
-        dp.step = self.step.data_ptr()
-        dp.n, dp.nl = L.total, L.nl
-        dp.opt = self._opt()
-        dp.set_dims(L.dims)
-        for l in range(L.nl):
-            dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
-        self.dense_apply_params = dp
-        # embedding update
-        ep = H.EmbUpdateParams()
-        ep.skeys, ep.svals = self.skeys.data_ptr(), self.svals.data_ptr()
-        ep.n = self.n_lookup
-        ep.contrib = self.contrib.data_ptr()
-        ep.K1, ep.Kp = self.K1, self.Kp
-        ep.emb = self.emb.data_ptr()
-        ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
-        ep.l2 = float(self.spec.l2_reg)
-        ep.grad_scale = 1.0
-        ep.opt = self._opt()
-        ep.step = self.step.data_ptr()
-        ep.mode = 1 if self.embedding_update == "exact" else 0
-        if self.dense_grad is not None:
-            ep.dense_grad = self.dense_grad.data_ptr()
-        self.emb_params = ep
-        if self.embedding_update == "exact":
-            ed = H.EmbDenseParams()
-            ed.emb = self.emb.data_ptr()
-            ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
-            ed.dense_grad = self.dense_grad.data_ptr()
-            ed.step = self.step.data_ptr()
-            ed.n4 = self.V * self.Kp // 4
-            ed.Kp, ed.K1 = self.Kp, self.K1
-            ed.l2 = float(self.spec.l2_reg)
-            ed.opt = self._opt()
-            self.emb_dense_params = ed
+        return rp
+
+    def _build_params(self):
+        H, L = self.H, self.layout
+        self.rows_params, self.wgrad_params, self.dense_apply_params = [], [], []
+        self.emb_params, self.emb_dense_params = [], []
+        for p in range(2):
+            step_ptr = self.steps[p:].data_ptr()
+            self.rows_params.append(self._rows_params(self.slot_ids[p], self.slot_vals[p], self.slot_labels[p],
+                                                      self.prob, self.loss_rows, step_ptr, True))
+            wp = H.WgradParams()
+            wp.g = self.g.data_ptr()
+            wp.params = self.dense.data_ptr()
+            wp.grads = self.dense_grads_flat.data_ptr()
+            wp.s0, wp.s1 = self._slot_ptrs(self.dense_slots)
+            wp.step = step_ptr
+            wp.nl, wp.Bp = L.nl, self.Bp
+            wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
+            wp.fuse_opt = 1 if self.fuse_dense_opt else 0
+            wp.opt = self._opt()
+            wp.grad_scale = 1.0
+            wp.set_dims(L.dims)
+            for a in range(L.nl + 1):
+                wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
+            for l in range(L.nl):
+                wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+            self.wgrad_params.append(wp)
+            dp = H.DenseApplyParams()
+            dp.params = self.dense.data_ptr()
+            dp.grads = self.dense_grads_flat.data_ptr()
+            dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
+            dp.step = step_ptr
+            dp.n, dp.nl = L.total, L.nl
+            dp.opt = self._opt()
+            dp.set_dims(L.dims)
+            for l in range(L.nl):
+                dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+            self.dense_apply_params.append(dp)
+            ep = H.EmbUpdateParams()
+            ep.skeys, ep.svals = self.skeys[p].data_ptr(), self.svals[p].data_ptr()
+            ep.n = self.n_lookup
+            ep.contrib = self.contrib.data_ptr()
+            ep.K1, ep.Kp = self.K1, self.Kp
+            ep.emb = self.emb.data_ptr()
+            ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
+            ep.l2 = float(self.spec.l2_reg)
+            ep.grad_scale = 1.0
+            ep.opt = self._opt()
+            ep.step = step_ptr
+            ep.mode = 1 if self.embedding_update == "exact" else 0
+            if self.dense_grad is not None:
+                ep.dense_grad = self.dense_grad.data_ptr()
+            self.emb_params.append(ep)
+            if self.embedding_update == "exact":
+                ed = H.EmbDenseParams()
+                ed.emb = self.emb.data_ptr()
+                ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
+                ed.dense_grad = self.dense_grad.data_ptr()
+                ed.step = step_ptr
+                ed.n4 = self.V * self.Kp // 4
+                ed.Kp, ed.K1 = self.Kp, self.K1
+                ed.l2 = float(self.spec.l2_reg)
+                ed.opt = self._opt()
+                self.emb_dense_params.append(ed)
+        self.pred_params = self._rows_params(self.pred_ids, self.pred_vals, self.pred_labels, self.pred_prob,
+                                             self.pred_loss, self.steps.data_ptr(), False)
+        self._build_fetch()
+
+    def _build_fetch(self):
+        H = self.H
+        self.fetch_params = []
+        for p in range(2):  # step with parity p fetches batch cur[p]+1 into slot 1-p
+            f = H.FetchParams()
+            f.ids_pool, f.vals_pool, f.labels_pool = (self.pool_ids.data_ptr(), self.pool_vals.data_ptr(),
+                                                      self.pool_labels.data_ptr())
+            f.pool_batches = self.pool_ids.shape[0]
+            f.B, f.F = self.B, self.F
+            f.cur_src, f.cur_dst, f.advance = self.cursor[p:].data_ptr(), self.cursor[1 - p:].data_ptr(), 1
+            f.step_src, f.step_dst, f.step_advance = self.steps[p:].data_ptr(), self.steps[1 - p:].data_ptr(), 1
+            f.ids, f.vals, f.labels = (self.slot_ids[1 - p].data_ptr(), self.slot_vals[1 - p].data_ptr(),
+                                       self.slot_labels[1 - p].data_ptr())
+            self.fetch_params.append(f)
+
+    def _set_pool(self, ids, vals, labels):
+        if ids.dim() != 3 or ids.shape[1:] != (self.B, self.F) or vals.shape != ids.shape or \
+                labels.shape != ids.shape[:2]:
+            raise ValueError(f"pool must be ids/vals [NB,{self.B},{self.F}], labels [NB,{self.B}]")
+        self.pool_ids = ids.to(self.device, torch.int32).contiguous()
+        self.pool_vals = vals.to(self.device, torch.float32).contiguous()
+        self.pool_labels = labels.to(self.device, torch.float32).contiguous()
+
+    def attach_pool(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor, start: int = 0) -> None:
+        """Train from a device-resident pool of batches ([NB,B,F] ids/vals, [NB,B] labels), cycling."""
+        self._set_pool(ids, vals, labels)
+        self._ring = False
+        self._build_fetch()
+        self._graphs = [None, None]
+        self._primed = False
+        self._start_batch = start
+
+    def push_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor) -> None:
+        """Ring mode: enqueue the next batch (must stay exactly one batch ahead of train_step)."""
+        if not self._ring:
+            raise RuntimeError("push_batch() is for the loader ring; this engine trains from an attached pool")
+        n = ids.shape[0]
+        if n != self.B:
+            raise ValueError(f"batch has {n} rows, engine built for {self.B} (drop_remainder semantics)")
+        slot = self._pushed % 2
+        self.pool_ids[slot].copy_(ids, non_blocking=True)
+        self.pool_vals[slot].copy_(vals, non_blocking=True)
+        self.pool_labels[slot].copy_(labels, non_blocking=True)
+        self._pushed += 1
+
+    def load_batch(self, ids, vals, labels=None) -> None:
+        """Compatibility helper: make (ids, vals, labels) the batch of the NEXT train_step().
+
+        Non-pipelined (re-primes the input slot); use push_batch/attach_pool for full speed.
+        """
+        if labels is None:
+            labels = torch.zeros(ids.shape[0], device=ids.device)
+        if not self._ring:
+            raise RuntimeError("load_batch() needs ring mode")
+        self._pushed = self._i
+        self.push_batch(ids, vals, labels)
+        self._primed = False
+
+    def train_on(self, batches):
+        """Train one step per (ids, vals, labels) batch from an iterable, feeding the ring one ahead.
+
+        Yields after each enqueued step (so callers can log / checkpoint between steps).
+        """
+        it = iter(batches)
+        cur = next(it, None)
+        if cur is None:
+            return
+        self.load_batch(*cur)
+        nxt = next(it, None)
+        while True:
+            if nxt is not None:
+                self.push_batch(*nxt)
+            self.train_step()
+            yield
+            if nxt is None:
+                break
+            nxt = next(it, None)
 
     def set_lr_scale(self, s: float) -> None:
         """Multiply the learning rate (Horovod's lr × world size, HVD:171)."""
-        o = self._opt(s)
-        self.wgrad_params.opt = o
-        self.dense_apply_params.opt = o
-        self.emb_params.opt = o
-        if self.embedding_update == "exact":
-            self.emb_dense_params.opt = o
-        self._graph = None
+        self.lr_scale = float(s)
+        o = self._opt()
+        for lst in (self.wgrad_params, self.dense_apply_params, self.emb_params, self.emb_dense_params):
+            for q in lst:
+                q.opt = o
+        self._graphs = [None, None]
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -276,95 +382,104 @@ class FusedDeepFM:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def refresh_bf16(self) -> None:
-        dp = self.dense_apply_params
+        dp = self.dense_apply_params[0]
         dp.apply = 0
         self.H.dense_apply(dp, self.stream_ptr)
 
-    def load_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None) -> None:
-        """Copy a batch into the static (graph-bound) input buffers (async on the current stream)."""
-        n = ids.shape[0]
-        if n != self.B:
-            raise ValueError(f"batch has {n} rows, engine built for {self.B} (drop_remainder semantics)")
-        self.ids_buf[:n].copy_(ids, non_blocking=True)
-        self.vals_buf[:n].copy_(vals, non_blocking=True)
-        if labels is not None:
-            self.labels_buf[:n].copy_(labels, non_blocking=True)
+    def _sort(self, q: int, stream) -> None:
+        self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.slot_ids[q].data_ptr(),
+                               self.skeys[q].data_ptr(), self.svals[q].data_ptr(), self.n_lookup, self.end_bit,
+                               stream.cuda_stream)
+
+    def prime(self) -> None:
+        """Fetch + sort the current step's batch into its slot (before the first step / after a reset)."""
+        p = self._i % 2
+        base = 0 if self._ring else getattr(self, "_start_batch", 0)
+        self.cursor[p] = base + self._i
+        self.steps[p] = self._i
+        f = self.H.FetchParams()
+        src = self.fetch_params[p]
+        f.ids_pool, f.vals_pool, f.labels_pool, f.pool_batches = (src.ids_pool, src.vals_pool, src.labels_pool,
+                                                                  src.pool_batches)
+        f.B, f.F = self.B, self.F
+        f.cur_src, f.cur_dst, f.advance = self.cursor[p:].data_ptr(), 0, 0
+        f.step_src, f.step_dst, f.step_advance = self.steps[p:].data_ptr(), 0, 0
+        f.ids, f.vals, f.labels = (self.slot_ids[p].data_ptr(), self.slot_vals[p].data_ptr(),
+                                   self.slot_labels[p].data_ptr())
+        self.H.fetch_batch(f, self.stream_ptr)
+        self._sort(p, torch.cuda.current_stream(self.device))
+        self._primed = True
 
     # ---- the step ------------------------------------------------------------------------------
-    def _enqueue_sort(self):
+    def _fork_next(self, p: int):
+        """Side stream: fetch + sort batch i+1 (into parity 1-p buffers)."""
         main = torch.cuda.current_stream(self.device)
         side = self.sort_stream
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.ids_buf.data_ptr(),
-                                   self.skeys.data_ptr(), self.svals.data_ptr(), self.n_lookup, self.end_bit,
-                                   side.cuda_stream)
+            self.H.fetch_batch(self.fetch_params[p], side.cuda_stream)
+            self._sort(1 - p, side)
         return side
 
-    def _enqueue_forward_backward(self):
-        """rows kernel + (fused or grad-only) wgrad; embedding not yet updated."""
-        s = self.stream_ptr
-        self.rows_params.train = 1
-        self.H.deepfm_rows(self.rows_params, s)
-        self.H.mlp_wgrad(self.wgrad_params, s)
+    def _join(self, side) -> None:
+        torch.cuda.current_stream(self.device).wait_stream(side)
 
-    def _enqueue_emb_update(self, side):
-        main = torch.cuda.current_stream(self.device)
-        main.wait_stream(side)
+    def _enqueue_forward_backward(self, p: int) -> None:
         s = self.stream_ptr
-        self.H.emb_rows_update(self.emb_params, s)
+        self.H.deepfm_rows(self.rows_params[p], s)
+        self.H.mlp_wgrad(self.wgrad_params[p], s)
+
+    def _enqueue_emb_update(self, p: int) -> None:
+        s = self.stream_ptr
+        self.H.emb_rows_update(self.emb_params[p], s)
         if self.embedding_update == "exact":
-            self.H.emb_dense_update(self.emb_dense_params, s)
+            self.H.emb_dense_update(self.emb_dense_params[p], s)
 
-    def _enqueue_step(self):
-        side = self._enqueue_sort()
-        self._enqueue_forward_backward()
-        self._enqueue_emb_update(side)
-        self.step.add_(1)
+    def _enqueue_step(self, p: int) -> None:
+        side = self._fork_next(p)
+        self._enqueue_forward_backward(p)
+        self._enqueue_emb_update(p)
+        self._join(side)
 
     def train_step(self) -> None:
-        """One optimisation step on the batch in the static buffers (asynchronous)."""
+        """One optimisation step on the current batch (asynchronous)."""
         if not self.fuse_dense_opt:
             raise RuntimeError("train_step() is the single-GPU step; distributed steps live in rocfm.parallel")
-        if not self.use_graph:
-            self._enqueue_step()
-            return
-        if self._graph is None:
-            if self._graph_warm < 2:  # warm up eagerly (allocator, kernel attributes) before capture
-                self._graph_warm += 1
-                self._enqueue_step()
-                return
-            g = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(g):
-                self._enqueue_step()
-            self._graph = g
-            # capture recorded the kernels but did not run them
-        self._graph.replay()
+        if not self._primed:
+            self.prime()
+        p = self._i % 2
+        if not self.use_graph or self._warm < 2:
+            self._warm += 1
+            self._enqueue_step(p)
+        else:
+            if self._graphs[p] is None:
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(self.device)
+                with torch.cuda.graph(g):
+                    self._enqueue_step(p)
+                self._graphs[p] = g
+            self._graphs[p].replay()
+        self._i += 1
 
     # ---- inference -----------------------------------------------------------------------------
     @torch.no_grad()
     def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
-        """Probabilities (and per-row losses) for up to B rows; no dropout, no update."""
+        """Probabilities (and per-row losses) for any number of rows; no dropout, no update."""
         n = ids.shape[0]
         if n > self.B:
             out = [self.predict_batch(ids[i:i + self.B], vals[i:i + self.B],
                                       None if labels is None else labels[i:i + self.B]) for i in range(0, n, self.B)]
             return torch.cat([o[0] for o in out]), torch.cat([o[1] for o in out])
-        self.ids_buf[:n].copy_(ids)
-        self.vals_buf[:n].copy_(vals)
+        self.pred_ids[:n].copy_(ids)
+        self.pred_vals[:n].copy_(vals)
         if labels is not None:
-            self.labels_buf[:n].copy_(labels)
+            self.pred_labels[:n].copy_(labels)
         else:
-            self.labels_buf.zero_()
-        rp = self.rows_params
-        rp.train = 0
-        saved_B = rp.B
+            self.pred_labels.zero_()
+        rp = self.pred_params
         rp.B = n
         self.H.deepfm_rows(rp, self.stream_ptr)
-        rp.B = saved_B
-        rp.train = 1
-        return self.prob[:n].clone(), self.loss_rows[:n].clone()
+        return self.pred_prob[:n].clone(), self.pred_loss[:n].clone()
 
     # ---- state ----------------------------------------------------------------------------------
     def l2_value(self) -> float:
@@ -376,14 +491,19 @@ class FusedDeepFM:
         return float(self.spec.l2_reg * 0.5 * part.double().sum().item())
 
     def batch_loss(self, include_l2: bool = True) -> float:
+        """Loss of the most recent training batch (mean data loss [+ full-table L2 terms])."""
         loss = float(self.loss_rows[: self.B].double().mean().item())
         return loss + (self.l2_value() if include_l2 else 0.0)
 
+    def last_probs(self) -> torch.Tensor:
+        return self.prob[: self.B]
+
     def global_step(self) -> int:
-        return int(self.step.item())
+        return self._i
 
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         """TF-named variables + optimizer slots + global_step (CPU tensors)."""
+        torch.cuda.synchronize(self.device)
         sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         tf = self._tf_views(self.emb, self.dense)
         for k, v in tf.items():
@@ -406,9 +526,11 @@ class FusedDeepFM:
             for si, sn in enumerate(slot_names(self.hp.name)):
                 self._load_views(sd, "/" + sn, self.emb_slots[si], self.dense_slots[si], strict)
             if "global_step" in sd:
-                self.step.fill_(int(sd["global_step"]))
+                self._i = int(sd["global_step"])
         self.refresh_bf16()
-        self._graph = None
+        self._graphs = [None, None]
+        self._primed = False
+        self._pushed = self._i
 
     def _tf_views(self, emb_like: torch.Tensor, dense_like: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
         v: "OrderedDict[str, torch.Tensor]" = OrderedDict()

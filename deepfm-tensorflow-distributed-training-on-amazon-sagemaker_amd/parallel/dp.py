@@ -1,0 +1,291 @@
+"""Data parallelism — the Horovod path of the reference (HVD:171, 296, 333, 393-418) on RCCL.
+
+Every rank holds a full replica (rank-0 initial values, like BroadcastGlobalVariablesHook(0)),
+trains on its own shard of the data and, each step, exchanges gradients:
+
+``dense_dp`` (``embedding_update=exact``)
+    Horovod-faithful: the full-table L2 makes the fm_w/fm_v gradients dense, so the
+    whole dense gradient — table + MLP in ONE flat bucket — is all-reduced and averaged (the
+    16.2 MB/step of the notebook config), then every rank applies the same dense
+    optimizer update.
+
+``dp`` (``embedding_update=sparse``, the default)
+    Each rank reduces its lookups to (unique id, Σ grad row) pairs (emb_update.hip mode 2) and
+    packs them next to its MLP gradient in one send buffer; ONE ``all_gather`` moves every rank's
+    buffer to every rank (xGMI is fully connected point-to-point, so RCCL's all-gather uses all
+    links); each rank then sums the MLP gradients over ranks in rank order and merges the gathered
+    rows with the same sort + segmented-sum kernel it uses locally (rank-major order ⇒ bitwise
+    identical results on every rank), applies lazy L2 once and the row optimizer.  Replicas stay
+    bit-identical without a broadcast.
+
+Gradients are averaged over ranks and the learning rate is scaled by the world size (HVD:171;
+``lr_scaling``).  Both the fused HIP engine and the eager engine are supported.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.deepfm import ModelSpec
+from ..optim import OptHParams
+
+
+def _world() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor) -> None:
+    """all_gather into a [world*n] buffer; RCCL fast path, host-staged fallback for gloo."""
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(out, inp)
+        return
+    n = inp.numel()
+    src = inp.detach().cpu()
+    outs = [torch.empty_like(src) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, src)
+    out.view(-1, n).copy_(torch.stack(outs))
+
+
+def _all_reduce(t: torch.Tensor) -> None:
+    if dist.get_backend() == "nccl" or t.device.type == "cpu":
+        dist.all_reduce(t)
+        return
+    c = t.detach().cpu()
+    dist.all_reduce(c)
+    t.copy_(c)
+
+
+# ================================================================================================
+# eager engine hooks (CPU/gloo tests, PyTorch baseline)
+# ================================================================================================
+def attach_torch_dp(eng, embedding_update: str = "sparse") -> None:
+    """Install gradient-exchange hooks on a TorchDeepFM (rocfm.models.torch_engine)."""
+    world = _world()
+    if world == 1:
+        return
+
+    def allreduce_dense(grads: Dict[str, torch.Tensor]) -> None:
+        names = sorted(grads)
+        flat = torch.cat([grads[k].reshape(-1) for k in names])
+        dist.all_reduce(flat)
+        flat /= world
+        off = 0
+        for k in names:
+            n = grads[k].numel()
+            grads[k].copy_(flat[off:off + n].view_as(grads[k]))
+            off += n
+
+    def exchange_rows(uniq: torch.Tensor, gw: torch.Tensor, gv: torch.Tensor):
+        dev = uniq.device
+        n = torch.tensor([uniq.numel()], dtype=torch.int64, device=dev)
+        ns = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(ns, n)
+        cap = int(max(int(x) for x in ns))
+        K = gv.shape[1]
+        pack = torch.zeros(cap, K + 2, dtype=torch.float64, device=dev)
+        pack[: uniq.numel(), 0] = uniq.double()
+        pack[: uniq.numel(), 1] = gw.double()
+        pack[: uniq.numel(), 2:] = gv.double()
+        bufs = [torch.zeros_like(pack) for _ in range(world)]
+        dist.all_gather(bufs, pack)
+        rows = torch.cat([b[: int(c)] for b, c in zip(bufs, ns)])  # rank-major, deterministic
+        ids = rows[:, 0].long()
+        u, inv = torch.unique(ids, return_inverse=True)
+        acc = torch.zeros(len(u), K + 1, dtype=torch.float64, device=dev)
+        acc.index_add_(0, inv, rows[:, 1:])
+        acc /= world
+        return u, acc[:, 0].float(), acc[:, 1:].float()
+
+    eng.allreduce_dense = allreduce_dense
+    if embedding_update != "exact":
+        eng.exchange_rows = exchange_rows
+
+
+# ================================================================================================
+# fused engine
+# ================================================================================================
+class FusedDataParallel:
+    """Data-parallel wrapper around one FusedDeepFM per rank (one GPU per process)."""
+
+    def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
+                 embedding_update: str = "sparse", mode: str = "dp", seed: int = 1234, use_graph: bool = True,
+                 capacity: Optional[int] = None):
+        from ..models.fused import FusedDeepFM
+
+        self.world = _world()
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        if mode not in ("dp", "dense_dp"):
+            raise ValueError(f"FusedDataParallel mode must be dp or dense_dp, got {mode}")
+        if mode == "dense_dp" and embedding_update != "exact":
+            embedding_update = "exact"
+        if mode == "dp" and embedding_update == "exact":
+            mode = "dense_dp"
+        self.mode = mode
+        self.eng = FusedDeepFM(spec, hp, batch_size, device, embedding_update=embedding_update, seed=seed,
+                               params=params, use_graph=False, fuse_dense_opt=False,
+                               dropout_seed=seed + 7919 * self.rank)
+        e = self.eng
+        self.use_graph = use_graph
+        self.device = e.device
+        # replicas start identical: broadcast rank 0's variables (HVD:418)
+        if self.world > 1:
+            from .dist import broadcast_tensors
+
+            broadcast_tensors([e.emb, e.dense] + list(e.emb_slots) + list(e.dense_slots))
+            e.refresh_bf16()
+        P = e.layout.total
+        H = e.H
+        if mode == "dense_dp":
+            # one flat bucket: [dense table grad (V*Kp) | MLP grads (P)]
+            self.bucket = torch.zeros(e.V * e.Kp + P, dtype=torch.float32, device=e.device)
+            e.dense_grad = self.bucket[: e.V * e.Kp].view(e.V, e.Kp)
+            e.dense_grads_flat = self.bucket[e.V * e.Kp:]
+            e._build_params()
+            for p in range(2):
+                e.emb_dense_params[p].grad_scale = 1.0 / self.world
+                e.dense_apply_params[p].grad_scale = 1.0 / self.world
+                e.dense_apply_params[p].apply = 1
+        else:
+            cap = (int(capacity or e.n_lookup) + 3) // 4 * 4  # keeps every row 16-B aligned
+            self.cap = cap
+            Kp = e.Kp
+            # send buffer (f32 words): [MLP grads P | count (int32) + pad 3 | keys cap (int32) | rows cap*Kp]
+            self.off_cnt = P
+            self.off_keys = P + 4
+            self.off_rows = self.off_keys + cap
+            self.S = self.off_rows + cap * Kp
+            self.send = torch.zeros(self.S, dtype=torch.float32, device=e.device)
+            self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+            e.dense_grads_flat = self.send[:P]
+            self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
+            self.mlp_sum = torch.zeros(P, dtype=torch.float32, device=e.device)
+            self.mkeys = torch.zeros(self.world * cap, dtype=torch.int32, device=e.device)
+            self.msk = torch.zeros_like(self.mkeys)
+            self.msv = torch.zeros_like(self.mkeys)
+            self.merge_bits = max(1, math.ceil(math.log2(e.V + 1)))
+            tb = H.sort_pairs_temp_bytes(self.world * cap, self.merge_bits)
+            self.merge_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=e.device)
+            self.col = torch.arange(cap, dtype=torch.int32, device=e.device)
+            e._build_params()
+            self.export_params = []
+            for p in range(2):
+                ex = H.EmbUpdateParams()
+                src = e.emb_params[p]
+                ex.skeys, ex.svals, ex.n, ex.contrib = src.skeys, src.svals, src.n, src.contrib
+                ex.K1, ex.Kp, ex.opt, ex.step = e.K1, e.Kp, src.opt, src.step
+                ex.mode = 2
+                ex.grad_scale = 1.0
+                ex.out_keys = self.send[self.off_keys:].data_ptr()
+                ex.out_rows = self.send[self.off_rows:].data_ptr()
+                ex.out_count = self.send[self.off_cnt:].data_ptr()
+                ex.out_cap = cap
+                self.export_params.append(ex)
+                m = e.emb_params[p]  # merge: the same row optimizer, fed by the gathered rows
+                m.skeys, m.svals = self.msk.data_ptr(), self.msv.data_ptr()
+                m.n = self.world * cap
+                m.contrib = self.recv[self.off_rows:].data_ptr()
+                m.contrib_seg = cap
+                m.contrib_seg_stride = self.S
+                m.max_key = e.V
+                m.grad_scale = 1.0 / self.world
+                e.dense_apply_params[p].apply = 1
+                e.dense_apply_params[p].grads = self.mlp_sum.data_ptr()
+                e.dense_apply_params[p].grad_scale = 1.0 / self.world
+            self.recv2d = self.recv.view(self.world, self.S)
+        for p in range(2):
+            e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
+        self._graphs = {}
+        self._warm = 0
+
+    # ---- batch feeding (delegated) ------------------------------------------------------------
+    def attach_pool(self, ids, vals, labels, start: int = 0):
+        self.eng.attach_pool(ids, vals, labels, start)
+        self._graphs = {}
+
+    def push_batch(self, ids, vals, labels):
+        self.eng.push_batch(ids, vals, labels)
+
+    def load_batch(self, ids, vals, labels=None):
+        self.eng.load_batch(ids, vals, labels)
+
+    def set_lr_scale(self, s: float) -> None:
+        self.eng.set_lr_scale(s)
+        if self.mode == "dp":
+            for p in range(2):
+                self.export_params[p].opt = self.eng.emb_params[p].opt
+        self._graphs = {}
+
+    # ---- step phases ---------------------------------------------------------------------------
+    def _phase_a(self, p: int):
+        e = self.eng
+        side = e._fork_next(p)
+        e._enqueue_forward_backward(p)
+        s = e.stream_ptr
+        if self.mode == "dense_dp":
+            e.H.emb_rows_update(e.emb_params[p], s)  # mode 1: Σ rows → dense grad table
+        else:
+            self.send_count.zero_()
+            e.H.emb_rows_update(self.export_params[p], s)
+        e._join(side)
+
+    def _exchange(self):
+        if self.mode == "dense_dp":
+            _all_reduce(self.bucket)
+        else:
+            _all_gather_flat(self.recv, self.send)
+
+    def _phase_b(self, p: int):
+        e = self.eng
+        s = e.stream_ptr
+        if self.mode == "dense_dp":
+            e.H.dense_apply(e.dense_apply_params[p], s)
+            e.H.emb_dense_update(e.emb_dense_params[p], s)
+            return
+        P = e.layout.total
+        torch.sum(self.recv2d[:, :P], dim=0, out=self.mlp_sum)  # rank order: deterministic
+        e.H.dense_apply(e.dense_apply_params[p], s)
+        counts = self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, :1]
+        keys = self.recv2d[:, self.off_keys:self.off_keys + self.cap].contiguous().view(torch.int32)
+        self.mkeys.view(self.world, self.cap).copy_(
+            torch.where(self.col[None, :] < counts, keys, torch.full_like(keys, e.V)))
+        e.H.sort_pairs_iota(self.merge_temp.data_ptr(), self.merge_temp.numel(), self.mkeys.data_ptr(),
+                            self.msk.data_ptr(), self.msv.data_ptr(), self.world * self.cap, self.merge_bits, s)
+        e.H.emb_rows_update(e.emb_params[p], s)
+
+    def _run(self, key, fn):
+        if not self.use_graph or self._warm < 4:
+            fn()
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(g):
+                fn()
+            self._graphs[key] = g
+        g.replay()
+
+    def train_step(self) -> None:
+        e = self.eng
+        if not e._primed:
+            e.prime()
+        p = e._i % 2
+        self._run(("a", p), lambda: self._phase_a(p))
+        self._exchange()
+        self._run(("b", p), lambda: self._phase_b(p))
+        self._warm += 1
+        e._i += 1
+
+    def overflowed(self) -> bool:
+        """True if any rank produced more unique rows than the exchange capacity (never with the default cap)."""
+        if self.mode != "dp":
+            return False
+        c = self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, 0]
+        return bool((c > self.cap).any())
+
+    # ---- delegation ----------------------------------------------------------------------------
+    def __getattr__(self, name):
+        return getattr(self.eng, name)

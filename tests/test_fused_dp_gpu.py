@@ -1,0 +1,82 @@
+"""Fused data-parallel step (2 ranks sharing one GPU over gloo) ≡ single-GPU step on the union batch."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _cfg():
+    from rocfm.models.deepfm import ModelSpec
+    from rocfm.optim import OptHParams
+
+    spec = ModelSpec(feature_size=4000, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[1.0, 1.0],
+                     l2_reg=1e-3)
+    return spec, OptHParams(name="Adam", lr=1e-3)
+
+
+def _batches(B, n, seed):
+    from rocfm.data.synthetic import SyntheticCriteo
+
+    g = torch.Generator().manual_seed(seed)
+    gen = SyntheticCriteo(4000, 39, seed=seed)
+    return [gen.batch(B, "cpu", g) for _ in range(n)]
+
+
+def _worker(rank, world, port, mode, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.dp import FusedDataParallel
+
+    spec, hp = _cfg()
+    B = 64
+    eng = FusedDataParallel(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3),
+                            embedding_update="exact" if mode == "dense_dp" else "sparse", mode=mode,
+                            use_graph=False)
+    batches = _batches(2 * B, 3, 11)
+    pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
+            for b in batches]
+    eng.attach_pool(torch.stack([x[0] for x in pool]).cuda(), torch.stack([x[1] for x in pool]).cuda(),
+                    torch.stack([x[2] for x in pool]).cuda())
+    for _ in range(3):
+        eng.train_step()
+    torch.cuda.synchronize()
+    if rank == 0:
+        torch.save({"emb": eng.emb.cpu(), "dense": eng.dense.cpu()}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["dp", "dense_dp"])
+def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode):
+    out = str(tmp_path / "dp.pt")
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True, start_method="spawn")
+    dp = torch.load(out, weights_only=True)
+    from rocfm.models.deepfm import init_params
+    from rocfm.models.fused import FusedDeepFM
+
+    spec, hp = _cfg()
+    single = FusedDeepFM(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
+                         embedding_update="exact" if mode == "dense_dp" else "sparse")
+    batches = _batches(128, 3, 11)
+    single.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
+                       torch.stack([b[2] for b in batches]).cuda())
+    for _ in range(3):
+        single.train_step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dp["dense"], single.dense.cpu(), rtol=2e-3, atol=2e-5)
+    torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=2e-5)

@@ -91,10 +91,10 @@ def test_fused_adam_two_steps_and_graph_replay():
     ids, vals, labels = _batch(B, F, V, gen)
     a = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 11), use_graph=False)
     b = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 11), use_graph=True)
+    batch = (ids.to(dev), vals.to(dev), labels.to(dev))
     for eng in (a, b):
-        eng.load_batch(ids.to(dev), vals.to(dev), labels.to(dev))
-        for _ in range(5):  # graph engine: 2 eager warm-up steps, capture, replays
-            eng.train_step()
+        for _ in eng.train_on([batch] * 5):  # graph engine: 2 eager warm-up steps, capture, replays
+            pass
     torch.cuda.synchronize()
     # deterministic kernels (no atomics): graph replay == eager, bitwise
     assert torch.equal(a.emb, b.emb)
