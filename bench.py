@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--steps_per_graph", type=int, default=8, help="fused engine: steps captured per HIP graph")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json_out", default="")
     return ap.parse_args()
@@ -107,8 +108,12 @@ def main():
 
         eng.attach_pool(pool_ids, pool_vals, pool_labels)
 
-        def step(i):
-            eng.train_step()
+        def run(n):
+            if hasattr(eng, "train_steps"):
+                eng.train_steps(n, a.steps_per_graph)
+            else:
+                for _ in range(n):
+                    eng.train_step()
     else:
         from rocfm.models.torch_engine import TorchDeepFM
 
@@ -118,22 +123,22 @@ def main():
 
             attach_torch_dp(eng, a.embedding_update)
 
-        def step(i):
-            ids, vals, labels = pool[i % len(pool)]
-            eng.train_step(ids, vals, labels)
+        def run(n, _it=[0]):
+            for _ in range(n):
+                ids, vals, labels = pool[_it[0] % len(pool)]
+                eng.train_step(ids, vals, labels)
+                _it[0] += 1
 
     if world > 1 and hasattr(eng, "set_lr_scale"):
         eng.set_lr_scale(float(world))  # Horovod linear LR scaling (HVD:171)
 
-    for i in range(a.warmup):
-        step(i)
+    run(a.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i)
+    run(a.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

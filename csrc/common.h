@@ -22,6 +22,15 @@
     if (!(cond)) throw std::invalid_argument(std::string(msg));   \
   } while (0)
 
+// Diagnostic phase stamps (cdna guide §7 "In-kernel stamps"): when a kernel's `stamps` pointer is
+// non-null, thread 0 of each workgroup records the 100 MHz real-time counter at phase boundaries
+// into stamps[blockIdx.x * 16 + i].  Null in production launches (one uniform branch per phase).
+#define ROCFM_STAMP(ptr, i)                                                               \
+  do {                                                                                    \
+    if ((ptr) != nullptr && threadIdx.x == 0)                                             \
+      (ptr)[blockIdx.x * 16 + (i)] = (unsigned long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 namespace rocfm {
 
 constexpr int kWave = 64;
@@ -58,6 +67,15 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)) and
+// leaves its global stores in flight (no vmcnt(0)), unlike __syncthreads().  Valid where no wave
+// reads, within the kernel, global memory another wave of the workgroup wrote (the fused kernels
+// exchange data between waves only through LDS).  Global-load results are still waited for by the
+// compiler at their first use.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // Wave-wide reductions (64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {

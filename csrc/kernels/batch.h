@@ -1,6 +1,7 @@
 // Parameter block of the batch-fetch kernel (batch.hip).
 #pragma once
 #include "../common.h"
+#include "optim.h"
 
 namespace rocfm {
 
@@ -19,6 +20,9 @@ struct FetchParams {
   int32_t* ids;
   float* vals;
   float* labels;
+  float* lrt_dst;  // nullable: lr_t for the step published in step_dst (Adam bias correction)
+  float lr, beta1, beta2;
+  int opt_type;
 };
 
 void launch_fetch_batch(const FetchParams& p, hipStream_t stream);

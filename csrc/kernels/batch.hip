@@ -32,7 +32,9 @@ __global__ __launch_bounds__(256) void fetch_batch_kernel(const FetchParams p) {
     p.labels[i] = p.labels_pool[b * p.B + i];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (p.cur_dst) *p.cur_dst = *p.cur_src + p.advance;
-    if (p.step_dst) *p.step_dst = *p.step_src + p.step_advance;
+    const int64_t st = *p.step_src + p.step_advance;
+    if (p.step_dst) *p.step_dst = st;
+    if (p.lrt_dst) *p.lrt_dst = p.opt_type == kAdam ? adam_lr_t(p.lr, p.beta1, p.beta2, st) : p.lr;
   }
 }
 

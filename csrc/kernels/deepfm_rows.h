@@ -7,12 +7,14 @@ namespace rocfm {
 
 constexpr int kMaxHidden = 6;  // hidden MLP layers supported by the fused engine
 constexpr int kRowTile = 16;   // rows per workgroup = one 16-row MFMA M tile
-constexpr int kRowThreads = 256;
+constexpr int kRowThreads = 512;  // 8 waves
 
 struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
   int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32;
   int lda[kMaxHidden + 1];  // bf16 row stride of each activation tile
   int ldz;                  // bf16 row stride of the dz ping-pong tiles
+  int prm;                  // f32 block of small parameters staged at kernel start:
+  int prm_bias[kMaxHidden], prm_wout, prm_bout, prm_fmb, prm_lab, prm_n;  // (float offsets within it)
   int total;
 };
 
@@ -31,6 +33,7 @@ struct RowsParams {
   float keep[kMaxHidden];
   int dims[kMaxHidden + 1];  // dims[0] = round_up(F*K, 32); dims[l>0] = hidden width padded to 32
   int nl, F, K, Kp, B, Bp;   // B valid rows; Bp = padded rows = leading dim of actT/dzT
+  uint32_t magicF;           // floor(2^32/F)+1 (set by the launcher)
   float inv_scale;           // dL/dy scale (1/B_local)
   int train, loss_type;      // loss_type 0 log_loss, 1 square_loss
   uint64_t seed;
@@ -43,6 +46,8 @@ struct RowsParams {
   uint16_t* actT[kMaxHidden + 1];  // [dims[a]][Bp] bf16, a = 0..nl (train)
   uint16_t* dzT[kMaxHidden + 1];   // [dims[a]][Bp] bf16, a = 1..nl (train)
   RowsLds lds;
+  unsigned long long* stamps;  // diagnostic (nullable)
+  int force_generic;           // 1: never use a compile-time-shape instantiation (tests)
 };
 
 struct WgradParams {
@@ -64,6 +69,7 @@ struct WgradParams {
   OptParams opt;
   const int64_t* step;
   float grad_scale;
+  unsigned long long* stamps;  // diagnostic (nullable)
 };
 
 struct DenseApplyParams {

@@ -1,7 +1,7 @@
 // DeepFM fused row-tile kernel: the whole per-example part of a training step in ONE launch.
 //
-// One 256-thread workgroup owns 16 consecutive examples (one MFMA M-tile) and runs, entirely
-// out of LDS:
+// One 512-thread workgroup (8 waves) owns 16 consecutive examples (one MFMA M-tile) and runs,
+// entirely out of LDS:
 //   A  gather fm_v/fm_w rows (f32, 16-B vector loads) → e = V[id]·x, h0 = bf16(e)  (PS:207-213)
 //   B  S = Σ_f e, y_v = ½Σ_k(S² − Σ_f e²), y_w = Σ_f w·x, y_lin = b + y_w + y_v    (PS:214-217)
 //   C  hidden layers: h_{l+1} = dropout(relu(h_l·W_l + c_l)) on v_mfma_f32_16x16x32_bf16
@@ -10,9 +10,21 @@
 //   E  backward data path through the MLP (dz_l = 1[h_l>0]/keep · dh_l, dh = dz·Wᵀ)
 //   F  FM backward: de = g·(S − e) + dh0, per-lookup gradient row [x·de | g·x]
 // It writes bf16 activations/dz transposed ([feature][batch]) for the weight-gradient kernel
-// (mlp_wgrad.hip) and the per-lookup gradient rows for the sort-based embedding update
-// (emb_update.hip).  Nothing here reduces across examples, so no atomics and no inter-workgroup
-// communication are needed.  Weights are read from L2 as MFMA B fragments (16 B per lane).
+// (mlp_wgrad.hip) and the per-lookup gradient rows for the embedding update (emb_update.hip).
+// Nothing reduces across examples, so there are no atomics and no inter-workgroup hand-offs.
+//
+// At the reference's 1024-row batches the kernel is LATENCY-bound (64 workgroups for 256 CUs):
+// its time is the chain of dependent memory round trips plus each wave's serial instruction
+// stream.  So:
+//  * every phase issues all of its global loads before consuming any (flattened gather items);
+//  * barriers wait for LDS only (lds_barrier): global stores stay in flight across phases;
+//  * small parameters (biases, deep_out, labels) are staged into LDS in phase 0;
+//  * the shape is a template parameter.  For the common model shapes (CtShape instantiations)
+//    every loop unrolls, all index arithmetic folds, and EVERY layer's MFMA weight fragments are
+//    prefetched into registers one or more phases before they are needed (forward layer 0 at
+//    kernel entry, under the id/value staging + gather; the backward fragments during the
+//    forward), so no GEMM phase waits on memory.  Other shapes run the same code with a runtime
+//    shape (RtShape) and per-GEMM batched fragment loads.
 #include "deepfm_rows.h"
 
 namespace rocfm {
@@ -25,21 +37,26 @@ __device__ __forceinline__ uint32_t pick4(const Philox4& b, int i) {
   return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
 }
 
-// acc[j] = A(16 × Kd, LDS bf16, row stride lda) · B(Kd × 16) for the n-tiles nt = nt0 + 4j (j < NTW)
-// owned by this wave.  B fragments come from global/L2: tile nt, k-step ks at
-// Bt + (nt*16 + (lane&15))*ldb + ks + 8*(lane>>4).  Latency-oriented: every batch issues KU k-steps
-// × NTW tiles of 16-B loads before the first MFMA; out-of-range k-steps load a clamped (valid)
-// address and are zeroed on the VALUE (no per-load predication — cdna guide §5 trap (c)).
+// x / F for x < 4096, F <= 64 (host-checked): magic = floor(2^32 / F) + 1
+__device__ __forceinline__ int fdiv(int x, uint32_t magic) { return (int)__umulhi((uint32_t)x, magic); }
+
+constexpr int kWaves = kRowThreads / 64;
+
+// acc[j] = A(16 × Kd, LDS bf16, row stride lda) · B(Kd × 16) for the n-tiles nt = nt0 + step*j
+// (j < NTW).  B fragments come from global/L2: tile nt, k-step ks at
+// Bt + (nt*16 + (lane&15))*ldb + ks + 8*(lane>>4).  Every batch issues KU k-steps × NTW tiles of
+// 16-B loads before the first MFMA; out-of-range k-steps load a clamped (valid) address and are
+// zeroed on the VALUE (no per-load predication — cdna guide §5 trap (c)).
 template <int NTW, int KU>
 __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const uint16_t* Bt, int ldb, int ntiles,
-                                             int nt0, int Kd, int lane, f32x4 (&acc)[NTW]) {
+                                             int nt0, int step, int Kd, int lane, f32x4 (&acc)[NTW]) {
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
   const uint16_t* bp[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    const int nt = min(nt0 + 4 * j, ntiles - 1);
+    const int nt = min(nt0 + step * j, ntiles - 1);
     bp[j] = Bt + (size_t)(nt * 16 + (lane & 15)) * ldb + 8 * (lane >> 4);
   }
   const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -60,14 +77,48 @@ __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const u
     for (int u = 0; u < KU; ++u)
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
-        if (nt0 + 4 * j < ntiles) acc[j] = mfma16x16x32(a[u], b[j][u], acc[j]);
+        if (nt0 + step * j < ntiles) acc[j] = mfma16x16x32(a[u], b[j][u], acc[j]);
   }
 }
 
+// ---- shapes ----------------------------------------------------------------------------------
+// Runtime shape: any F/K/MLP the host validated.
+struct RtShape {
+  static constexpr bool kStatic = false;
+  static constexpr int KSF0 = 1, KSF1 = 1, KSF2 = 1, NJB0 = 1, KSB0 = 1, KSB1 = 1, KSB2 = 1;
+  int F, K, nl, d[kMaxHidden + 1];
+  __device__ explicit RtShape(const RowsParams& p) : F(p.F), K(p.K), nl(p.nl) {
+#pragma unroll
+    for (int i = 0; i <= kMaxHidden; ++i) d[i] = p.dims[i];
+  }
+  __device__ int dim(int l) const { return d[l]; }
+};
+
+// Compile-time shape: F fields, K embedding dims, hidden widths D1 ≥ … (0 = absent), ≤ 3 layers of
+// ≤ 128 units, F·K ≤ 512 (host-checked).  Fragment-prefetch counts per wave:
+//   forward layer l : one 16-column tile (wave w owns tile w), dims[l]/32 k-steps   → KSF_l
+//   backward li     : tiles w, w+8, … of dims[li]/16 (NJB_li of them), dims[li+1]/32 k-steps → KSB_li
+template <int F_, int K_, int D1, int D2, int D3>
+struct CtShape {
+  static constexpr bool kStatic = true;
+  static constexpr int F = F_, K = K_;
+  static constexpr int nl = D3 ? 3 : (D2 ? 2 : 1);
+  static constexpr int D0 = (F_ * K_ + 31) / 32 * 32;
+  __device__ static constexpr int dim(int l) { return l == 0 ? D0 : l == 1 ? D1 : l == 2 ? D2 : D3; }
+  static constexpr int KSF0 = D0 / 32, KSF1 = D1 / 32 > 0 ? D1 / 32 : 1, KSF2 = D2 / 32 > 0 ? D2 / 32 : 1;
+  static constexpr int NJB0 = (D0 / 16 + kWaves - 1) / kWaves;
+  static constexpr int KSB0 = D1 / 32, KSB1 = D2 / 32 > 0 ? D2 / 32 : 1, KSB2 = D3 / 32 > 0 ? D3 / 32 : 1;
+  __device__ explicit CtShape(const RowsParams&) {}
+  static_assert(D0 <= 512 && D1 <= 128 && D2 <= 128 && D3 <= 128, "CtShape limits");
+  static_assert(D1 % 32 == 0 && D2 % 32 == 0 && D3 % 32 == 0, "hidden dims padded to 32");
+};
+
 }  // namespace
 
+template <int KP4, class SH>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SH sh(p);
   const RowsLds& L = p.lds;
   int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
   float* s_vals = reinterpret_cast<float*>(smem + L.vals);
@@ -76,45 +127,68 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   float* s_ylin = reinterpret_cast<float*>(smem + L.ylin);
   float* s_g = reinterpret_cast<float*>(smem + L.g);
   float* s_f32 = reinterpret_cast<float*>(smem + L.f32);  // e (forward) / dh0 (backward), stride dims[0]
+  float* s_prm = reinterpret_cast<float*>(smem + L.prm);
 
+  constexpr int Kp = KP4 * 4;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int row0 = blockIdx.x * kRowTile;
-  const int F = p.F, K = p.K, Kp = p.Kp, D0 = F * K, D0p = p.dims[0];
+  const int F = sh.F, K = sh.K, NL = sh.nl;
+  const int D0 = F * K, D0p = sh.dim(0);
+  const uint32_t magicF = p.magicF;
   const int Bp = p.Bp;
+  const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
+  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  ROCFM_STAMP(p.stamps, 0);
+
+  // ---- static shapes: prefetch the forward layer-0 weight fragments at kernel entry --------------
+  bf16x8 fw0[SH::KSF0];
+  if constexpr (SH::kStatic) {
+    const bool own = wave < sh.dim(1) / 16;
+    const uint16_t* bp = p.WT[0] + (size_t)(min(wave, sh.dim(1) / 16 - 1) * 16 + (lane & 15)) * sh.dim(0) +
+                         8 * (lane >> 4);
+#pragma unroll
+    for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(bp + 32 * u);
+    (void)own;
+  }
   const uint32_t step = p.step ? (uint32_t)(*p.step) : 0u;
 
-  // ---- phase 0: stage ids / values ------------------------------------------------------------
+  // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
   for (int i = t; i < kRowTile * F; i += kRowThreads) {
-    const int r = i / F, gr = row0 + r;
-    const bool valid = gr < p.B;
+    const bool valid = row0 + fdiv(i, magicF) < p.B;
     s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
     s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
   }
-  __syncthreads();
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+    for (int c = t; c < sh.dim(l + 1); c += kRowThreads) s_prm[L.prm_bias[l] + c] = p.bias[l][c];
+  for (int c = t; c < sh.dim(NL); c += kRowThreads) s_prm[L.prm_wout + c] = p.w_out[c];
+  if (t == 0) {
+    s_prm[L.prm_bout] = *p.b_out;
+    s_prm[L.prm_fmb] = *p.fm_bias;
+  }
+  if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
+  lds_barrier();
+  ROCFM_STAMP(p.stamps, 1);
 
   // ---- phase A: gather rows, e = V·x (f32 scratch), h0 = bf16(e), w·x ---------------------------
-  // Work items (row, field, float4-column) are flattened so each thread issues up to 8 independent
-  // 16-B row loads before consuming any (one HBM/MALL latency for the whole tile's gather).
   {
     uint16_t* h0 = reinterpret_cast<uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
-    const int KP4 = Kp >> 2;
     const int nitems = kRowTile * F * KP4;
-    const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
-    for (int base = 0; base < nitems; base += kRowThreads * 8) {
-      float4 v[8];
+    for (int base = 0; base < nitems; base += kRowThreads * 4) {
+      float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitems - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
         v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int idx = base + u * kRowThreads + t;
         if (idx < nitems) {
           const int rf = idx / KP4, c4 = idx - rf * KP4;
-          const int r = rf / F, f = rf - r * F;
+          const int r = fdiv(rf, magicF), f = rf - r * F;
           const float x = s_vals[rf];
           const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
@@ -131,17 +205,21 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         }
       }
     }
-    const int r = t >> 4, q = t & 15;
-    for (int c = D0 + q; c < D0p; c += 16) h0[r * lda + c] = 0;
+    for (int i = t; i < kRowTile * (D0p - D0); i += kRowThreads) {
+      const int r = i / (D0p - D0), c = D0 + i - r * (D0p - D0);
+      h0[r * lda + c] = 0;
+    }
   }
-  __syncthreads();
+  lds_barrier();
+  ROCFM_STAMP(p.stamps, 2);
 
-  // ---- phase B: FM second order + first order -------------------------------------------------
+  // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
   {
-    const int r = t >> 4, q = t & 15;
+    const int r = t >> 5, q = t & 31;
     float cterm = 0.f, yw = 0.f;
-    for (int k = q; k < K; k += 16) {
+    for (int k = q; k < K; k += 32) {
       float S = 0.f, Q = 0.f;
+#pragma unroll 4
       for (int f = 0; f < F; ++f) {
         const float e = s_f32[r * D0p + f * K + k];
         S += e;
@@ -150,13 +228,13 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       s_S[r * K + k] = S;
       cterm += S * S - Q;
     }
-    for (int f = q; f < F; f += 16) yw += s_wx[r * F + f];
+    for (int f = q; f < F; f += 32) yw += s_wx[r * F + f];
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
+    for (int o = 16; o > 0; o >>= 1) {
       cterm += __shfl_xor(cterm, o, 64);
       yw += __shfl_xor(yw, o, 64);
     }
-    if (q == 0) s_ylin[r] = *p.fm_bias + yw + 0.5f * cterm;
+    if (q == 0) s_ylin[r] = s_prm[L.prm_fmb] + yw + 0.5f * cterm;
   }
   if (p.train) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
@@ -171,62 +249,114 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   }
 
-  // ---- phase C: hidden layers on MFMA --------------------------------------------------------
-  for (int l = 0; l < p.nl; ++l) {
-    const int Din = p.dims[l], Dout = p.dims[l + 1];
-    const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + L.act[l]);
-    uint16_t* O = reinterpret_cast<uint16_t*>(smem + L.act[l + 1]);
-    const int lda = L.lda[l], ldo = L.lda[l + 1];
-    const uint16_t* W = p.WT[l];
-    const float keep = p.keep[l];
-    const bool drop = p.train && keep < 1.f;
-    const float inv_keep = 1.f / keep;
-    __syncthreads();  // previous layer's tile (and phase A/B) complete
-    const int ntiles = Dout >> 4;
-    for (int nt0 = wave; nt0 < ntiles; nt0 += 8) {
-      f32x4 accs[2];
-      rowtile_gemm<2, 8>(A, lda, W, Din, ntiles, nt0, Din, lane, accs);
+  // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
+  bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
+  bf16x8 bw0[SH::NJB0][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
+  if constexpr (SH::kStatic) {
+    if constexpr (SH::nl >= 2) {
+      const uint16_t* bp = p.WT[1] + (size_t)(min(wave, sh.dim(2) / 16 - 1) * 16 + (lane & 15)) * sh.dim(1) +
+                           8 * (lane >> 4);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int nt = nt0 + 4 * j;
-        if (nt >= ntiles) continue;
-        const f32x4 acc = accs[j];
-        const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
-        const float bc = p.bias[l][c];
-        Philox4 bits{0u, 0u, 0u, 0u};
-        if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
-        float hv[4];
+      for (int u = 0; u < SH::KSF1; ++u) fw1[u] = ld_frag(bp + 32 * u);
+    }
+    if constexpr (SH::nl >= 3) {
+      const uint16_t* bp = p.WT[2] + (size_t)(min(wave, sh.dim(3) / 16 - 1) * 16 + (lane & 15)) * sh.dim(2) +
+                           8 * (lane >> 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float a = fmaxf(acc[i] + bc, 0.f);
-          if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
-          if (row0 + rb + i >= p.B) a = 0.f;
-          hv[i] = a;
-          O[(rb + i) * ldo + c] = f2bf(a);
-        }
-        if (p.train)
-          *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
-              make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+      for (int u = 0; u < SH::KSF2; ++u) fw2[u] = ld_frag(bp + 32 * u);
+    }
+    if (p.train) {
+      // backward of layer 0: dh0 tiles w + 8j of dims[0]/16, k = dims[1]
+#pragma unroll
+      for (int j = 0; j < SH::NJB0; ++j) {
+        const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
+        const uint16_t* bp = p.Wb[0] + (size_t)(nt * 16 + (lane & 15)) * sh.dim(1) + 8 * (lane >> 4);
+#pragma unroll
+        for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(bp + 32 * u);
+      }
+      if constexpr (SH::nl >= 2) {
+        const uint16_t* bp = p.Wb[1] + (size_t)(min(wave, sh.dim(1) / 16 - 1) * 16 + (lane & 15)) * sh.dim(2) +
+                             8 * (lane >> 4);
+#pragma unroll
+        for (int u = 0; u < SH::KSB1; ++u) bw1[u] = ld_frag(bp + 32 * u);
+      }
+      if constexpr (SH::nl >= 3) {
+        const uint16_t* bp = p.Wb[2] + (size_t)(min(wave, sh.dim(2) / 16 - 1) * 16 + (lane & 15)) * sh.dim(3) +
+                             8 * (lane >> 4);
+#pragma unroll
+        for (int u = 0; u < SH::KSB2; ++u) bw2[u] = ld_frag(bp + 32 * u);
       }
     }
   }
-  __syncthreads();
 
+  // ---- phase C: hidden layers on MFMA -----------------------------------------------------------
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int Din = sh.dim(l), Dout = sh.dim(l + 1);
+    const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + L.act[l]);
+    uint16_t* O = reinterpret_cast<uint16_t*>(smem + L.act[l + 1]);
+    const int lda = L.lda[l], ldo = L.lda[l + 1];
+    const float keep = p.keep[l];
+    const bool drop = p.train && keep < 1.f;
+    const float inv_keep = 1.f / keep;
+    lds_barrier();  // previous layer's tile (and phase A/B) complete
+    ROCFM_STAMP(p.stamps, 3 + l);
+    const int ntiles = Dout >> 4;
+    for (int nt = wave; nt < ntiles; nt += kWaves) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (SH::kStatic) {
+        const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
+        if (l == 0) {
+#pragma unroll
+          for (int u = 0; u < SH::KSF0; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
+        } else if (l == 1) {
+#pragma unroll
+          for (int u = 0; u < SH::KSF1; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw1[u], acc);
+        } else {
+#pragma unroll
+          for (int u = 0; u < SH::KSF2; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw2[u], acc);
+        }
+      } else {
+        f32x4 accs[1];
+        rowtile_gemm<1, 16>(A, lda, p.WT[l], Din, ntiles, nt, kWaves, Din, lane, accs);
+        acc = accs[0];
+      }
+      const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
+      const float bc = s_prm[L.prm_bias[l] + c];
+      Philox4 bits{0u, 0u, 0u, 0u};
+      if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
+      float hv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = fmaxf(acc[i] + bc, 0.f);
+        if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
+        if (row0 + rb + i >= p.B) a = 0.f;
+        hv[i] = a;
+        O[(rb + i) * ldo + c] = f2bf(a);
+      }
+      if (p.train)
+        *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
+            make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+    }
+  }
+  lds_barrier();
+
+  ROCFM_STAMP(p.stamps, 9);
   // ---- phase D: output layer + loss head (wave 0) ----------------------------------------------
   if (wave == 0) {
-    const int Dn = p.dims[p.nl];
-    const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[p.nl]);
-    const int ldh = L.lda[p.nl];
+    const int Dn = sh.dim(NL);
+    const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[NL]);
+    const int ldh = L.lda[NL];
     const int r = lane >> 2, q = lane & 3;
     float s = 0.f;
-    for (int c = q; c < Dn; c += 4) s += bf2f(H[r * ldh + c]) * p.w_out[c];
+    for (int c = q; c < Dn; c += 4) s += bf2f(H[r * ldh + c]) * s_prm[L.prm_wout + c];
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     if (q == 0) {
       const int gr = row0 + r;
       const bool valid = gr < p.B;
-      const float y = s_ylin[r] + s + *p.b_out;
-      const float tl = valid ? p.labels[gr] : 0.f;
+      const float y = s_ylin[r] + s + s_prm[L.prm_bout];
+      const float tl = s_prm[L.prm_lab + r];
       const float pr = 1.f / (1.f + __expf(-y));
       float loss, g;
       if (p.loss_type == 0) {
@@ -247,20 +377,30 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   }
   if (!p.train) return;
-  __syncthreads();
+
+  // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E)
+  const int nitemsF = kRowTile * F * KP4;
+  float4 rowsF[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = min(u * kRowThreads + t, nitemsF - 1);
+    const int rf = idx / KP4, c4 = idx - rf * KP4;
+    rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+  }
+  lds_barrier();
 
   // ---- phase E: backward through the MLP ------------------------------------------------------
   uint16_t* dz_cur = reinterpret_cast<uint16_t*>(smem + L.dzA);
   uint16_t* dz_nxt = reinterpret_cast<uint16_t*>(smem + L.dzB);
   const int ldz = L.ldz;
   {
-    const int a = p.nl, Dn = p.dims[a];
+    const int a = NL, Dn = sh.dim(a);
     const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[a]);
     const int ldh = L.lda[a];
     const float inv_keep = 1.f / p.keep[a - 1];
     for (int it = t; it < Dn * 4; it += kRowThreads) {
-      const int c = it % Dn, rg = it / Dn;
-      const float wc = p.w_out[c];
+      const int rg = it / Dn, c = it - rg * Dn;
+      const float wc = s_prm[L.prm_wout + c];
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -273,18 +413,43 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     }
   }
-  for (int a = p.nl; a >= 1; --a) {
-    __syncthreads();
-    const int li = a - 1, Dout = p.dims[a], Din = p.dims[li];
-    const uint16_t* W = p.Wb[li];  // [Din][Dout]
-    const int ntiles = Din >> 4;
-    for (int nt0 = wave; nt0 < ntiles; nt0 += 16) {
-      f32x4 accs[4];
-      rowtile_gemm<4, 4>(dz_cur, ldz, W, Dout, ntiles, nt0, Dout, lane, accs);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nt = nt0 + 4 * j;
+  for (int a = NL; a >= 1; --a) {
+    lds_barrier();
+    if (a == NL) ROCFM_STAMP(p.stamps, 10);
+    const int li = a - 1, Dout = sh.dim(a), Din = sh.dim(li);
+    const int ntiles = Din >> 4;
+    constexpr int NJ = SH::kStatic ? (SH::NJB0 > 1 ? SH::NJB0 : 1) : 4;
+    for (int nt0 = wave; nt0 < ntiles; nt0 += NJ * kWaves) {
+      f32x4 accs[NJ];
+      if constexpr (SH::kStatic) {
+        const uint16_t* ap = dz_cur + (lane & 15) * ldz + 8 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) accs[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (li == 0) {
+#pragma unroll
+          for (int u = 0; u < SH::KSB0; ++u) {
+            const bf16x8 av = ld_frag(ap + 32 * u);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              if (j < SH::NJB0 && nt0 + kWaves * j < ntiles) accs[j] = mfma16x16x32(av, bw0[j][u], accs[j]);
+          }
+        } else if (li == 1) {
+#pragma unroll
+          for (int u = 0; u < SH::KSB1; ++u) accs[0] = mfma16x16x32(ld_frag(ap + 32 * u), bw1[u], accs[0]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < SH::KSB2; ++u) accs[0] = mfma16x16x32(ld_frag(ap + 32 * u), bw2[u], accs[0]);
+        }
+        (void)zero8;
+      } else {
+        rowtile_gemm<NJ, 4>(dz_cur, ldz, p.Wb[li], Dout, ntiles, nt0, kWaves, Dout, lane, accs);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int nt = nt0 + kWaves * j;
         if (nt >= ntiles) continue;
+        if (SH::kStatic && li > 0 && j > 0) continue;
         const f32x4 acc = accs[j];
         const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
         if (li >= 1) {
@@ -310,42 +475,42 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     dz_cur = dz_nxt;
     dz_nxt = tmp;
   }
-  __syncthreads();
+  lds_barrier();
+  ROCFM_STAMP(p.stamps, 11);
 
   // ---- phase F: FM backward → per-lookup gradient rows -----------------------------------------
-  {
-    const int KP4 = Kp >> 2;
-    const int nitems = kRowTile * F * KP4;
-    const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
-    for (int base = 0; base < nitems; base += kRowThreads * 8) {
-      float4 v[8];
+  for (int base = 0; base < nitemsF; base += kRowThreads * 4) {
+    if (base > 0) {  // more than 4 items per thread (large F·Kp): load this batch now
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int idx = min(base + u * kRowThreads + t, nitems - 1);
+      for (int u = 0; u < 4; ++u) {
+        const int idx = min(base + u * kRowThreads + t, nitemsF - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
-        v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int idx = base + u * kRowThreads + t;
-        if (idx >= nitems) continue;
-        const int rf = idx / KP4, c4 = idx - rf * KP4;
-        const int r = rf / F, f = rf - r * F;
-        if (row0 + r >= p.B) continue;
-        const float g = s_g[r], x = s_vals[rf];
-        const float* S = s_S + r * K;
-        const float* dh = s_f32 + r * D0p + f * K;
-        const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        float o[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int k = c4 * 4 + c;
-          o[c] = (k < K) ? x * (g * (S[k] - vv[c] * x) + dh[k]) : ((k == K) ? g * x : 0.f);
-        }
-        reinterpret_cast<float4*>(p.contrib + ((size_t)(row0 + r) * F + f) * Kp)[c4] = make_float4(o[0], o[1], o[2], o[3]);
+        rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = base + u * kRowThreads + t;
+      if (idx >= nitemsF) continue;
+      const int rf = idx / KP4, c4 = idx - rf * KP4;
+      const int r = fdiv(rf, magicF), f = rf - r * F;
+      if (row0 + r >= p.B) continue;
+      const float g = s_g[r], x = s_vals[rf];
+      const float* S = s_S + r * K;
+      const float* dh = s_f32 + r * D0p + f * K;
+      const float vv[4] = {rowsF[u].x, rowsF[u].y, rowsF[u].z, rowsF[u].w};
+      float o[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = c4 * 4 + c;
+        o[c] = (k < K) ? x * (g * (S[k] - vv[c] * x) + dh[k]) : ((k == K) ? g * x : 0.f);
+      }
+      reinterpret_cast<float4*>(p.contrib + ((size_t)(row0 + r) * F + f) * Kp)[c4] =
+          make_float4(o[0], o[1], o[2], o[3]);
+    }
   }
+  lds_barrier();
+  ROCFM_STAMP(p.stamps, 12);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -372,31 +537,86 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
     if (a > 0 && dims[a] > maxh) maxh = dims[a];
   }
   L.ldz = maxh + 8;
-  L.dzA = take(kRowTile * L.ldz * 2);
-  L.dzB = take(kRowTile * L.ldz * 2);
+  if (2 * L.ldz <= L.lda[0]) {  // h0's tile is dead after the first layer: the dz tiles reuse it
+    L.dzA = L.act[0];
+    L.dzB = L.act[0] + kRowTile * L.ldz * 2;
+  } else {
+    L.dzA = take(kRowTile * L.ldz * 2);
+    L.dzB = take(kRowTile * L.ldz * 2);
+  }
   L.f32 = take(kRowTile * dims[0] * 4);
+  int n = 0;
+  for (int l = 0; l < nl; ++l) {
+    L.prm_bias[l] = n;
+    n += dims[l + 1];
+  }
+  L.prm_wout = n;
+  n += dims[nl];
+  L.prm_bout = n++;
+  L.prm_fmb = n++;
+  L.prm_lab = n;
+  n += kRowTile;
+  L.prm_n = n;
+  L.prm = take(n * 4);
   L.total = off;
   return L;
 }
 
-void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
+template <int KP4, class SH>
+static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
-    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel),
+    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
+  hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
+                     p);
+}
+
+// Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
+// the runtime-shape kernel.
+template <int F, int K, int D1, int D2, int D3>
+static bool try_static(const RowsParams& p, hipStream_t stream) {
+  const int nl = D3 ? 3 : (D2 ? 2 : 1);
+  if (p.F != F || p.K != K || p.nl != nl || p.dims[1] != D1 || (nl >= 2 && p.dims[2] != D2) ||
+      (nl >= 3 && p.dims[3] != D3))
+    return false;
+  constexpr int KP4 = (K + 1 + 3) / 4;
+  launch_rows_t<KP4, CtShape<F, K, D1, D2, D3>>(p, stream);
+  return true;
+}
+
+void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.nl >= 1 && p.nl <= kMaxHidden, "deepfm_rows: 1..6 hidden layers supported");
-  ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= p.K + 1, "deepfm_rows: Kp must be a multiple of 4 and > K");
+  ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= p.K + 1 && p.Kp <= 64, "deepfm_rows: Kp must be a multiple of 4, > K, <= 64");
+  ROCFM_REQUIRE(p.F >= 1 && p.F <= 64, "deepfm_rows: field_size must be in [1, 64]");
   ROCFM_REQUIRE(p.dims[0] % 32 == 0 && p.dims[0] >= p.F * p.K, "deepfm_rows: dims[0] = round_up(F*K, 32)");
   for (int a = 1; a <= p.nl; ++a) ROCFM_REQUIRE(p.dims[a] % 32 == 0, "deepfm_rows: hidden dims padded to 32");
   ROCFM_REQUIRE(p.Bp % kRowTile == 0 && p.Bp >= p.B, "deepfm_rows: Bp must be a multiple of 16 and >= B");
   ROCFM_REQUIRE((p.Bp % 64) == 0 || !p.train, "deepfm_rows: training needs Bp % 64 == 0");
+  p.magicF = (uint32_t)((1ull << 32) / (uint64_t)p.F + 1ull);
   p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
-  const int grid = p.Bp / kRowTile;
-  if (grid == 0) return;
-  hipLaunchKernelGGL(deepfm_rows_kernel, dim3(grid), dim3(kRowThreads), p.lds.total, stream, p);
+  if (p.Bp / kRowTile == 0) return;
+  if (!p.force_generic) {
+    if (try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
+        try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream)) {
+      ROCFM_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N)                          \
+  case N:                                     \
+    launch_rows_t<N, RtShape>(p, stream);     \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("deepfm_rows: unsupported Kp");
+  }
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

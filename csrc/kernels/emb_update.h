@@ -30,6 +30,7 @@ struct EmbUpdateParams {
   int contrib_seg;     // if > 0: lookup j lives at contrib + (j/seg)*seg_stride + (j%seg)*Kp
   long long contrib_seg_stride;  // floats between segments (per-rank blocks of a gathered buffer)
   int out_cap;         // mode 2: capacity of out_keys/out_rows (rows past it are dropped, count kept)
+  unsigned long long* stamps;  // diagnostic (nullable)
 };
 
 struct EmbDenseParams {

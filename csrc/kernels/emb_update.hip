@@ -39,28 +39,6 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
   return make_float4(__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64), __shfl_xor(v.z, d, 64), __shfl_xor(v.w, d, 64));
 }
 
-__device__ __forceinline__ void finish_row(const EmbUpdateParams& p, const OptStep& st, uint32_t key, int col,
-                                           float g, int out_slot) {
-  if (col >= p.K1) return;
-  g *= p.grad_scale;
-  if (p.mode == 2) {
-    if (out_slot < p.out_cap) p.out_rows[(size_t)out_slot * p.Kp + col] = g;
-    return;
-  }
-  const size_t row = (size_t)((key - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
-  const size_t idx = row * p.Kp + col;
-  if (p.mode == 1) {
-    p.dense_grad[idx] = g;
-    return;
-  }
-  float w = p.emb[idx];
-  float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
-  opt_apply(p.opt, st, w, g + p.l2 * w, a, b);
-  p.emb[idx] = w;
-  if (p.s0) p.s0[idx] = a;
-  if (p.s1) p.s1[idx] = b;
-}
-
 }  // namespace
 
 // One workgroup per 256 consecutive sorted entries.  Every thread loads ONE entry's gradient row
@@ -80,6 +58,7 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
   const int cend = min(c0 + kChunk, p.n);
   const int i = c0 + t;
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  ROCFM_STAMP(p.stamps, 0);
 
   // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
   uint32_t key = 0xffffffffu;
@@ -124,31 +103,40 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
   }
   if (t == 0) s_nh = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
   __syncthreads();
+  ROCFM_STAMP(p.stamps, 1);
   const int nh = s_nh;
   if (nh == 0) return;
-  // 4. end of the last run; mode 2 reserves output slots
-  if (wave == 0) {
+  // 4. end of the last run (all 256 threads probe 256 entries per round); mode 2 reserves slots
+  {
     const int last = s_head[nh - 1];
     const uint32_t lk = p.skeys[last];
-    int pos = cend;
-    int end = p.n;
-    if (p.max_key && lk >= p.max_key) pos = p.n;  // sentinel padding sorts last
+    const bool sentinel = p.max_key && lk >= p.max_key;  // sentinel padding sorts last: runs to n
+    int pos = sentinel ? p.n : cend;
+    if (t == 0) s_last_end = p.n;
+    __syncthreads();
     while (pos < p.n) {
-      const int j = pos + lane;
+      const int j = pos + t;
       const bool diff = (j >= p.n) || (p.skeys[j] != lk);
       const unsigned long long dm = __ballot(diff);
-      if (dm) {
-        end = min(pos + __ffsll((long long)dm) - 1, p.n);
+      if (lane == 0) s_wcnt[wave] = dm ? (__ffsll((long long)dm) - 1) : 64;
+      __syncthreads();
+      int found = -1;
+      for (int w = 0; w < 4; ++w)
+        if (s_wcnt[w] < 64) {
+          found = pos + 64 * w + s_wcnt[w];
+          break;
+        }
+      __syncthreads();
+      if (found >= 0) {
+        if (t == 0) s_last_end = min(found, p.n);
         break;
       }
-      pos += 64;
+      pos += kChunk;
     }
-    if (lane == 0) {
-      s_last_end = end;
-      if (p.mode == 2) s_out_base = atomicAdd(p.out_count, nh);
-    }
+    if (t == 0 && p.mode == 2) s_out_base = atomicAdd(p.out_count, nh);
   }
   __syncthreads();
+  ROCFM_STAMP(p.stamps, 2);
   if (t == 0) s_head[nh] = min(s_last_end, cend);
   // 5. continuation of the last run past the chunk: full reductions over following chunks
   const int last_end = s_last_end;
@@ -181,34 +169,71 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
     }
   }
   __syncthreads();
-  // 6. one 16-lane group per owned run: add the wave pieces (+ continuation), apply the optimizer
-  const int grp = t >> 4, q = t & 15;
-  const int Kp = KP4 * 4;
-  for (int r = grp; r < nh; r += 16) {
-    const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
-    const uint32_t kk = p.skeys[s];
-    if (p.max_key && kk >= p.max_key) continue;
-    const int slot = (p.mode == 2) ? s_out_base + r : 0;
-    if (p.mode == 2 && q == 0 && slot < p.out_cap) p.out_keys[slot] = kk;
-    const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
-    for (int col = q; col < Kp; col += 16) {
-      const int u = col >> 2, comp = col & 3;
-      float g = 0.f;
-      for (int w = w0; w <= w1; ++w) {
-        const int lastw = min(e, c0 + 64 * (w + 1)) - 1 - c0;
-        const float4 x = s_rows[lastw * KP4 + u];
-        g += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
+  ROCFM_STAMP(p.stamps, 3);
+  // 6. (run, column) items over all threads: add the run's wave pieces (+ continuation), then the
+  //    optimizer; every thread issues its table/slot loads for up to 4 items before using any.
+  constexpr int Kp = KP4 * 4;
+  const int nitems = nh * Kp;
+  for (int base = 0; base < nitems; base += kChunk * 4) {
+    float w[4], a[4], b[4], g[4];
+    uint32_t kk[4];
+    size_t idx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = min(base + u * kChunk + t, nitems - 1);
+      const int r = it / Kp, col = it - r * Kp;
+      const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
+      kk[u] = p.skeys[s];
+      const bool skip = p.max_key && kk[u] >= p.max_key;
+      const int u4 = col >> 2, comp = col & 3;
+      float acc = 0.f;
+      const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
+      for (int ww = w0; ww <= w1; ++ww) {
+        const int lastw = min(e, c0 + 64 * (ww + 1)) - 1 - c0;
+        const float4 x = s_rows[lastw * KP4 + u4];
+        acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
       }
       if (cont && r == nh - 1) {
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const float4 x = s_cont[w * KP4 + u];
-          g += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
+        for (int ww = 0; ww < 4; ++ww) {
+          const float4 x = s_cont[ww * KP4 + u4];
+          acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
         }
       }
-      finish_row(p, st, kk, col, g, slot);
+      g[u] = acc * p.grad_scale;
+      const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
+      idx[u] = row * Kp + col;
+      if (p.mode == 0) {  // issue the row's parameter + slot loads now
+        w[u] = p.emb[idx[u]];
+        a[u] = p.s0 ? p.s0[idx[u]] : 0.f;
+        b[u] = p.s1 ? p.s1[idx[u]] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = base + u * kChunk + t;
+      if (it >= nitems) continue;
+      const int r = it / Kp, col = it - r * Kp;
+      if ((p.max_key && kk[u] >= p.max_key) || col >= p.K1) continue;
+      if (p.mode == 2) {
+        const int slot = s_out_base + r;
+        if (slot < p.out_cap) {
+          p.out_rows[(size_t)slot * Kp + col] = g[u];
+          if (col == 0) p.out_keys[slot] = kk[u];
+        }
+      } else if (p.mode == 1) {
+        p.dense_grad[idx[u]] = g[u];
+      } else {
+        float ww = w[u], aa = a[u], bb = b[u];
+        opt_apply(p.opt, st, ww, g[u] + p.l2 * ww, aa, bb);
+        p.emb[idx[u]] = ww;
+        if (p.s0) p.s0[idx[u]] = aa;
+        if (p.s1) p.s1[idx[u]] = bb;
+      }
     }
   }
+  __syncthreads();
+  ROCFM_STAMP(p.stamps, 4);
 }
 
 template <int KP4>

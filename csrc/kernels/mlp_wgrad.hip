@@ -39,13 +39,17 @@ __device__ __forceinline__ float dot_bf16x8_f32(uint4 v, const float* g) {
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
-  __shared__ __attribute__((aligned(16))) float s_red[3 * 16 * 64];
+constexpr int kWgThreads = 512;  // 8 waves: each takes 1/8 of the batch
+
+__global__ __launch_bounds__(kWgThreads) void mlp_wgrad_kernel(const WgradParams p) {
+  __shared__ __attribute__((aligned(16))) float s_red[(kWgThreads / 64) * 16 * 64];
+  __shared__ uint16_t s_T[32 * 34];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int bid = blockIdx.x;
   const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int Bp = p.Bp;
+  ROCFM_STAMP(p.stamps, 0);
 
   if (bid < n_tiles) {
     int li = 0;
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
     const int ti = local / nto, to = local % nto;
     const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
     const uint16_t* Bm = p.dzT[li + 1] + (size_t)(to * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
-    const int q = Bp >> 2;  // batch quarter per wave (Bp % 64 == 0)
+    const int q = Bp >> 3;  // batch eighth per wave (Bp % 64 == 0 → q % 8 == 0, a multiple of 16 for Bp >= 128)
     f32x16 acc = {};
     const int bs = wave * q, be = bs + q;
     const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -64,7 +68,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
       bf16x8 fa[8], fb[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int b = min(b0 + 16 * u, be - 16);
+        const int b = max(bs, min(b0 + 16 * u, be - 16));
         fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
         fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
       }
@@ -74,43 +78,74 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
         acc = mfma32x32x16(fa[u], fb[u], acc);
       }
     }
-    if (wave > 0) {
+    // every wave parks its partial tile in LDS; then all 512 threads own 2 tile elements each
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s_red[((wave - 1) * 16 + r) * 64 + lane] = acc[r];
-    }
+    for (int r = 0; r < 16; ++r) s_red[(wave * 16 + r) * 64 + lane] = acc[r];
     __syncthreads();
-    if (wave == 0) {
+    ROCFM_STAMP(p.stamps, 1);
+    float g[2], w[2], a[2], b[2];
+    int idx[2], il[2], ol[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float g = (acc[r] + s_red[(0 * 16 + r) * 64 + lane] + s_red[(1 * 16 + r) * 64 + lane] +
-                         s_red[(2 * 16 + r) * 64 + lane]) *
-                        p.grad_scale;
-        const int i = ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int o = to * 32 + (lane & 31);
-        const int idx = p.offW[li] + i * Dout + o;
-        emit(p, st, idx, g);
-        if (p.fuse_opt) {
-          const uint16_t w = f2bf(p.params[idx]);
-          p.WT[li][(size_t)o * Din + i] = w;
-          p.Wb[li][(size_t)i * Dout + o] = w;
-        }
+    for (int e = 0; e < 2; ++e) {
+      const int el = t + kWgThreads * e, r = el >> 6, ln = el & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kWgThreads / 64; ++ww) v += s_red[(ww * 16 + r) * 64 + ln];
+      g[e] = v * p.grad_scale;
+      il[e] = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+      ol[e] = ln & 31;
+      idx[e] = p.offW[li] + (ti * 32 + il[e]) * Dout + to * 32 + ol[e];
+    }
+    if (!p.fuse_opt) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) p.grads[idx[e]] = g[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        w[e] = p.params[idx[e]];
+        a[e] = p.s0 ? p.s0[idx[e]] : 0.f;
+        b[e] = p.s1 ? p.s1[idx[e]] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        opt_apply(p.opt, st, w[e], g[e], a[e], b[e]);
+        p.params[idx[e]] = w[e];
+        if (p.s0) p.s0[idx[e]] = a[e];
+        if (p.s1) p.s1[idx[e]] = b[e];
+        const uint16_t hw = f2bf(w[e]);
+        p.Wb[li][(size_t)(ti * 32 + il[e]) * Dout + to * 32 + ol[e]] = hw;  // 64-B runs along o
+        s_T[ol[e] * 34 + il[e]] = hw;
+      }
+      __syncthreads();
+      {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
+        const int o = t >> 4, ip = (t & 15) * 2;
+        const uint32_t v2 = (uint32_t)s_T[o * 34 + ip] | ((uint32_t)s_T[o * 34 + ip + 1] << 16);
+        *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)(to * 32 + o) * Din + ti * 32 + ip) = v2;
       }
     }
+    ROCFM_STAMP(p.stamps, 2);
     return;
   }
+  // column reductions over the batch: 16 threads per column, 8 chunks (64 rows) in flight each
+  const int sub = t & 15;
   if (bid < n_tiles + n_bias) {  // bias gradients: Σ_b dz[o][b] for 32 columns
     const int lb = bid - n_tiles;
     int li = 0;
     while (lb >= p.bias_start[li + 1]) ++li;
     const int cb = lb - p.bias_start[li];
-    const int o = cb * 32 + (t >> 3), sub = t & 7;
+    const int o = cb * 32 + (t >> 4);
     const uint16_t* row = p.dzT[li + 1] + (size_t)o * Bp;
     float s = 0.f;
-#pragma unroll 4
-    for (int b = sub * 8; b < Bp; b += 64) s += sum_bf16x8(*reinterpret_cast<const uint4*>(row + b));
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+    for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + 128 * u < Bp) s += sum_bf16x8(v[u]);
+    }
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
     if (sub == 0) emit(p, st, p.offb[li] + o, s * p.grad_scale);
     return;
   }
@@ -119,24 +154,30 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
     const int Dn = p.dims[p.nl];
     const uint16_t* H = p.actT[p.nl];
     for (int c0 = 0; c0 < Dn; c0 += 32) {
-      const int c = c0 + (t >> 3), sub = t & 7;
+      const int c = min(c0 + (t >> 4), Dn - 1);
+      const uint16_t* row = H + (size_t)c * Bp;
       float s = 0.f;
-      if (c < Dn) {
-        const uint16_t* row = H + (size_t)c * Bp;
-        for (int b = sub * 8; b < Bp; b += 64) s += dot_bf16x8_f32(*reinterpret_cast<const uint4*>(row + b), p.g + b);
+      for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (b0 + 128 * u < Bp) s += dot_bf16x8_f32(v[u], p.g + b0 + 128 * u);
       }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      if (sub == 0 && c < Dn) emit(p, st, p.off_wout + c, s * p.grad_scale);
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
+      if (sub == 0 && c0 + (t >> 4) < Dn) emit(p, st, p.off_wout + c, s * p.grad_scale);
     }
     float s = 0.f;
-    for (int b = t; b < Bp; b += 256) s += p.g[b];
+    for (int b = t; b < Bp; b += kWgThreads) s += p.g[b];
     s = wave_sum(s);
     if (lane == 0) s_red[wave] = s;
     __syncthreads();
     if (t == 0) {
-      const float tot = (s_red[0] + s_red[1] + s_red[2] + s_red[3]) * p.grad_scale;
+      float tot = 0.f;
+      for (int w = 0; w < kWgThreads / 64; ++w) tot += s_red[w];
+      tot *= p.grad_scale;
       emit(p, st, p.off_bout, tot);
       emit(p, st, p.off_fmb, tot);
     }
@@ -144,7 +185,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(const WgradParams p) {
 }
 
 void launch_mlp_wgrad(WgradParams p, hipStream_t stream) {
-  ROCFM_REQUIRE(p.Bp % 64 == 0, "mlp_wgrad: Bp must be a multiple of 64");
+  ROCFM_REQUIRE(p.Bp % 128 == 0, "mlp_wgrad: Bp must be a multiple of 128");
   p.tile_start[0] = 0;
   p.bias_start[0] = 0;
   for (int l = 0; l < p.nl; ++l) {
@@ -157,7 +198,7 @@ void launch_mlp_wgrad(WgradParams p, hipStream_t stream) {
     p.bias_start[l] = p.bias_start[p.nl];
   }
   const int grid = p.tile_start[p.nl] + p.bias_start[p.nl] + 1;
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(grid), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(grid), dim3(kWgThreads), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

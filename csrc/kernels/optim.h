@@ -13,6 +13,7 @@ struct OptParams {
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
   float momentum = 0.95f;
   float ftrl_lr_power = -0.5f, ftrl_l1 = 0.f, ftrl_l2 = 0.f;
+  const float* lrt = nullptr;  // precomputed step-dependent lr_t (written by fetch_batch), or null
 };
 
 // Step-dependent scalars, computed once per thread from the device step counter (t = step+1).
@@ -20,11 +21,17 @@ struct OptStep {
   float lr_t;  // Adam: lr·√(1−β2ᵗ)/(1−β1ᵗ); others: lr
 };
 
+__host__ __device__ inline float adam_lr_t(float lr, float beta1, float beta2, int64_t step) {
+  const double t = (double)(step + 1);
+  return (float)((double)lr * sqrt(1.0 - pow((double)beta2, t)) / (1.0 - pow((double)beta1, t)));
+}
+
 __device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
   OptStep s;
-  if (o.type == kAdam) {
-    double t = (double)(step + 1);
-    s.lr_t = (float)((double)o.lr * sqrt(1.0 - pow((double)o.beta2, t)) / (1.0 - pow((double)o.beta1, t)));
+  if (o.lrt) {
+    s.lr_t = *o.lrt;
+  } else if (o.type == kAdam) {
+    s.lr_t = adam_lr_t(o.lr, o.beta1, o.beta2, step);
   } else {
     s.lr_t = o.lr;
   }

@@ -75,10 +75,12 @@ def latest_checkpoint(model_dir: str) -> Optional[str]:
 
 def save_checkpoint(model_dir: str, state: Dict[str, torch.Tensor], step: int, keep_max: int = 5,
                     shard: Tuple[int, int] = (0, 1), row_sets: Optional[Dict[str, torch.Tensor]] = None,
-                    extra: Optional[dict] = None, write_index: bool = True) -> str:
+                    extra: Optional[dict] = None, write_index: bool = True,
+                    global_rows: Optional[Dict[str, int]] = None) -> str:
     """Write shard ``shard=(r, n)`` of checkpoint ``step``; the rank with r == 0 writes the manifest.
 
-    ``row_sets``: for row-sharded variables, the global row ids held by this shard (1-D int64).
+    ``row_sets``: for row-sharded variables, the global row ids held by this shard (1-D int64);
+    ``global_rows``: their full row counts (default: 1 + the largest row id of this shard's set).
     """
     os.makedirs(model_dir, exist_ok=True)
     r, n = shard
@@ -93,10 +95,16 @@ def save_checkpoint(model_dir: str, state: Dict[str, torch.Tensor], step: int, k
     save_file(tensors, tmp)
     os.replace(tmp, os.path.join(model_dir, data))
     if r == 0 and write_index:
+        def gshape(k, v):
+            if row_sets and k in row_sets:
+                rows = (global_rows or {}).get(k, int(row_sets[k].max()) + 1 if row_sets[k].numel() else 0)
+                return [int(rows)] + list(v.shape[1:])
+            return list(v.shape)
+
         manifest = {
             "step": int(step),
             "num_shards": int(n),
-            "variables": {k: {"shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", ""),
+            "variables": {k: {"shape": gshape(k, v), "dtype": str(v.dtype).replace("torch.", ""),
                               "row_sharded": bool(row_sets and k in row_sets)} for k, v in state.items()},
             "created": time.time(),
         }

@@ -98,7 +98,8 @@ class FusedDeepFM:
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device="cuda",
                  embedding_update: str = "sparse", seed: int = 1234,
                  params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
-                 use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None):
+                 use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None,
+                 force_generic_kernels: bool = False):
         if spec.batch_norm:
             raise ValueError("the fused engine does not implement batch_norm; use engine=torch")
         if len(spec.layers) > 6:
@@ -107,7 +108,7 @@ class FusedDeepFM:
         self.spec, self.hp = spec, hp
         self.device = torch.device(device)
         self.B = int(batch_size)
-        self.Bp = (self.B + 63) // 64 * 64
+        self.Bp = (self.B + 127) // 128 * 128
         self.F, self.K = spec.field_size, spec.embedding_size
         self.K1 = self.K + 1
         self.Kp = (self.K1 + 3) // 4 * 4
@@ -122,6 +123,7 @@ class FusedDeepFM:
         self.seed = int(seed if dropout_seed is None else dropout_seed)
         self.loss_code = 0 if spec.loss_type == "log_loss" else 1
         self.lr_scale = 1.0
+        self.force_generic = bool(force_generic_kernels)
         dev = self.device
         L = self.layout
 
@@ -138,6 +140,7 @@ class FusedDeepFM:
         self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         self.steps = torch.zeros(2, dtype=torch.int64, device=dev)   # global_step, by parity
         self.cursor = torch.zeros(2, dtype=torch.int64, device=dev)  # pool batch index, by parity
+        self.lrt = torch.zeros(2, dtype=torch.float32, device=dev)     # per-step lr_t, by parity
 
         # ---- static step buffers (double-buffered by parity where the pipeline needs it) -------
         B, Bp, F = self.B, self.Bp, self.F
@@ -160,6 +163,7 @@ class FusedDeepFM:
         self.dense_grad = (torch.zeros_like(self.emb) if embedding_update == "exact" else None)
         self.dense_grads_flat = torch.zeros(L.total, dtype=torch.float32, device=dev)
         self.sort_stream = torch.cuda.Stream(device=dev)
+        self.aux_stream = torch.cuda.Stream(device=dev)  # mlp_wgrad runs concurrently with the embedding update
         # inference buffers (separate from the training slots)
         self.pred_ids = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
         self.pred_vals = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
@@ -181,8 +185,9 @@ class FusedDeepFM:
         self.refresh_bf16()
 
     # ------------------------------------------------------------------------------------------
-    def _opt(self):
+    def _opt(self, p: int = 0):
         o = self.H.OptParams()
+        o.lrt = self.lrt[p:].data_ptr()
         hp = self.hp
         o.type = OPT_ID[hp.name]
         o.lr = hp.lr * self.lr_scale
@@ -213,6 +218,7 @@ class FusedDeepFM:
         rp.train = 1 if train else 0
         rp.loss_type = self.loss_code
         rp.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+        rp.force_generic = 1 if self.force_generic else 0
         rp.set_dims(L.dims)
         for l in range(L.nl):
             rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),
@@ -240,7 +246,7 @@ class FusedDeepFM:
             wp.nl, wp.Bp = L.nl, self.Bp
             wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
             wp.fuse_opt = 1 if self.fuse_dense_opt else 0
-            wp.opt = self._opt()
+            wp.opt = self._opt(p)
             wp.grad_scale = 1.0
             wp.set_dims(L.dims)
             for a in range(L.nl + 1):
@@ -254,7 +260,7 @@ class FusedDeepFM:
             dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
             dp.step = step_ptr
             dp.n, dp.nl = L.total, L.nl
-            dp.opt = self._opt()
+            dp.opt = self._opt(p)
             dp.set_dims(L.dims)
             for l in range(L.nl):
                 dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
@@ -268,7 +274,7 @@ class FusedDeepFM:
             ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
             ep.l2 = float(self.spec.l2_reg)
             ep.grad_scale = 1.0
-            ep.opt = self._opt()
+            ep.opt = self._opt(p)
             ep.step = step_ptr
             ep.mode = 1 if self.embedding_update == "exact" else 0
             if self.dense_grad is not None:
@@ -283,7 +289,7 @@ class FusedDeepFM:
                 ed.n4 = self.V * self.Kp // 4
                 ed.Kp, ed.K1 = self.Kp, self.K1
                 ed.l2 = float(self.spec.l2_reg)
-                ed.opt = self._opt()
+                ed.opt = self._opt(p)
                 self.emb_dense_params.append(ed)
         self.pred_params = self._rows_params(self.pred_ids, self.pred_vals, self.pred_labels, self.pred_prob,
                                              self.pred_loss, self.steps.data_ptr(), False)
@@ -302,6 +308,9 @@ class FusedDeepFM:
             f.step_src, f.step_dst, f.step_advance = self.steps[p:].data_ptr(), self.steps[1 - p:].data_ptr(), 1
             f.ids, f.vals, f.labels = (self.slot_ids[1 - p].data_ptr(), self.slot_vals[1 - p].data_ptr(),
                                        self.slot_labels[1 - p].data_ptr())
+            f.lrt_dst = self.lrt[1 - p:].data_ptr()
+            f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
+            f.opt_type = OPT_ID[self.hp.name]
             self.fetch_params.append(f)
 
     def _set_pool(self, ids, vals, labels):
@@ -318,6 +327,7 @@ class FusedDeepFM:
         self._ring = False
         self._build_fetch()
         self._graphs = [None, None]
+        self._multi_graph = None
         self._primed = False
         self._start_batch = start
 
@@ -370,11 +380,13 @@ class FusedDeepFM:
     def set_lr_scale(self, s: float) -> None:
         """Multiply the learning rate (Horovod's lr × world size, HVD:171)."""
         self.lr_scale = float(s)
-        o = self._opt()
         for lst in (self.wgrad_params, self.dense_apply_params, self.emb_params, self.emb_dense_params):
-            for q in lst:
-                q.opt = o
+            for p, q in enumerate(lst):
+                q.opt = self._opt(p)
+        for f in self.fetch_params:
+            f.lr = self.hp.lr * self.lr_scale
         self._graphs = [None, None]
+        self._primed = False
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -397,6 +409,8 @@ class FusedDeepFM:
         base = 0 if self._ring else getattr(self, "_start_batch", 0)
         self.cursor[p] = base + self._i
         self.steps[p] = self._i
+        lr = self.hp.lr * self.lr_scale
+        self.lrt[p] = (self.H.adam_lr_t(lr, self.hp.beta1, self.hp.beta2, self._i) if self.hp.name == "Adam" else lr)
         f = self.H.FetchParams()
         src = self.fetch_params[p]
         f.ids_pool, f.vals_pool, f.labels_pool, f.pool_batches = (src.ids_pool, src.vals_pool, src.labels_pool,
@@ -429,6 +443,17 @@ class FusedDeepFM:
         self.H.deepfm_rows(self.rows_params[p], s)
         self.H.mlp_wgrad(self.wgrad_params[p], s)
 
+    def _enqueue_rows_then_fork_wgrad(self, p: int):
+        """rows kernel on the main stream, then mlp_wgrad on the aux stream (it only reads the
+        activations; the embedding update on the main stream is independent of it)."""
+        main = torch.cuda.current_stream(self.device)
+        self.H.deepfm_rows(self.rows_params[p], main.cuda_stream)
+        aux = self.aux_stream
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            self.H.mlp_wgrad(self.wgrad_params[p], aux.cuda_stream)
+        return aux
+
     def _enqueue_emb_update(self, p: int) -> None:
         s = self.stream_ptr
         self.H.emb_rows_update(self.emb_params[p], s)
@@ -437,9 +462,32 @@ class FusedDeepFM:
 
     def _enqueue_step(self, p: int) -> None:
         side = self._fork_next(p)
-        self._enqueue_forward_backward(p)
+        aux = self._enqueue_rows_then_fork_wgrad(p)
         self._enqueue_emb_update(p)
+        self._join(aux)
         self._join(side)
+
+    def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
+        """``n`` optimisation steps from the attached pool; full step-pairs are replayed from one
+        multi-step HIP graph (``steps_per_graph`` steps per launch) to amortise launch overhead."""
+        S = max(2, steps_per_graph // 2 * 2)
+        while n > 0:
+            if (self.use_graph and self._primed and self._warm >= 2 and n >= S and self._i % 2 == 0
+                    and not self._ring):
+                g = getattr(self, "_multi_graph", None)
+                if g is None or self._multi_S != S:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize(self.device)
+                    with torch.cuda.graph(g):
+                        for k in range(S):
+                            self._enqueue_step(k % 2)
+                    self._multi_graph, self._multi_S = g, S
+                g.replay()
+                self._i += S
+                n -= S
+            else:
+                self.train_step()
+                n -= 1
 
     def train_step(self) -> None:
         """One optimisation step on the current batch (asynchronous)."""

@@ -74,6 +74,7 @@ class TorchDeepFM:
             for k in self.trainable:
                 apply_dense(hp, self.P[k], grads[k], self.slots[k], step)
             self.t += 1
+            self._last_loss_t, self._last_has_l2 = loss.detach(), True
             return loss.detach()
         # sparse: autograd over the batch's unique rows only
         uniq, inv = torch.unique(ids.reshape(-1), return_inverse=True)
@@ -88,13 +89,14 @@ class TorchDeepFM:
         y = forward(params, ids, vals, self.spec, train=True, gen=self.gen, rows_w=rw[inv], rows_v=rv[inv])
         loss = data_loss(y, labels, self.spec.loss_type)
         loss.backward()
-        gw = rw.grad + self.spec.l2_reg * rw.detach()  # lazy L2 on touched rows
-        gv = rv.grad + self.spec.l2_reg * rv.detach()
+        gw, gv = rw.grad, rv.grad
         dgrads = {k: params[k].grad for k in dense_names}
         for k in dense_names:
             self.P[k].requires_grad_(False)
-        if self.exchange_rows is not None:
+        if self.exchange_rows is not None:  # (union of ids, rank-averaged data gradients)
             uniq, gw, gv = self.exchange_rows(uniq, gw, gv)
+        gw = gw + self.spec.l2_reg * self.P["fm_w"][uniq]  # lazy L2 on touched rows, once
+        gv = gv + self.spec.l2_reg * self.P["fm_v"][uniq]
         if self.allreduce_dense is not None:
             self.allreduce_dense(dgrads)
         apply_rows(hp, self.P["fm_w"], uniq, gw, self.slots["fm_w"], step)
@@ -102,7 +104,19 @@ class TorchDeepFM:
         for k in dense_names:
             apply_dense(hp, self.P[k], dgrads[k], self.slots[k], step)
         self.t += 1
+        self._last_loss_t, self._last_has_l2 = loss.detach(), False
         return loss.detach()
+
+    def batch_loss(self, include_l2: bool = True) -> float:
+        """Loss of the most recent training batch (data loss + full-table L2 terms)."""
+        if not hasattr(self, "_last_loss_t"):
+            return float("nan")
+        v = float(self._last_loss_t)
+        if include_l2 and not self._last_has_l2:
+            v += self.l2_value()
+        if not include_l2 and self._last_has_l2:
+            v -= self.l2_value()
+        return v
 
     @torch.no_grad()
     def predict_batch(self, ids, vals, labels=None):

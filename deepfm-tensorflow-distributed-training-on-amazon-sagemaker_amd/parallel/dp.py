@@ -222,13 +222,14 @@ class FusedDataParallel:
     def _phase_a(self, p: int):
         e = self.eng
         side = e._fork_next(p)
-        e._enqueue_forward_backward(p)
+        self.send_count.zero_() if self.mode == "dp" else None
+        aux = e._enqueue_rows_then_fork_wgrad(p)
         s = e.stream_ptr
         if self.mode == "dense_dp":
             e.H.emb_rows_update(e.emb_params[p], s)  # mode 1: Σ rows → dense grad table
         else:
-            self.send_count.zero_()
             e.H.emb_rows_update(self.export_params[p], s)
+        e._join(aux)
         e._join(side)
 
     def _exchange(self):

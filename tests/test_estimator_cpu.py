@@ -1,0 +1,102 @@
+"""End-to-end Estimator on CPU (BASELINE config 1 plumbing): train on a synthetic train file +
+the bundled val file's schema, evaluate, checkpoint/resume bit-exactness, export, pred.txt."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from rocfm import checkpoint as ckpt
+from rocfm.config import parse_flags
+from rocfm.data.synthetic import write_synthetic_tfrecord
+from rocfm.estimator import Estimator
+
+
+@pytest.fixture(scope="module")
+def data_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("data")
+    write_synthetic_tfrecord(str(d / "tr.tfrecords"), 6000, 2000, seed=1)
+    write_synthetic_tfrecord(str(d / "va.tfrecords"), 1500, 2000, seed=2)
+    write_synthetic_tfrecord(str(d / "te.tfrecords"), 700, 2000, seed=3)
+    return str(d)
+
+
+def _cfg(data_dir, model_dir, **kw):
+    argv = ["--feature_size", "2000", "--field_size", "39", "--embedding_size", "8", "--deep_layers", "32,16",
+            "--dropout", "1.0,1.0", "--batch_size", "256", "--learning_rate", "0.005", "--l2_reg", "0.00001",
+            "--training_data_dir", data_dir, "--val_data_dir", data_dir, "--model_dir", model_dir,
+            "--log_steps", "5", "--engine", "torch", "--num_threads", "2", "--save_checkpoints_secs", "0"]
+    for k, v in kw.items():
+        argv += [f"--{k}", str(v)]
+    return parse_flags(argv)
+
+
+def test_train_eval_checkpoint_export(data_dir, tmp_path):
+    md = str(tmp_path / "m")
+    est = Estimator(_cfg(data_dir, md))
+    ev0 = est.evaluate([os.path.join(data_dir, "va.tfrecords")])
+    out = est.train([os.path.join(data_dir, "tr.tfrecords")], num_epochs=2)
+    assert out["steps"] == 2 * (6000 // 256)
+    ev1 = est.evaluate([os.path.join(data_dir, "va.tfrecords")])
+    assert ev1["loss"] < ev0["loss"] and ev1["auc_exact"] > 0.7 and abs(ev1["auc"] - ev1["auc_exact"]) < 0.02
+    assert ev1["examples"] == (1500 // 256) * 256  # drop_remainder on eval too (reference input_fn)
+    prefix = ckpt.latest_checkpoint(md)
+    assert prefix and ckpt.checkpoint_step(prefix) == est.global_step
+    sd = ckpt.load_checkpoint(prefix)
+    assert "fm_v/Adam" in sd and "Deep-part/mlp0/weights/Adam_1" in sd and int(sd["global_step"]) == est.global_step
+    # resume: a fresh estimator restores the checkpoint and continues bit-exactly
+    a = Estimator(_cfg(data_dir, md))
+    assert a.global_step == est.global_step
+    b_sd = est.state_dict()
+    for k, v in a.state_dict().items():
+        assert torch.equal(v, b_sd[k]), k
+    # export + servable predictions == estimator predictions
+    exp = est.export(str(tmp_path / "export"))
+    meta = json.load(open(os.path.join(exp, "model.json")))
+    assert meta["signatures"]["serving_default"]["inputs"]["feat_ids"]["shape"] == [None, 39]
+    from rocfm.serving import Predictor
+
+    pr = Predictor(str(tmp_path / "export"))
+    from rocfm.data.tfrecord import decode_file
+
+    L, I, V = decode_file(os.path.join(data_dir, "te.tfrecords"), 39)
+    p_est = est.predict([os.path.join(data_dir, "te.tfrecords")], str(tmp_path / "pred.txt"))
+    p_srv = pr.predict(I[: len(p_est)], V[: len(p_est)])
+    torch.testing.assert_close(p_srv, p_est, rtol=1e-5, atol=1e-6)
+    lines = open(tmp_path / "pred.txt").read().splitlines()
+    assert len(lines) == (700 // 256) * 256 and all(len(x.split(".")[1]) == 6 for x in lines)
+
+
+def test_keep_checkpoint_max(tmp_path):
+    md = str(tmp_path / "k")
+    sd = {"w": torch.zeros(3)}
+    for s in range(1, 9):
+        ckpt.save_checkpoint(md, sd, s, keep_max=3)
+    assert ckpt.list_checkpoints(md) == ["model.ckpt-6", "model.ckpt-7", "model.ckpt-8"]
+    assert not any(f.startswith("model.ckpt-5.") for f in os.listdir(md))
+
+
+def test_sharded_checkpoint_reshard(tmp_path):
+    md = str(tmp_path / "s")
+    full = torch.arange(40, dtype=torch.float32).view(10, 4)
+    for r in range(2):  # 2 shards, id % 2 == r
+        rows = torch.arange(r, 10, 2)
+        ckpt.save_checkpoint(md, {"fm_v": full[rows]}, 7, shard=(r, 2), row_sets={"fm_v": rows},
+                             write_index=(r == 0), global_rows={"fm_v": 10})
+    p = ckpt.latest_checkpoint(md)
+    assert torch.equal(ckpt.load_checkpoint(p)["fm_v"], full)
+    sub = ckpt.load_checkpoint(p, rows_for={"fm_v": torch.tensor([9, 0, 4])})["fm_v"]
+    assert torch.equal(sub, full[[9, 0, 4]])
+
+
+def test_cli_train_infer(data_dir, tmp_path):
+    from rocfm.cli import run
+
+    md = str(tmp_path / "cli")
+    cfg = _cfg(data_dir, md, num_epochs=1, servable_model_dir=str(tmp_path / "exp"), task_type="train")
+    res = run(cfg)
+    assert res["epochs"][0]["eval_auc"] > 0.6 and os.path.isdir(res["export"])
+    res = run(_cfg(data_dir, md, task_type="infer"))
+    assert os.path.exists(os.path.join(data_dir, "pred.txt")) and res["infer"]["n"] == 512
+    os.remove(os.path.join(data_dir, "pred.txt"))

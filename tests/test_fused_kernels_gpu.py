@@ -38,15 +38,18 @@ def _ref_inputs(eng: FusedDeepFM, spec: ModelSpec, step: int, keeps):
     return emb, layers, w_out, b_out, fmb, masks
 
 
-@pytest.mark.parametrize("K,layers", [(10, [128, 64, 32]), (32, [256, 128, 64]), (8, [48, 16])])
-def test_fused_step_gradients_match_oracle(K, layers):
+@pytest.mark.parametrize("K,layers,generic", [(10, [128, 64, 32], False), (10, [128, 64, 32], True),
+                                              (32, [256, 128, 64], False), (8, [48, 16], False),
+                                              (10, [64, 32], False)])
+def test_fused_step_gradients_match_oracle(K, layers, generic):
     torch.manual_seed(0)
     dev = torch.device("cuda")
     V, F, B = 5000, 39, 192
     spec = ModelSpec(feature_size=V, field_size=F, embedding_size=K, layers=layers,
                      keep_probs=[0.5] * len(layers), l2_reg=1e-3)
     hp = OptHParams(name="GD", lr=1.0)
-    eng = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 7), use_graph=False)
+    eng = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 7), use_graph=False,
+                      force_generic_kernels=generic)
     gen = torch.Generator().manual_seed(1)
     ids, vals, labels = _batch(B, F, V, gen)
     emb, lays, w_out, b_out, fmb, masks = _ref_inputs(eng, spec, 0, spec.keep_probs)

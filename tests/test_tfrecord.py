@@ -1,0 +1,164 @@
+"""C++ TFRecord runtime: framing/CRC, Example decoding, loader sharding & batching, libsvm tool.
+
+Golden statistics of the bundled data/val.tfrecords are from SURVEY.md §2.8 (10,000 records,
+2,553 positives, ids in 1..117565, first record ids)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from rocfm.data import tfrecord as T
+from rocfm.ops import io
+
+FIRST_IDS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 19, 586, 1079, 12368, 26191, 26341, 27172, 35362, 35613,
+             36145, 47521, 51365, 63273, 65964, 66584, 71629, 84088, 84521, 86888, 88279, 88284, 100289, 100301,
+             100316, 109930, 109982]
+
+
+def test_golden_stats_of_bundled_data(ref_data_path):
+    L, I, V = T.decode_file(ref_data_path, 39, 117581)
+    assert L.shape == (10000,) and I.shape == (10000, 39) and V.shape == (10000, 39)
+    assert int(L.sum()) == 2553
+    assert int(I.min()) == 1 and int(I.max()) == 117565
+    assert I[0].tolist() == FIRST_IDS and float(L[0]) == 1.0
+    assert (I[:, :13] == torch.arange(1, 14, dtype=torch.int32)).all()  # numeric fields: fixed ids 1..13
+    assert (V[:, 13:] == 1.0).all()
+    assert len(torch.unique(I)) == 28116
+
+
+def test_native_matches_python_oracle(ref_data_path):
+    L, I, V = T.decode_file(ref_data_path, 39)
+    for k, rec in enumerate(T.read_records(ref_data_path, verify=True)):
+        ex = T.parse_example(rec)
+        assert ex["ids"] == I[k].tolist()
+        assert np.allclose(ex["values"], V[k].numpy())
+        assert ex["label"][0] == float(L[k])
+        if k == 50:
+            break
+
+
+def test_crc32c_known_vectors():
+    m = io()
+    assert m.crc32c(b"") == 0
+    assert m.crc32c(b"123456789") == 0xE3069283  # standard CRC-32C check value
+    assert m.masked_crc32c(b"abc") == T.masked_crc32c_py(b"abc")
+
+
+def _write(path, n, F=5, seed=0, V=100):
+    g = np.random.default_rng(seed)
+    ids = g.integers(0, V, (n, F)).astype(np.int64)
+    vals = g.random((n, F)).astype(np.float32)
+    labels = (g.random(n) < 0.3).astype(np.float32)
+    io().write_tfrecord(path, labels, ids, vals, False)
+    return labels, ids, vals
+
+
+def test_writer_roundtrip(tmp_path):
+    p = str(tmp_path / "a.tfrecords")
+    labels, ids, vals = _write(p, 300)
+    L, I, V = T.decode_file(p, 5)
+    assert np.array_equal(L.numpy(), labels) and np.array_equal(I.numpy(), ids) and np.array_equal(V.numpy(), vals)
+    # the python oracle reads the C++ writer's bytes too
+    ex = T.parse_example(next(T.read_records(p, verify=True)))
+    assert ex["ids"] == ids[0].tolist()
+
+
+def test_corrupt_record_fail_and_skip(tmp_path):
+    p = str(tmp_path / "c.tfrecords")
+    _write(p, 10)
+    data = bytearray(open(p, "rb").read())
+    (n0,) = struct.unpack("<Q", data[:8])
+    data[12 + 5] ^= 0xFF  # corrupt the first record's payload
+    open(p, "wb").write(bytes(data))
+    with pytest.raises(RuntimeError):
+        T.decode_file(p, 5)
+    L, _, _ = T.decode_file(p, 5, skip_bad=True)
+    assert len(L) == 9
+
+
+def test_wrong_field_count_is_an_error(tmp_path):
+    p = str(tmp_path / "w.tfrecords")
+    _write(p, 4, F=5)
+    with pytest.raises(RuntimeError, match="decode error"):
+        T.decode_file(p, 6)
+
+
+def _collect(ds):
+    out = []
+    for ids, vals, labels in ds:
+        out.append((ids.clone(), vals.clone(), labels.clone()))
+    return out
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_loader_batches_shards_epochs(tmp_path, threads):
+    p1, p2 = str(tmp_path / "tr1.tfrecords"), str(tmp_path / "tr2.tfrecords")
+    l1, i1, v1 = _write(p1, 250, seed=1)
+    l2, i2, v2 = _write(p2, 170, seed=2)
+    all_ids = np.concatenate([i1, i2])
+    # shard(3, 1) over the concatenated files, batch 16, drop remainder, 2 epochs
+    ds = T.TFRecordDataset([p1, p2], 5, 16, num_epochs=2, shard_count=3, shard_index=1, num_threads=threads,
+                           num_slots=3, pin_memory=False)
+    got = _collect(ds)
+    kept = all_ids[1::3]
+    nb = len(kept) // 16
+    assert len(got) == 2 * nb
+    for e in range(2):
+        for b in range(nb):
+            assert np.array_equal(got[e * nb + b][0].numpy(), kept[b * 16:(b + 1) * 16])
+    # no drop_remainder: the tail batch is emitted
+    ds = T.TFRecordDataset([p1], 5, 64, drop_remainder=False, pin_memory=False)
+    sizes = [len(b[0]) for b in _collect(ds)]
+    assert sizes == [64, 64, 64, 58]
+
+
+def test_loader_shuffle_buffer_is_a_permutation(tmp_path):
+    p = str(tmp_path / "tr.tfrecords")
+    _, ids, _ = _write(p, 200, seed=3)
+    ds = T.TFRecordDataset([p], 5, 10, shuffle_buffer=50, seed=7, pin_memory=False)
+    got = torch.cat([b[0] for b in _collect(ds)]).numpy()
+    assert got.shape == ids.shape
+    assert sorted(map(tuple, got.tolist())) == sorted(map(tuple, ids.tolist()))
+    assert not np.array_equal(got, ids)
+
+
+def test_pipe_mode_stream(tmp_path):
+    p = str(tmp_path / "pipe.tfrecords")
+    _, ids, _ = _write(p, 40, seed=4)
+    fifo = str(tmp_path / "fifo")
+    os.mkfifo(fifo)
+    import threading
+
+    def feed():
+        with open(fifo, "wb") as f:
+            f.write(open(p, "rb").read())
+
+    th = threading.Thread(target=feed)
+    th.start()
+    ds = T.TFRecordDataset([fifo], 5, 8, stream_mode=True, pin_memory=False)
+    got = torch.cat([b[0] for b in _collect(ds)]).numpy()
+    th.join()
+    assert np.array_equal(got, ids)
+
+
+def test_libsvm_converter_roundtrip(tmp_path):
+    src = tmp_path / "tr.libsvm"
+    src.write_text("1 1:0.5 2:0.03519 3:1\n0 4:0.25 5:1 6:1\n\n1 7:2 8:3 9:4\n")
+    out = str(tmp_path / "tr.tfrecords")
+    n = io().convert_libsvm(str(src), out, 2)
+    assert n == 3
+    L, I, V = T.decode_file(out, 3)
+    assert L.tolist() == [1.0, 0.0, 1.0]
+    assert I.tolist() == [[1, 2, 3], [4, 5, 6], [7, 8, 9]]
+    assert np.allclose(V.numpy(), [[0.5, 0.03519, 1], [0.25, 1, 1], [2, 3, 4]])
+
+
+def test_discover_files(tmp_path):
+    (tmp_path / "a").mkdir()
+    for n in ["tr1.tfrecords", "a/tr2.tfrecords", "va.tfrecords", "te.tfrecords", "other.txt"]:
+        (tmp_path / n).write_bytes(b"")
+    tr = T.discover_files(str(tmp_path), "tr")
+    assert [os.path.basename(x) for x in tr] == ["tr2.tfrecords", "tr1.tfrecords"] or len(tr) == 2
+    assert len(T.discover_files(str(tmp_path), "va")) == 1 and len(T.discover_files(str(tmp_path), "te")) == 1

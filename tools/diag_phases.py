@@ -1,0 +1,66 @@
+"""Diagnostic: per-phase durations of the fused kernels from in-kernel s_memrealtime stamps.
+
+Stamps are recorded by thread 0 of every workgroup (100 MHz real-time counter).  Prints the mean /
+max over workgroups of each phase's duration (µs) and of the whole kernel, for a few eager steps.
+Not a performance measurement of the real kernels (stamps add a little work).
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from rocfm.data.synthetic import SyntheticCriteo  # noqa: E402
+from rocfm.models.deepfm import ModelSpec, init_params  # noqa: E402
+from rocfm.models.fused import FusedDeepFM  # noqa: E402
+from rocfm.optim import OptHParams  # noqa: E402
+
+
+def report(name, st, idx, labels):
+    st = st[:, idx].double()
+    valid = (st > 0).all(1)
+    st = st[valid]
+    d = (st[:, 1:] - st[:, :-1]) * 0.01  # ticks of 10 ns → µs
+    tot = (st[:, -1] - st[:, 0]) * 0.01
+    span = (st[:, -1].max() - st[:, 0].min()) * 0.01
+    print(f"== {name}: {int(valid.sum())} workgroups, kernel span {span:.2f} us, per-WG total mean {tot.mean():.2f} max {tot.max():.2f}")
+    for i in range(d.shape[1]):
+        print(f"   {labels[i]:<28} mean {d[:, i].mean():7.2f}  max {d[:, i].max():7.2f}")
+
+
+def main():
+    B = int(os.environ.get("B", "1024"))
+    dev = torch.device("cuda")
+    spec = ModelSpec(1_000_000, 39, 10, [128, 64, 32], [0.5] * 3, l2_reg=1e-4)
+    eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=False)
+    gen = SyntheticCriteo(1_000_000, 39, seed=1)
+    g = torch.Generator(device=dev).manual_seed(1)
+    pool = [gen.batch(B, dev, g) for _ in range(8)]
+    eng.attach_pool(torch.stack([x[0] for x in pool]), torch.stack([x[1] for x in pool]),
+                    torch.stack([x[2] for x in pool]))
+    for _ in range(6):
+        eng.train_step()
+    torch.cuda.synchronize()
+    nrows = eng.Bp // 16
+    s_rows = torch.zeros(nrows * 16, dtype=torch.int64, device=dev)
+    s_wg = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+    s_emb = torch.zeros(((eng.n_lookup + 255) // 256) * 16, dtype=torch.int64, device=dev)
+    for p in range(2):
+        eng.rows_params[p].stamps = s_rows.data_ptr()
+        eng.wgrad_params[p].stamps = s_wg.data_ptr()
+        eng.emb_params[p].stamps = s_emb.data_ptr()
+    for _ in range(3):
+        s_rows.zero_(); s_wg.zero_(); s_emb.zero_()
+        eng.train_step()
+        torch.cuda.synchronize()
+    report("deepfm_rows", s_rows.view(-1, 16).cpu(), [0, 1, 2, 3, 4, 5, 9, 10, 11, 12],
+           ["0 ids/vals stage", "A gather+e+h0", "B FM + h0T store", "C layer0 fwd", "C layer1 fwd",
+            "C layer2 fwd", "D head + dz_L", "E backward (3 GEMMs)", "F FM bwd + contrib"])
+    wg = s_wg.view(-1, 16).cpu()
+    report("mlp_wgrad (tile WGs)", wg[wg[:, 1] > 0], [0, 1, 2], ["MFMA + LDS reduce", "epilogue (opt+bf16)"])
+    report("emb_rows_update", s_emb.view(-1, 16).cpu(), [0, 1, 2, 3, 4],
+           ["keys+rows+scan+heads", "end search", "continuation", "optimizer items"])
+
+
+if __name__ == "__main__":
+    main()
