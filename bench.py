@@ -25,7 +25,16 @@ sys.path.insert(0, ROOT)
 
 METRIC = "examples/sec (whole node) DeepFM Criteo-39-field at 1/2/4/8 MI355X"
 # PyTorch-eager (engine=torch, same semantics, same shapes) measured on one MI355X; see BASELINE.md.
-EAGER_BASELINE = {"sparse": None, "exact": None}
+# Measured 2026-10 on one MI355X: bench.py --engine torch [--embedding_update exact], B=1024, 1M vocab, k=10.
+EAGER_BASELINE = {"sparse": 439405.8, "exact": 535396.5}
+
+
+def _human(n: int) -> str:
+    for div, suf in ((10**9, "B"), (10**6, "M"), (10**3, "K")):
+        if n >= div and n % (div // 10) == 0:
+            v = n / div
+            return (f"{v:.0f}" if v == int(v) else f"{v:.1f}") + suf
+    return str(n)
 
 
 def parse():
@@ -48,6 +57,7 @@ def parse():
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--steps_per_graph", type=int, default=8, help="fused engine: steps captured per HIP graph")
+    ap.add_argument("--shard_capacity", type=int, default=0, help="rowshard: per-owner exchange rows (0 = auto)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json_out", default="")
     return ap.parse_args()
@@ -81,7 +91,10 @@ def main():
     keeps = [float(x) for x in a.dropout.split(",")]
     spec = ModelSpec(a.feature_size, a.field_size, a.embedding_size, layers, keeps, l2_reg=a.l2_reg)
     hp = OptHParams(name=a.optimizer, lr=a.learning_rate)
-    params = init_params(spec, a.seed)  # identical on every rank (= rank-0 broadcast, HVD:418)
+    if a.parallelism == "rowshard":
+        params = None  # each rank initialises only its own shard (100M-1B rows never materialise on one host)
+    else:
+        params = init_params(spec, a.seed)  # identical on every rank (= rank-0 broadcast, HVD:418)
 
     B = a.batch_size
     gen = SyntheticCriteo(a.feature_size, a.field_size, seed=a.seed)
@@ -95,7 +108,12 @@ def main():
     if parallelism == "auto":
         parallelism = "dp" if a.embedding_update == "sparse" else "dense_dp"
     if a.engine == "fused":
-        if world > 1:
+        if parallelism == "rowshard":
+            from rocfm.parallel.emb_shard import FusedRowShard
+
+            eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
+                                use_graph=not a.no_graph, capacity=a.shard_capacity or None)
+        elif world > 1:
             from rocfm.parallel.dp import FusedDataParallel
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
@@ -117,8 +135,13 @@ def main():
     else:
         from rocfm.models.torch_engine import TorchDeepFM
 
-        eng = TorchDeepFM(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
-        if world > 1:
+        if parallelism == "rowshard":
+            from rocfm.parallel.emb_shard import TorchRowShard
+
+            eng = TorchRowShard(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
+        else:
+            eng = TorchDeepFM(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
+        if world > 1 and parallelism != "rowshard":
             from rocfm.parallel.dp import attach_torch_dp
 
             attach_torch_dp(eng, a.embedding_update)
@@ -165,11 +188,11 @@ def main():
         "dtype": "bf16",
         "data": "synthetic Criteo-shape (39 fields, Zipf ids, HBM-resident batch pool), random-init weights",
         "config": {
-            "model": f"DeepFM Criteo-shape (39 fields, {a.feature_size // 1000}K-hash vocab, k={a.embedding_size}, "
+            "model": f"DeepFM Criteo-shape ({a.field_size} fields, {_human(a.feature_size)}-hash vocab, k={a.embedding_size}, "
                      f"mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
             "global_batch": B * world,
             "seq_len": a.field_size,
-            "parallelism": f"{parallelism}{world}" if world > 1 else "dp1",
+            "parallelism": f"{parallelism}{world}" if (world > 1 or parallelism == "rowshard") else "dp1",
             "engine": a.engine,
             "embedding_update": a.embedding_update,
         },

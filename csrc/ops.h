@@ -8,6 +8,7 @@
 #include "kernels/batch.h"
 #include "kernels/emb_update.h"
 #include "kernels/optim.h"
+#include "kernels/shard.h"
 
 namespace rocfm {
 

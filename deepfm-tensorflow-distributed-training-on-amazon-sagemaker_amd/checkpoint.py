@@ -89,7 +89,7 @@ def save_checkpoint(model_dir: str, state: Dict[str, torch.Tensor], step: int, k
     tensors = {_sanitize(k): v.detach().contiguous().cpu() for k, v in state.items()}
     if row_sets:
         for k, rows in row_sets.items():
-            tensors[f"__rows__/{k}"] = rows.detach().to(torch.int64).cpu().contiguous()
+            tensors[f"__rows__/{k}"] = rows.detach().to(torch.int64).cpu().clone()
     fd, tmp = tempfile.mkstemp(dir=model_dir, prefix=".tmp-", suffix=".safetensors")
     os.close(fd)
     save_file(tensors, tmp)

@@ -118,3 +118,23 @@ def emb_grad_reference(ids: torch.Tensor, contrib: torch.Tensor):
     acc = torch.zeros(len(uniq), contrib.shape[1], dtype=contrib.dtype)
     acc.index_add_(0, inv, contrib)
     return uniq, acc
+
+
+def shard_route_reference(ids: np.ndarray, W: int, Vs: int, cap: int):
+    """Oracle of shard.hip's routing: (send_ids [W,cap] with -1 padding, local_idx [n], counts [W]).
+
+    Owner of id i is i % W; an owner's requests are its unique ids in ascending local-row order;
+    lookup l reads received row o*cap + j of its id's owner o.
+    """
+    ids = np.asarray(ids, dtype=np.int64).reshape(-1)
+    send = np.full((W, cap), -1, dtype=np.int64)
+    local = np.zeros(len(ids), dtype=np.int64)
+    counts = np.zeros(W, dtype=np.int64)
+    for o in range(W):
+        mine = np.unique(ids[ids % W == o])  # ascending id == ascending local row
+        counts[o] = len(mine)
+        send[o, : min(len(mine), cap)] = mine[:cap]
+        pos = {int(v): j for j, v in enumerate(mine)}
+        for l in np.nonzero(ids % W == o)[0]:
+            local[l] = o * cap + min(pos[int(ids[l])], cap - 1)
+    return send, local, counts

@@ -1,0 +1,732 @@
+"""Row-sharded embedding tables — the reference's Parameter-Server mode on RCCL all-to-all.
+
+The reference's PS mode (PS:461-490 cluster spec, PS:521-531 ``replica_device_setter``) keeps
+``fm_w``/``fm_v`` on the parameter servers: each worker pulls the rows its batch touches and
+pushes their gradients, which the servers apply asynchronously.  On one MI355X node the servers
+are the GPUs themselves: id ``i`` is owned by rank ``i % W`` and stored there at local row
+``i // W`` (a 1B-row table is 125M rows × (K+1) f32 + optimizer slots per GPU, well inside 288 GB
+of HBM).  Every step, synchronously:
+
+    route   sort the batch's ids owner-major; per owner the unique ids to request       (side stream)
+    X1      all_to_all  requested ids                  [W, cap] int32
+    serve   owners gather the requested rows from their shard
+    X2      all_to_all  rows                           [W, cap, K+1] f32 → the step's "table"
+    step    the fused row kernel runs unchanged, with the received rows as its table and
+            each lookup's received-row index as its id; the lookup gradients are reduced per
+            received row (emb_update.hip mode 1)
+    X3      all_to_all  row gradients back to owners   [W, cap, K+1] f32
+    update  owners sort the requests by local row, segment-sum over source ranks, apply lazy L2
+            once and the row optimizer (or, ``embedding_update=exact``, the dense full-table
+            update of the shard — the reference's full L2, with no dense traffic at all)
+    X4      all_reduce  MLP gradients (one flat bucket), then the dense optimizer
+
+The exchange buffers have a fixed per-owner capacity so that every collective has static shapes
+(no host round trip, graph-capturable phases).  The default capacity (1.25× the even share of the
+batch's lookups + 64) is exceeded only by a pathological id distribution; an owner that needs more
+sets a sticky device flag that is checked every ``check_every`` steps and raises — results are
+never silently truncated without an error.  ``capacity=B*F`` makes overflow impossible.
+
+Synchronous semantics: with gradient averaging over ranks and the learning rate × W (HVD:171,
+``lr_scaling``) the result equals the single-process step on the union batch (tests).
+
+``TorchRowShard`` is the same algorithm in eager PyTorch (variable-size all-to-all), used on CPU
+(gloo tests) and as the eager baseline; ``FusedRowShard`` is the HIP path (shard.hip kernels +
+the fused DeepFM step).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.deepfm import TRUNC_NORMAL_STD, ModelSpec, init_params
+from ..optim import OptHParams, apply_dense, apply_rows, slot_names
+
+PAD = -1  # int32 view of 0xFFFFFFFF (request padding)
+
+
+def _world_rank():
+    if dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_size(V: int, W: int) -> int:
+    """Rows per shard: ⌈V / W⌉ (the last ranks may hold one padding row that is never touched)."""
+    return (V + W - 1) // W
+
+
+def shard_rows(V: int, W: int, r: int) -> torch.Tensor:
+    """Global ids owned by rank r, in local-row order."""
+    return torch.arange(r, V, W, dtype=torch.int64)
+
+
+def slice_rows(t: torch.Tensor, V: int, W: int, r: int) -> torch.Tensor:
+    """Rows of a full table [V, ...] owned by rank r, zero-padded to shard_size(V, W) rows."""
+    Vs = shard_size(V, W)
+    out = torch.zeros((Vs,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    loc = t[r::W]
+    out[: loc.shape[0]] = loc
+    return out
+
+
+def _truncated_normal_(t: torch.Tensor, std: float, gen: torch.Generator) -> torch.Tensor:
+    x = torch.randn(t.shape, generator=gen, device=t.device, dtype=torch.float32)
+    bad = x.abs() > 2.0
+    while bool(bad.any()):
+        x = torch.where(bad, torch.randn(t.shape, generator=gen, device=t.device, dtype=torch.float32), x)
+        bad = x.abs() > 2.0
+    return t.copy_(x * std)
+
+
+def init_shard_params(spec: ModelSpec, seed: int, rank: int, world: int, device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    """Initial values of rank ``rank``'s shard without materialising the full table (100M-1B rows).
+
+    Same distributions as ``init_params`` (TF glorot_normal over the FULL table's fans, SURVEY
+    App. A); the table rows are drawn on ``device`` from a per-rank stream, the dense part is
+    identical on every rank.
+    """
+    V, K = spec.feature_size, spec.embedding_size
+    Vs = shard_size(V, world)
+    dense_spec = dataclasses.replace(spec, feature_size=1)
+    P = init_params(dense_spec, seed)
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev).manual_seed(seed * 1000003 + 7 * rank + 1)
+    n_loc = len(range(rank, V, world))
+    fm_w = torch.zeros(Vs, device=dev)
+    fm_v = torch.zeros(Vs, K, device=dev)
+    _truncated_normal_(fm_w[:n_loc], math.sqrt(2.0 / (V + V)) / TRUNC_NORMAL_STD, gen)
+    _truncated_normal_(fm_v[:n_loc], math.sqrt(2.0 / (V + K)) / TRUNC_NORMAL_STD, gen)
+    P["fm_w"], P["fm_v"] = fm_w, fm_v
+    return P
+
+
+def local_params(spec: ModelSpec, params: Optional[Dict[str, torch.Tensor]], seed: int, rank: int, world: int,
+                 device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    """This rank's parameter set: slice full tables if given, else a fresh sharded init."""
+    if params is None:
+        return init_shard_params(spec, seed, rank, world, device)
+    V = spec.feature_size
+    out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    for k, v in params.items():
+        out[k] = slice_rows(v, V, world, rank) if k in ("fm_w", "fm_v") else v.clone()
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# collectives (RCCL fast path; host-staged for gloo with device tensors)
+# ------------------------------------------------------------------------------------------------
+def all_to_all_equal(out: torch.Tensor, inp: torch.Tensor) -> None:
+    """Equal-split all_to_all: inp/out [W * chunk] (first dim split evenly over ranks)."""
+    if dist.get_backend() == "nccl" or inp.device.type == "cpu":
+        dist.all_to_all_single(out, inp)
+        return
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.detach().cpu())
+    out.copy_(o)
+
+
+def all_to_all_var(inp: torch.Tensor, send_counts: List[int], recv_counts: List[int]) -> torch.Tensor:
+    out = torch.empty((sum(recv_counts),) + tuple(inp.shape[1:]), dtype=inp.dtype, device=inp.device)
+    if dist.get_backend() == "nccl" or inp.device.type == "cpu":
+        dist.all_to_all_single(out, inp.contiguous(), recv_counts, send_counts)
+        return out
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.detach().cpu().contiguous(), recv_counts, send_counts)
+    return o.to(inp.device)
+
+
+def all_reduce_(t: torch.Tensor, op=None) -> torch.Tensor:
+    op = op or dist.ReduceOp.SUM
+    if dist.get_backend() == "nccl" or t.device.type == "cpu":
+        dist.all_reduce(t, op=op)
+        return t
+    c = t.detach().cpu()
+    dist.all_reduce(c, op=op)
+    t.copy_(c)
+    return t
+
+
+def _gather_table(local: torch.Tensor, V: int, W: int) -> torch.Tensor:
+    """Reassemble a full table [V, ...] from every rank's shard [Vs, ...] (all ranks get it)."""
+    Vs = local.shape[0]
+    dev_ok = dist.get_backend() == "nccl" or local.device.type == "cpu"
+    src = local.contiguous() if dev_ok else local.detach().cpu().contiguous()
+    buf = torch.empty((W * Vs,) + tuple(local.shape[1:]), dtype=local.dtype, device=src.device)
+    dist.all_gather_into_tensor(buf, src) if dev_ok else dist.all_gather(list(buf.chunk(W)), src)
+    # buf[r*Vs + l] holds global id l*W + r
+    full = buf.view(W, Vs, *local.shape[1:]).transpose(0, 1).reshape(W * Vs, *local.shape[1:])
+    return full[:V].to(local.device)
+
+
+# ================================================================================================
+# eager engine
+# ================================================================================================
+class TorchRowShard:
+    """Eager-PyTorch DeepFM with row-sharded fm_w/fm_v (one process per device)."""
+
+    row_sharded = True
+    collective_predict = True
+
+    def __init__(self, spec: ModelSpec, hp: OptHParams, device="cpu", embedding_update: str = "sparse",
+                 params: Optional[Dict[str, torch.Tensor]] = None, seed: int = 1234,
+                 dropout_seed: Optional[int] = None):
+        from ..models.torch_engine import TorchDeepFM
+
+        self.W, self.rank = _world_rank()
+        self.V = spec.feature_size
+        self.Vs = shard_size(self.V, self.W)
+        self.spec = spec
+        P = local_params(spec, params, seed, self.rank, self.W, device)
+        self.base = TorchDeepFM(spec, hp, device, embedding_update=embedding_update, params=P, seed=seed,
+                                dropout_seed=dropout_seed if dropout_seed is not None else seed + 7919 * self.rank)
+        b = self.base
+        if self.W > 1:  # dense variables start identical (rank-0 broadcast, HVD:418)
+            from .dist import broadcast_tensors
+
+            broadcast_tensors([v for k, v in b.P.items() if k not in ("fm_w", "fm_v")])
+        self.hp, self.device, self.embedding_update = hp, b.device, embedding_update
+        self.n_loc = len(range(self.rank, self.V, self.W))
+
+    # ---- exchange -------------------------------------------------------------------------------
+    def _lookup(self, ids_flat: torch.Tensor):
+        W = self.W
+        uniq, inv = torch.unique(ids_flat, return_inverse=True)
+        owner = uniq % W
+        order = torch.argsort(owner, stable=True)
+        us = uniq[order]
+        sc_t = torch.bincount(owner, minlength=W)
+        if W > 1:
+            rc_t = torch.empty_like(sc_t)
+            all_to_all_equal(rc_t, sc_t)
+            sc, rc = sc_t.tolist(), rc_t.tolist()
+            recv_ids = all_to_all_var(us, sc, rc)
+        else:
+            sc = rc = [int(len(us))]
+            recv_ids = us
+        lr = recv_ids // W
+        P = self.base.P
+        rows = torch.cat([P["fm_w"][lr].unsqueeze(1), P["fm_v"][lr]], 1)
+        got = all_to_all_var(rows, rc, sc) if W > 1 else rows
+        rows_u = torch.empty_like(got)
+        rows_u[order] = got
+        return uniq, inv, rows_u, (order, sc, rc, lr)
+
+    def _push(self, g_u: torch.Tensor, route):
+        order, sc, rc, lr = route
+        gs = g_u[order]
+        gr = all_to_all_var(gs, sc, rc) if self.W > 1 else gs
+        lu, linv = torch.unique(lr, return_inverse=True)
+        acc = torch.zeros(len(lu), g_u.shape[1], dtype=torch.float64, device=g_u.device)
+        acc.index_add_(0, linv, gr.double())
+        return lu, (acc / self.W).float()
+
+    def _allreduce_dense(self, grads: Dict[str, torch.Tensor]) -> None:
+        if self.W == 1:
+            return
+        names = sorted(grads)
+        flat = torch.cat([grads[k].reshape(-1) for k in names])
+        all_reduce_(flat)
+        flat /= self.W
+        off = 0
+        for k in names:
+            n = grads[k].numel()
+            grads[k].copy_(flat[off:off + n].view_as(grads[k]))
+            off += n
+
+    # ---- training -------------------------------------------------------------------------------
+    def set_lr_scale(self, s: float) -> None:
+        self.base.set_lr_scale(s)
+
+    def train_step(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        from ..models.deepfm import data_loss, forward
+
+        b, spec = self.base, self.spec
+        ids = ids.to(self.device).long()
+        vals = vals.to(self.device).float()
+        labels = labels.to(self.device).float()
+        step = b.t + 1
+        hp = b._hp()
+        uniq, inv, rows_u, route = self._lookup(ids.reshape(-1))
+        inv = inv.reshape(ids.shape)
+        rw = rows_u[:, 0].clone().requires_grad_(True)
+        rv = rows_u[:, 1:].clone().requires_grad_(True)
+        dense_names = [k for k in b.trainable if k not in ("fm_w", "fm_v")]
+        params = dict(b.P)
+        for k in dense_names:
+            params[k] = b.P[k].requires_grad_(True)
+            params[k].grad = None
+        y = forward(params, ids, vals, spec, train=True, gen=b.gen, rows_w=rw[inv], rows_v=rv[inv])
+        loss = data_loss(y, labels, spec.loss_type)
+        loss.backward()
+        dgrads = {k: params[k].grad for k in dense_names}
+        for k in dense_names:
+            b.P[k].requires_grad_(False)
+        lu, g = self._push(torch.cat([rw.grad.unsqueeze(1), rv.grad], 1), route)
+        fw, fv = b.P["fm_w"], b.P["fm_v"]
+        if self.embedding_update == "exact":  # full-table L2 on the owner's shard (PS:277-278)
+            Gw = torch.zeros_like(fw)
+            Gv = torch.zeros_like(fv)
+            Gw[lu] = g[:, 0]
+            Gv[lu] = g[:, 1:]
+            apply_dense(hp, fw, Gw + spec.l2_reg * fw, b.slots["fm_w"], step)
+            apply_dense(hp, fv, Gv + spec.l2_reg * fv, b.slots["fm_v"], step)
+        else:  # lazy L2 on the rows touched by any rank, once
+            gw = g[:, 0] + spec.l2_reg * fw[lu]
+            gv = g[:, 1:] + spec.l2_reg * fv[lu]
+            apply_rows(hp, fw, lu, gw, b.slots["fm_w"], step)
+            apply_rows(hp, fv, lu, gv, b.slots["fm_v"], step)
+        self._allreduce_dense(dgrads)
+        for k in dense_names:
+            apply_dense(hp, b.P[k], dgrads[k], b.slots[k], step)
+        b.t += 1
+        b._last_loss_t, b._last_has_l2 = loss.detach(), False
+        return loss.detach()
+
+    # ---- inference (collective: every rank calls it the same number of times) --------------------
+    @torch.no_grad()
+    def predict_batch(self, ids, vals, labels=None):
+        from ..models.deepfm import forward
+
+        ids = ids.to(self.device).long()
+        vals = vals.to(self.device).float()
+        uniq, inv, rows_u, _ = self._lookup(ids.reshape(-1))
+        inv = inv.reshape(ids.shape)
+        if ids.shape[0] == 0:
+            z = torch.zeros(0, device=self.device)
+            return z, z
+        y = forward(self.base.P, ids, vals, self.spec, train=False, rows_w=rows_u[:, 0][inv],
+                    rows_v=rows_u[:, 1:][inv])
+        p = torch.sigmoid(y)
+        if labels is None:
+            return p, torch.zeros_like(p)
+        labels = labels.to(self.device).float()
+        if self.spec.loss_type == "log_loss":
+            lr = torch.clamp(y, min=0) - y * labels + torch.log1p(torch.exp(-y.abs()))
+        else:
+            lr = (p - labels) ** 2
+        return p, lr
+
+    # ---- bookkeeping ----------------------------------------------------------------------------
+    def l2_value(self) -> float:
+        P = self.base.P
+        t = torch.tensor([float((P["fm_w"].double() ** 2).sum() + (P["fm_v"].double() ** 2).sum())],
+                         dtype=torch.float64, device=self.device)
+        if self.W > 1:
+            all_reduce_(t)
+        return float(self.spec.l2_reg * 0.5 * t.item())
+
+    def batch_loss(self, include_l2: bool = True) -> float:
+        v = self.base.batch_loss(include_l2=False)
+        return v + (self.l2_value() if include_l2 else 0.0)
+
+    def global_step(self) -> int:
+        return self.base.t
+
+    def row_sets(self) -> Dict[str, torch.Tensor]:
+        rows = shard_rows(self.V, self.W, self.rank)
+        names = ["fm_w", "fm_v"] + [f"{t}/{s}" for t in ("fm_w", "fm_v") for s in slot_names(self.hp.name)]
+        return {k: rows for k in names}
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """Local shard (row-sharded variables trimmed to this rank's real rows) + dense state."""
+        sd = self.base.state_dict()
+        for k in self.row_sets():
+            sd[k] = sd[k][: self.n_loc].clone()
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
+        self.base.load_state_dict(sd, strict=strict)
+
+    def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
+        """Full variables (collective: the tables are gathered from every rank)."""
+        out = self.base.parameters_tf()
+        if self.W > 1:
+            out["fm_w"] = _gather_table(self.base.P["fm_w"], self.V, self.W).cpu()
+            out["fm_v"] = _gather_table(self.base.P["fm_v"], self.V, self.W).cpu()
+        else:
+            out["fm_w"], out["fm_v"] = out["fm_w"][: self.V], out["fm_v"][: self.V]
+        return out
+
+
+def _localize(sd, row_names, V, W, rank, Vs, n_loc):
+    """Map checkpoint rows to this shard: full tables ([V,…]) are sliced, local ones ([n_loc,…])
+    padded to Vs rows."""
+    out = dict(sd)
+    for k in row_names:
+        if k not in sd:
+            continue
+        t = sd[k]
+        if t.shape[0] == n_loc and not (t.shape[0] == V and W > 1):
+            pad = torch.zeros((Vs,) + tuple(t.shape[1:]), dtype=t.dtype)
+            pad[:n_loc] = t
+            out[k] = pad
+        elif t.shape[0] == V:
+            out[k] = slice_rows(t, V, W, rank)
+        else:
+            raise ValueError(f"{k}: {t.shape[0]} rows is neither the full table ({V}) nor this shard ({n_loc})")
+    return out
+
+
+# ================================================================================================
+# fused HIP engine
+# ================================================================================================
+class FusedRowShard:
+    """Row-sharded DeepFM on the fused HIP step (one GPU per process)."""
+
+    row_sharded = True
+    collective_predict = True
+
+    def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
+                 embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
+                 capacity: Optional[int] = None, check_every: int = 256):
+        from ..models.fused import FusedDeepFM
+
+        W, r = _world_rank()
+        self.W, self.rank = W, r
+        self.V = spec.feature_size
+        self.Vs = Vs = shard_size(self.V, W)
+        self.n_loc = len(range(r, self.V, W))
+        self.spec, self.hp = spec, hp
+        dev = torch.device(device)
+        P = local_params(spec, params, seed, r, W, dev)
+        spec_loc = dataclasses.replace(spec, feature_size=Vs)
+        self.eng = e = FusedDeepFM(spec_loc, hp, batch_size, dev, embedding_update=embedding_update, seed=seed,
+                                   params=P, use_graph=False, fuse_dense_opt=False,
+                                   dropout_seed=seed + 7919 * r)
+        del P
+        self.H, self.device, self.embedding_update = e.H, e.device, embedding_update
+        self.use_graph, self.check_every = use_graph, int(check_every)
+        if W > 1:
+            from .dist import broadcast_tensors
+
+            broadcast_tensors([e.dense] + list(e.dense_slots))
+            e.refresh_bf16()
+        H, B, F, Kp = e.H, e.B, e.F, e.Kp
+        n = e.n_lookup
+        self.n = n
+        cap = int(capacity) if capacity else min(n, int(math.ceil(1.25 * n / W)) + 64)
+        self.cap = cap = max(1, min(cap, n))
+        M = W * cap
+        self.M = M
+        i32 = dict(dtype=torch.int32, device=dev)
+        # ---- routing buffers (parity q = the step that will consume them) ----
+        self.route_bits = max(1, math.ceil(math.log2(max(W * Vs, 2))))
+        self.rkeys = torch.zeros(n, **i32)
+        self.rsk = torch.zeros(n, **i32)
+        self.rsv = [torch.zeros(n, **i32) for _ in range(2)]
+        self.send_ids = [torch.full((M,), PAD, **i32) for _ in range(2)]
+        self.local_idx = [torch.zeros(e.Bp, F, **i32) for _ in range(2)]
+        self.skl = [torch.zeros(n, **i32) for _ in range(2)]
+        self.counts = [torch.zeros(W, **i32) for _ in range(2)]
+        self.overflow = torch.zeros(1, **i32)
+        self.bad = torch.zeros(1, **i32)
+        self.route_temp = torch.zeros(max(H.sort_pairs_temp_bytes(n, self.route_bits), 16), dtype=torch.uint8,
+                                      device=dev)
+        # ---- exchange buffers ----
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.recv_ids = torch.full((M,), PAD, **i32)
+        self.rows_out = torch.zeros(M, Kp, **f32)
+        self.rows_in = torch.zeros(M, Kp, **f32)
+        self.grad_stage = torch.zeros(M, Kp, **f32)
+        self.grad_back = torch.zeros(M, Kp, **f32)
+        self.olk = torch.zeros(M, **i32)
+        self.osk = torch.zeros(M, **i32)
+        self.osv = torch.zeros(M, **i32)
+        self.owner_bits = max(1, math.ceil(math.log2(Vs + 1)))
+        self.osort_temp = torch.zeros(max(H.sort_pairs_temp_bytes(M, self.owner_bits), 16), dtype=torch.uint8,
+                                      device=dev)
+        self.osort_stream = torch.cuda.Stream(device=dev)
+        # prediction routing (own buffers: never races the pipelined training route)
+        self.pred_rsv = torch.zeros(n, **i32)
+        self.pred_send = torch.full((M,), PAD, **i32)
+        self.pred_local = torch.zeros(e.Bp, F, **i32)
+        self.pred_skl = torch.zeros(n, **i32)
+        self.pred_counts = torch.zeros(W, **i32)
+        self._graphs: Dict = {}
+        self._warm = 0
+        self._build()
+
+    # ---- kernel parameter blocks ------------------------------------------------------------------
+    def _route_params(self, ids, rsv, send, local, skl, counts, n):
+        H = self.H
+        kp = H.ShardKeysParams()
+        kp.ids, kp.n, kp.W, kp.Vs, kp.keys = ids.data_ptr(), n, self.W, self.Vs, self.rkeys.data_ptr()
+        rp = H.ShardRouteParams()
+        rp.skeys, rp.svals, rp.n = self.rsk.data_ptr(), rsv.data_ptr(), n
+        rp.W, rp.Vs, rp.cap = self.W, self.Vs, self.cap
+        rp.send_ids, rp.local_idx, rp.skeys_local = send.data_ptr(), local.data_ptr(), skl.data_ptr()
+        rp.counts, rp.overflow = counts.data_ptr(), self.overflow.data_ptr()
+        return kp, rp
+
+    def _build(self):
+        e, H = self.eng, self.H
+        self.route = [self._route_params(e.slot_ids[q], self.rsv[q], self.send_ids[q], self.local_idx[q], self.skl[q],
+                                         self.counts[q], self.n) for q in range(2)]
+        sv = H.ShardServeParams()
+        sv.ids, sv.m, sv.W, sv.rank, sv.Vs = self.recv_ids.data_ptr(), self.M, self.W, self.rank, self.Vs
+        sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), self.olk.data_ptr()
+        sv.bad = self.bad.data_ptr()
+        self.serve = sv
+        pv = H.ShardServeParams()
+        pv.ids, pv.m, pv.W, pv.rank, pv.Vs = self.recv_ids.data_ptr(), self.M, self.W, self.rank, self.Vs
+        pv.table, pv.Kp, pv.rows_out, pv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
+        pv.bad = self.bad.data_ptr()
+        self.pred_serve = pv
+        self.owner_params = []
+        for p in range(2):
+            rp = e.rows_params[p]
+            rp.ids, rp.emb = self.local_idx[p].data_ptr(), self.rows_in.data_ptr()
+            lp = e.emb_params[p]  # local: Σ lookup grads per received row → grad_stage
+            lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
+            lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
+            op = H.EmbUpdateParams()  # owner: Σ over source ranks per local row → optimizer
+            op.skeys, op.svals, op.n = self.osk.data_ptr(), self.osv.data_ptr(), self.M
+            op.contrib, op.K1, op.Kp = self.grad_back.data_ptr(), e.K1, e.Kp
+            op.emb = e.emb.data_ptr()
+            op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
+            op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
+            op.opt, op.step = e._opt(p), e.steps[p:].data_ptr()
+            op.max_key = self.Vs
+            if self.embedding_update == "exact":
+                op.mode, op.dense_grad = 1, e.dense_grad.data_ptr()
+                e.emb_dense_params[p].grad_scale = 1.0
+            else:
+                op.mode = 0
+            self.owner_params.append(op)
+            da = e.dense_apply_params[p]
+            da.apply, da.grads, da.grad_scale = 1, e.dense_grads_flat.data_ptr(), 1.0 / self.W
+            e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
+        pp = e.pred_params
+        pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
+        self.pred_route = self._route_params(e.pred_ids, self.pred_rsv, self.pred_send, self.pred_local,
+                                             self.pred_skl, self.pred_counts, self.n)
+
+    # ---- batch feeding (delegated) ------------------------------------------------------------
+    def attach_pool(self, ids, vals, labels, start: int = 0):
+        self.eng.attach_pool(ids, vals, labels, start)
+        self._graphs = {}
+
+    def push_batch(self, ids, vals, labels):
+        self.eng.push_batch(ids, vals, labels)
+
+    def load_batch(self, ids, vals, labels=None):
+        self.eng.load_batch(ids, vals, labels)
+
+    def set_lr_scale(self, s: float) -> None:
+        e = self.eng
+        e.set_lr_scale(s)
+        for p in range(2):
+            self.owner_params[p].opt = e._opt(p)
+        self._graphs = {}
+
+    # ---- step pieces ---------------------------------------------------------------------------
+    def _route_launch(self, rt, n, stream) -> None:
+        kp, rp = rt
+        H, s = self.H, stream.cuda_stream
+        if n > 0:
+            H.shard_keys(kp, s)
+            H.sort_pairs_iota(self.route_temp.data_ptr(), self.route_temp.numel(), self.rkeys.data_ptr(),
+                              self.rsk.data_ptr(), rp.svals, n, self.route_bits, s)
+        H.shard_route(rp, s)
+
+    def prime(self) -> None:
+        e = self.eng
+        e.prime()  # fetch the current batch into its slot
+        self._route_launch(self.route[e._i % 2], self.n, torch.cuda.current_stream(self.device))
+        e._primed = True
+
+    def _fork_next(self, p: int):
+        e = self.eng
+        main = torch.cuda.current_stream(self.device)
+        side = e.sort_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            e.H.fetch_batch(e.fetch_params[p], side.cuda_stream)
+            self._route_launch(self.route[1 - p], self.n, side)
+        return side
+
+    def _phase_serve(self, p: int) -> None:
+        self.H.shard_serve(self.serve, self.eng.stream_ptr)
+
+    def _phase_compute(self, p: int) -> None:
+        e, H = self.eng, self.H
+        main = torch.cuda.current_stream(self.device)
+        side = self._fork_next(p)
+        os_ = self.osort_stream
+        os_.wait_stream(main)
+        with torch.cuda.stream(os_):
+            H.sort_pairs_iota(self.osort_temp.data_ptr(), self.osort_temp.numel(), self.olk.data_ptr(),
+                              self.osk.data_ptr(), self.osv.data_ptr(), self.M, self.owner_bits, os_.cuda_stream)
+        aux = e._enqueue_rows_then_fork_wgrad(p)
+        H.emb_rows_update(e.emb_params[p], main.cuda_stream)
+        e._join(aux)
+        e._join(os_)
+        e._join(side)
+
+    def _phase_update(self, p: int) -> None:
+        e, H = self.eng, self.H
+        s = e.stream_ptr
+        H.emb_rows_update(self.owner_params[p], s)
+        if self.embedding_update == "exact":
+            H.emb_dense_update(e.emb_dense_params[p], s)
+        H.dense_apply(e.dense_apply_params[p], s)
+
+    def _run(self, key, fn):
+        if not self.use_graph or self._warm < 4:
+            fn()
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(g):
+                fn()
+            self._graphs[key] = g
+        g.replay()
+
+    def _exchange(self, out, inp):
+        if self.W > 1:
+            all_to_all_equal(out, inp)
+        else:
+            out.copy_(inp)
+
+    def train_step(self) -> None:
+        e = self.eng
+        if not e._primed:
+            self.prime()
+        p = e._i % 2
+        self._exchange(self.recv_ids, self.send_ids[p])                       # X1 requests
+        self._run(("serve", p), lambda: self._phase_serve(p))
+        self._exchange(self.rows_in, self.rows_out)                            # X2 rows
+        self._run(("compute", p), lambda: self._phase_compute(p))
+        self._exchange(self.grad_back, self.grad_stage)                        # X3 row grads
+        if self.W > 1:
+            all_reduce_(e.dense_grads_flat)                                    # X4 MLP grads
+        self._run(("update", p), lambda: self._phase_update(p))
+        self._warm += 1
+        e._i += 1
+        if self.check_every and e._i % self.check_every == 0:
+            self.check()
+
+    def train_steps(self, n: int, steps_per_graph: int = 0) -> None:
+        for _ in range(n):
+            self.train_step()
+
+    def train_on(self, batches):
+        it = iter(batches)
+        cur = next(it, None)
+        if cur is None:
+            return
+        self.load_batch(*cur)
+        nxt = next(it, None)
+        while True:
+            if nxt is not None:
+                self.push_batch(*nxt)
+            self.train_step()
+            yield
+            if nxt is None:
+                break
+            nxt = next(it, None)
+
+    def check(self) -> None:
+        """Raise if any owner's request list overflowed the exchange capacity (or a request was
+        routed to the wrong owner) since construction."""
+        ov, bad = int(self.overflow.item()), int(self.bad.item())
+        if ov:
+            c = torch.stack(self.counts).max().item()
+            raise RuntimeError(f"row-shard exchange overflow: an owner needed {c} rows > capacity {self.cap}; "
+                               f"rebuild with capacity >= {c} (or capacity=batch_size*field_size)")
+        if bad:
+            raise RuntimeError("row-shard routing error: a rank received ids it does not own")
+
+    # ---- inference (collective) ------------------------------------------------------------------
+    @torch.no_grad()
+    def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
+        e = self.eng
+        nrows = int(ids.shape[0])
+        nch = max(1, (nrows + e.B - 1) // e.B)
+        if self.W > 1:
+            t = torch.tensor([nch], dtype=torch.int64, device=self.device if dist.get_backend() == "nccl" else "cpu")
+            all_reduce_(t, dist.ReduceOp.MAX)
+            nch = int(t.item())
+        probs, losses = [], []
+        for c in range(nch):
+            a, b = min(c * e.B, nrows), min((c + 1) * e.B, nrows)
+            m = b - a
+            if m:
+                e.pred_ids[:m].copy_(ids[a:b])
+                e.pred_vals[:m].copy_(vals[a:b])
+                if labels is not None:
+                    e.pred_labels[:m].copy_(labels[a:b])
+                else:
+                    e.pred_labels.zero_()
+            kp, rp = self.pred_route
+            kp.n = rp.n = m * e.F
+            self._route_launch(self.pred_route, m * e.F, torch.cuda.current_stream(self.device))
+            self._exchange(self.recv_ids, self.pred_send)
+            self.H.shard_serve(self.pred_serve, e.stream_ptr)
+            self._exchange(self.rows_in, self.rows_out)
+            if m:
+                pp = e.pred_params
+                pp.B = m
+                self.H.deepfm_rows(pp, e.stream_ptr)
+                probs.append(e.pred_prob[:m].clone())
+                losses.append(e.pred_loss[:m].clone())
+        if not probs:
+            z = torch.zeros(0, device=self.device)
+            return z, z
+        return torch.cat(probs), torch.cat(losses)
+
+    # ---- bookkeeping ----------------------------------------------------------------------------
+    def l2_value(self) -> float:
+        e = self.eng
+        nb = 1024
+        part = torch.zeros(nb, dtype=torch.float32, device=self.device)
+        self.H.emb_sumsq(e.emb.data_ptr(), e.V * e.Kp // 4, e.Kp, e.K1, part.data_ptr(), nb, e.stream_ptr)
+        t = part.double().sum().reshape(1)
+        if self.W > 1:
+            all_reduce_(t)
+        return float(self.spec.l2_reg * 0.5 * t.item())
+
+    def batch_loss(self, include_l2: bool = True) -> float:
+        v = self.eng.batch_loss(include_l2=False)
+        return v + (self.l2_value() if include_l2 else 0.0)
+
+    def global_step(self) -> int:
+        return self.eng._i
+
+    def row_sets(self) -> Dict[str, torch.Tensor]:
+        rows = shard_rows(self.V, self.W, self.rank)
+        names = ["fm_w", "fm_v"] + [f"{t}/{s}" for t in ("fm_w", "fm_v") for s in slot_names(self.hp.name)]
+        return {k: rows for k in names}
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        sd = self.eng.state_dict()
+        for k in self.row_sets():
+            sd[k] = sd[k][: self.n_loc].clone()
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
+        self.eng.load_state_dict(sd, strict=strict)
+        self._graphs = {}
+        self._warm = 0
+
+    def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
+        e = self.eng
+        out = e.parameters_tf()
+        if self.W > 1:
+            out["fm_w"] = _gather_table(e.emb[:, e.K].contiguous(), self.V, self.W).cpu()
+            out["fm_v"] = _gather_table(e.emb[:, : e.K].contiguous(), self.V, self.W).cpu()
+        else:
+            out["fm_w"], out["fm_v"] = out["fm_w"][: self.V], out["fm_v"][: self.V]
+        return out
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["eng"], name)

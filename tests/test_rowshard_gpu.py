@@ -1,0 +1,178 @@
+"""Row-shard HIP path: routing kernels vs the numpy oracle; the fused row-shard step (1 rank, and 2
+ranks sharing one GPU over gloo) ≡ the single-GPU fused step on the union batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _route(ids, W, V, cap):
+    from rocfm.ops import require_hip
+
+    H = require_hip()
+    n = ids.numel()
+    Vs = (V + W - 1) // W
+    dev = ids.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    keys, sk, sv = (torch.zeros(n, **i32) for _ in range(3))
+    send = torch.zeros(W * cap, **i32)
+    local = torch.zeros(n, **i32)
+    skl = torch.zeros(n, **i32)
+    counts = torch.zeros(W, **i32)
+    ov = torch.zeros(1, **i32)
+    bits = int(np.ceil(np.log2(max(W * Vs, 2))))
+    temp = torch.zeros(max(H.sort_pairs_temp_bytes(n, bits), 16), dtype=torch.uint8, device=dev)
+    kp = H.ShardKeysParams()
+    kp.ids, kp.n, kp.W, kp.Vs, kp.keys = ids.data_ptr(), n, W, Vs, keys.data_ptr()
+    s = torch.cuda.current_stream().cuda_stream
+    H.shard_keys(kp, s)
+    H.sort_pairs_iota(temp.data_ptr(), temp.numel(), keys.data_ptr(), sk.data_ptr(), sv.data_ptr(), n, bits, s)
+    rp = H.ShardRouteParams()
+    rp.skeys, rp.svals, rp.n, rp.W, rp.Vs, rp.cap = sk.data_ptr(), sv.data_ptr(), n, W, Vs, cap
+    rp.send_ids, rp.local_idx, rp.skeys_local = send.data_ptr(), local.data_ptr(), skl.data_ptr()
+    rp.counts, rp.overflow = counts.data_ptr(), ov.data_ptr()
+    H.shard_route(rp, s)
+    torch.cuda.synchronize()
+    return send.cpu().numpy(), local.cpu().numpy(), counts.cpu().numpy(), int(ov.item()), skl, sv, local
+
+
+@pytest.mark.parametrize("W,n,V", [(1, 3000, 500), (3, 40000, 100003), (8, 39 * 1024, 1_000_000)])
+def test_shard_route_matches_reference(W, n, V):
+    from rocfm.ops.reference import shard_route_reference
+
+    g = torch.Generator().manual_seed(W * 7 + 1)
+    ids = torch.randint(0, V, (n,), generator=g, dtype=torch.int32)
+    ids[::5] = 17  # hot id
+    ids[1::7] = torch.randint(0, 50, (len(ids[1::7]),), generator=g, dtype=torch.int32)
+    cap = n
+    send, local, counts, ov, skl, sv, local_t = _route(ids.cuda(), W, V, cap)
+    rs, rl, rc = shard_route_reference(ids.numpy(), W, (V + W - 1) // W, cap)
+    assert ov == 0
+    np.testing.assert_array_equal(counts, rc)
+    np.testing.assert_array_equal(send.astype(np.int64).reshape(W, cap), rs)
+    np.testing.assert_array_equal(local, rl)
+    # sorted local keys are the lookup rows in sort order
+    np.testing.assert_array_equal(skl.cpu().numpy(), local_t[sv.long()].cpu().numpy())
+
+
+def test_shard_route_overflow_flag():
+    ids = torch.arange(0, 4000, dtype=torch.int32).cuda()  # 2000 unique ids per owner
+    _, _, counts, ov, *_ = _route(ids, 2, 4000, 1000)
+    assert ov == 1 and counts.tolist() == [2000, 2000]
+
+
+def _cfg(opt="Adam"):
+    from rocfm.models.deepfm import ModelSpec
+    from rocfm.optim import OptHParams
+
+    spec = ModelSpec(feature_size=4001, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[1.0, 1.0],
+                     l2_reg=1e-3)
+    return spec, OptHParams(name=opt, lr=1e-3)
+
+
+def _batches(B, n, seed):
+    from rocfm.data.synthetic import SyntheticCriteo
+
+    g = torch.Generator().manual_seed(seed)
+    gen = SyntheticCriteo(4001, 39, seed=seed)
+    return [gen.batch(B, "cpu", g) for _ in range(n)]
+
+
+def _single(update, nsteps, B=128, opt="Adam"):
+    from rocfm.models.deepfm import init_params
+    from rocfm.models.fused import FusedDeepFM
+
+    spec, hp = _cfg(opt)
+    single = FusedDeepFM(spec, hp, B, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
+                         embedding_update=update)
+    batches = _batches(128, nsteps, 11)
+    single.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
+                       torch.stack([b[2] for b in batches]).cuda())
+    for _ in range(nsteps):
+        single.train_step()
+    torch.cuda.synchronize()
+    return single
+
+
+@pytest.mark.parametrize("update,graph", [("sparse", False), ("sparse", True), ("exact", False)])
+def test_fused_rowshard_world1_equals_single(update, graph):
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg()
+    n = 10
+    eng = FusedRowShard(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=update,
+                        use_graph=graph)
+    batches = _batches(128, n, 11)
+    eng.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
+                    torch.stack([b[2] for b in batches]).cuda())
+    for _ in range(n):
+        eng.train_step()
+    torch.cuda.synchronize()
+    eng.check()
+    ref = _single(update, n)
+    got = eng.parameters_tf()
+    exp = ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got[k], exp[k], rtol=2e-3, atol=2e-5)
+    ids, vals, labels = _batches(100, 1, 5)[0]
+    p, _ = eng.predict_batch(ids.cuda(), vals.cuda())
+    pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
+    torch.testing.assert_close(p, pr, rtol=1e-4, atol=1e-5)
+
+
+def _worker(rank, world, port, update, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg()
+    B = 64
+    eng = FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), embedding_update=update,
+                        use_graph=False)
+    batches = _batches(2 * B, 3, 11)
+    pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
+            for b in batches]
+    eng.attach_pool(torch.stack([x[0] for x in pool]).cuda(), torch.stack([x[1] for x in pool]).cuda(),
+                    torch.stack([x[2] for x in pool]).cuda())
+    for _ in range(3):
+        eng.train_step()
+    torch.cuda.synchronize()
+    eng.check()
+    P = eng.parameters_tf()
+    ids, vals, _ = _batches(100, 1, 5)[0]
+    p, _ = eng.predict_batch(ids.cuda() if rank == 0 else ids[:0].cuda(), vals.cuda() if rank == 0 else vals[:0].cuda())
+    if rank == 0:
+        torch.save({"P": dict(P), "pred": p.cpu()}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_rowshard_2ranks_equals_single_gpu_union_batch(tmp_path, update):
+    out = str(tmp_path / "rs.pt")
+    mp.start_processes(_worker, args=(2, _free_port(), update, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    ref = _single(update, 3)
+    exp = ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got["P"][k], exp[k], rtol=2e-3, atol=2e-5)
+    ids, vals, _ = _batches(100, 1, 5)[0]
+    pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
+    torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
