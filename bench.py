@@ -57,7 +57,9 @@ def parse():
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--steps_per_graph", type=int, default=8, help="fused engine: steps captured per HIP graph")
-    ap.add_argument("--shard_capacity", type=int, default=0, help="rowshard: per-owner exchange rows (0 = auto)")
+    ap.add_argument("--capacity", default="auto",
+                    help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
+                         "over the batch pool, 'safe' = batch_size*field_size (never overflows), or a number")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json_out", default="")
     return ap.parse_args()
@@ -78,10 +80,17 @@ def main():
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
                "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000), __file__] + sys.argv[1:]
         sys.exit(subprocess.call(cmd))
+    # ROCFM_BENCH_BACKEND=gloo rehearses the N>1 code path with ranks sharing the visible GPUs
+    # (host-staged collectives); the real multi-GPU run uses nccl (= RCCL over xGMI), one GPU per rank.
+    backend = os.environ.get("ROCFM_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from rocfm.data.synthetic import SyntheticCriteo
     from rocfm.models.deepfm import ModelSpec, init_params
@@ -107,17 +116,25 @@ def main():
     parallelism = a.parallelism
     if parallelism == "auto":
         parallelism = "dp" if a.embedding_update == "sparse" else "dense_dp"
+    cap = None
+    if a.engine == "fused" and (world > 1 or parallelism == "rowshard") and parallelism != "dense_dp":
+        if a.capacity == "auto":
+            from rocfm.parallel.dp import pool_exchange_capacity
+
+            cap = pool_exchange_capacity(pool_ids, world if parallelism == "rowshard" else 1)
+        elif a.capacity != "safe":
+            cap = int(a.capacity)
     if a.engine == "fused":
         if parallelism == "rowshard":
             from rocfm.parallel.emb_shard import FusedRowShard
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
-                                use_graph=not a.no_graph, capacity=a.shard_capacity or None)
+                                use_graph=not a.no_graph, capacity=cap)
         elif world > 1:
             from rocfm.parallel.dp import FusedDataParallel
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
-                                    mode=parallelism, seed=a.seed, use_graph=not a.no_graph)
+                                    mode=parallelism, seed=a.seed, use_graph=not a.no_graph, capacity=cap)
         else:
             from rocfm.models.fused import FusedDeepFM
 
@@ -195,6 +212,7 @@ def main():
             "parallelism": f"{parallelism}{world}" if (world > 1 or parallelism == "rowshard") else "dp1",
             "engine": a.engine,
             "embedding_update": a.embedding_update,
+            "exchange_capacity": cap,
         },
     }
     if rank == 0:

@@ -1,0 +1,47 @@
+// Multi-source row-gradient merge by direct addressing (merge.hip).
+//
+// W source lists (one per rank) each hold UNIQUE keys with one gradient row per key — the DP
+// all-gather of every rank's (id, Σ grad) export, or an owner's per-source requests in row-shard
+// mode.  Instead of radix-sorting the W·cap gathered keys, two kernels use HBM-resident position
+// maps (W × Vmap int32, 32 MB for a 1M vocabulary at W=8; kept at −1 between steps):
+//   merge_scatter : pos[r][key] = j ; rep[key] = min r holding key
+//   merge_apply   : the representative entry (r == rep[key]) sums the rows of key over r..W−1 in
+//                   rank order (deterministic, no float atomics), applies lazy L2 + the row
+//                   optimizer (or writes a dense gradient row), and restores pos/rep.
+#pragma once
+#include "../common.h"
+#include "optim.h"
+
+namespace rocfm {
+
+struct MergeParams {
+  // source r: keys at keys + r*key_stride, rows at rows + r*row_stride ([cap][Kp] f32),
+  // count at counts[r*count_stride] (nullable: lists are padded with key 0xFFFFFFFF instead)
+  const uint32_t* keys;
+  long long key_stride;
+  const float* rows;
+  long long row_stride;
+  const int32_t* counts;
+  long long count_stride;
+  int W, cap, Kp, K1;
+  uint32_t key_div;   // table row = key / key_div (1: DP; W: row-shard owner, global id → local row)
+  uint32_t Vmap;      // rows of the table / maps
+  int32_t* pos;       // [W][Vmap], -1 = empty
+  int32_t* rep;       // [Vmap], W = none
+  // apply
+  float* emb;  // [Vmap][Kp]
+  float* s0;
+  float* s1;
+  float l2;
+  float grad_scale;
+  OptParams opt;
+  const int64_t* step;
+  int mode;           // 0: lazy L2 + optimizer on the rows; 1: dense_grad[row] = Σ · grad_scale
+  float* dense_grad;  // mode 1
+};
+
+void launch_merge_scatter(const MergeParams& p, hipStream_t stream);
+void launch_merge_apply(const MergeParams& p, hipStream_t stream);
+void launch_merge_init(const MergeParams& p, hipStream_t stream);  // pos = −1, rep = W
+
+}  // namespace rocfm

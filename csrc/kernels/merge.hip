@@ -1,0 +1,188 @@
+// Multi-source row-gradient merge by direct addressing — see merge.h.
+#include "merge.h"
+
+namespace rocfm {
+namespace {
+
+constexpr uint32_t kPadKey = 0xFFFFFFFFu;
+constexpr int kMergeThreads = 256;
+constexpr int kMaxW = 64;
+
+__device__ __forceinline__ bool entry_valid(const MergeParams& p, int r, int j, uint32_t key) {
+  if (key == kPadKey) return false;
+  if (p.counts && j >= p.counts[(size_t)r * p.count_stride]) return false;
+  return key / p.key_div < p.Vmap;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_init_kernel(MergeParams p) {
+  const long long i = (long long)blockIdx.x * kMergeThreads + threadIdx.x;
+  const long long n = (long long)p.W * p.Vmap;
+  if (i < n) p.pos[i] = -1;
+  if (i < p.Vmap) p.rep[i] = p.W;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParams p) {
+  const int i = blockIdx.x * kMergeThreads + threadIdx.x;
+  if (i >= p.W * p.cap) return;
+  const int r = i / p.cap, j = i - r * p.cap;
+  const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
+  if (!entry_valid(p, r, j, key)) return;
+  const uint32_t row = key / p.key_div;
+  p.pos[(size_t)r * p.Vmap + row] = j;
+  atomicMin(&p.rep[row], r);
+}
+
+// One thread per source entry; only representatives (lowest rank holding the key) do work.
+// WMAX = 8 (one node): every later source's position and row are loaded before any is summed.
+template <int KP4, int WMAX>
+__global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams p) {
+  const int i = blockIdx.x * kMergeThreads + threadIdx.x;
+  if (i >= p.W * p.cap) return;
+  const int r = i / p.cap, j = i - r * p.cap;
+  const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
+  if (!entry_valid(p, r, j, key)) return;
+  const uint32_t row = key / p.key_div;
+  if (p.rep[row] != r) return;
+  const int W = p.W;
+  float4 acc[KP4];
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (WMAX <= 8 && KP4 <= 4) {
+    int pj[WMAX];
+#pragma unroll
+    for (int q = 0; q < WMAX; ++q)
+      pj[q] = (q < W && q > r) ? p.pos[(size_t)q * p.Vmap + row] : (q == r ? j : -1);
+    float4 v[WMAX][KP4];
+#pragma unroll
+    for (int q = 0; q < WMAX; ++q) {
+      const float4* src = reinterpret_cast<const float4*>(
+          p.rows + (pj[q] >= 0 ? (size_t)q * p.row_stride + (size_t)pj[q] * p.Kp : 0));
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) v[q][c] = src[c];
+    }
+#pragma unroll
+    for (int q = 0; q < WMAX; ++q) {  // rank order: deterministic sum
+      if (pj[q] < 0) continue;
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) {
+        acc[c].x += v[q][c].x;
+        acc[c].y += v[q][c].y;
+        acc[c].z += v[q][c].z;
+        acc[c].w += v[q][c].w;
+      }
+    }
+  } else {
+    for (int q = r; q < W; ++q) {  // rank order: deterministic sum
+      const int pq = q == r ? j : p.pos[(size_t)q * p.Vmap + row];
+      if (pq < 0) continue;
+      const float4* src = reinterpret_cast<const float4*>(p.rows + (size_t)q * p.row_stride + (size_t)pq * p.Kp);
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) {
+        const float4 v = src[c];
+        acc[c].x += v.x;
+        acc[c].y += v.y;
+        acc[c].z += v.z;
+        acc[c].w += v.w;
+      }
+    }
+  }
+  // restore the maps for the next step (no other thread reads them for this key any more)
+  for (int q = r; q < W; ++q) p.pos[(size_t)q * p.Vmap + row] = -1;
+  p.rep[row] = W;
+
+  const size_t base = (size_t)row * KP4;
+  if (p.mode == 1) {
+    float4* dg = reinterpret_cast<float4*>(p.dense_grad) + base;
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) {
+      float4 g = acc[c];
+      g.x *= p.grad_scale;
+      g.y *= p.grad_scale;
+      g.z *= p.grad_scale;
+      g.w *= p.grad_scale;
+      dg[c] = g;
+    }
+    return;
+  }
+  const OptStep st = opt_step(p.opt, *p.step);
+  float4* e4 = reinterpret_cast<float4*>(p.emb) + base;
+  float4* a4 = p.s0 ? reinterpret_cast<float4*>(p.s0) + base : nullptr;
+  float4* b4 = p.s1 ? reinterpret_cast<float4*>(p.s1) + base : nullptr;
+  float4 w[KP4], a[KP4], b[KP4];
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) {
+    w[c] = e4[c];
+    a[c] = a4 ? a4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    b[c] = b4 ? b4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) {
+    float* wc = &w[c].x;
+    float* ac = &a[c].x;
+    float* bc = &b[c].x;
+    const float* gc = &acc[c].x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (c * 4 + u >= p.K1) continue;
+      opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
+    }
+    e4[c] = w[c];
+    if (a4) a4[c] = a[c];
+    if (b4) b4[c] = b[c];
+  }
+}
+
+template <int KP4>
+void launch_apply_t(const MergeParams& p, hipStream_t stream) {
+  const dim3 grid(cdiv(p.W * p.cap, kMergeThreads)), block(kMergeThreads);
+  if (p.W <= 8)
+    hipLaunchKernelGGL((merge_apply_kernel<KP4, 8>), grid, block, 0, stream, p);
+  else
+    hipLaunchKernelGGL((merge_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p);
+}
+
+void check(const MergeParams& p) {
+  ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge: 1 <= W <= 64");
+  ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
+  ROCFM_REQUIRE(p.key_div >= 1 && p.pos && p.rep, "merge: maps/key_div");
+  ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
+}
+
+}  // namespace
+
+void launch_merge_init(const MergeParams& p, hipStream_t stream) {
+  check(p);
+  const long long n = (long long)p.W * p.Vmap;
+  hipLaunchKernelGGL(merge_init_kernel, dim3((unsigned)((n + kMergeThreads - 1) / kMergeThreads)),
+                     dim3(kMergeThreads), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_merge_scatter(const MergeParams& p, hipStream_t stream) {
+  check(p);
+  if (p.cap <= 0) return;
+  hipLaunchKernelGGL(merge_scatter_kernel, dim3(cdiv(p.W * p.cap, kMergeThreads)), dim3(kMergeThreads), 0, stream,
+                     p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_merge_apply(const MergeParams& p, hipStream_t stream) {
+  check(p);
+  if (p.cap <= 0) return;
+  ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : (p.emb != nullptr && p.step != nullptr),
+                "merge_apply: missing outputs");
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N)               \
+  case N:                          \
+    launch_apply_t<N>(p, stream);  \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("merge: unsupported Kp");
+  }
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rocfm

@@ -9,6 +9,7 @@
 #include "kernels/emb_update.h"
 #include "kernels/optim.h"
 #include "kernels/shard.h"
+#include "kernels/merge.h"
 
 namespace rocfm {
 

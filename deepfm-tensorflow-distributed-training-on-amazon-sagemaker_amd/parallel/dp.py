@@ -58,6 +58,23 @@ def _all_reduce(t: torch.Tensor) -> None:
     t.copy_(c)
 
 
+def pool_exchange_capacity(pool_ids: torch.Tensor, owners: int = 1) -> int:
+    """Exact exchange capacity for training on a known batch pool ([NB, B, F] ids): the largest
+    number of unique ids in any batch (``owners`` > 1: per owner ``id % owners``, the row-shard
+    request lists), MAX-reduced over ranks so every rank builds identical collective shapes."""
+    m = 1
+    for b in pool_ids:
+        u = torch.unique(b)
+        c = int(torch.bincount((u % owners).long(), minlength=owners).max()) if owners > 1 else int(u.numel())
+        m = max(m, c)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dev = pool_ids.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([m], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = int(t.item())
+    return m
+
+
 # ================================================================================================
 # eager engine hooks (CPU/gloo tests, PyTorch baseline)
 # ================================================================================================
@@ -112,7 +129,7 @@ class FusedDataParallel:
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", mode: str = "dp", seed: int = 1234, use_graph: bool = True,
-                 capacity: Optional[int] = None):
+                 capacity: Optional[int] = None, check_every: int = 256):
         from ..models.fused import FusedDeepFM
 
         self.world = _world()
@@ -129,6 +146,7 @@ class FusedDataParallel:
                                dropout_seed=seed + 7919 * self.rank)
         e = self.eng
         self.use_graph = use_graph
+        self.check_every = int(check_every)
         self.device = e.device
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
@@ -162,15 +180,11 @@ class FusedDataParallel:
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
             self.mlp_sum = torch.zeros(P, dtype=torch.float32, device=e.device)
-            self.mkeys = torch.zeros(self.world * cap, dtype=torch.int32, device=e.device)
-            self.msk = torch.zeros_like(self.mkeys)
-            self.msv = torch.zeros_like(self.mkeys)
-            self.merge_bits = max(1, math.ceil(math.log2(e.V + 1)))
-            tb = H.sort_pairs_temp_bytes(self.world * cap, self.merge_bits)
-            self.merge_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=e.device)
-            self.col = torch.arange(cap, dtype=torch.int32, device=e.device)
+            # merge maps (merge.hip): position of each key in every rank's list, representative rank
+            self.pos = torch.empty(self.world * e.V, dtype=torch.int32, device=e.device)
+            self.rep = torch.empty(e.V, dtype=torch.int32, device=e.device)
             e._build_params()
-            self.export_params = []
+            self.export_params, self.merge_params = [], []
             for p in range(2):
                 ex = H.EmbUpdateParams()
                 src = e.emb_params[p]
@@ -183,17 +197,24 @@ class FusedDataParallel:
                 ex.out_count = self.send[self.off_cnt:].data_ptr()
                 ex.out_cap = cap
                 self.export_params.append(ex)
-                m = e.emb_params[p]  # merge: the same row optimizer, fed by the gathered rows
-                m.skeys, m.svals = self.msk.data_ptr(), self.msv.data_ptr()
-                m.n = self.world * cap
-                m.contrib = self.recv[self.off_rows:].data_ptr()
-                m.contrib_seg = cap
-                m.contrib_seg_stride = self.S
-                m.max_key = e.V
-                m.grad_scale = 1.0 / self.world
+                mp_ = H.MergeParams()  # merge the gathered lists: Σ over ranks per id → row optimizer
+                mp_.keys = self.recv[self.off_keys:].data_ptr()
+                mp_.rows = self.recv[self.off_rows:].data_ptr()
+                mp_.counts = self.recv[self.off_cnt:].data_ptr()
+                mp_.key_stride = mp_.row_stride = mp_.count_stride = self.S
+                mp_.W, mp_.cap, mp_.Kp, mp_.K1 = self.world, cap, Kp, e.K1
+                mp_.key_div, mp_.Vmap = 1, e.V
+                mp_.pos, mp_.rep = self.pos.data_ptr(), self.rep.data_ptr()
+                mp_.emb = e.emb.data_ptr()
+                mp_.s0, mp_.s1 = e._slot_ptrs(e.emb_slots)
+                mp_.l2, mp_.grad_scale = float(spec.l2_reg), 1.0 / self.world
+                mp_.opt, mp_.step = e._opt(p), e.steps[p:].data_ptr()
+                mp_.mode = 0
+                self.merge_params.append(mp_)
                 e.dense_apply_params[p].apply = 1
                 e.dense_apply_params[p].grads = self.mlp_sum.data_ptr()
                 e.dense_apply_params[p].grad_scale = 1.0 / self.world
+            H.merge_init(self.merge_params[0], e.stream_ptr)
             self.recv2d = self.recv.view(self.world, self.S)
         for p in range(2):
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
@@ -216,6 +237,7 @@ class FusedDataParallel:
         if self.mode == "dp":
             for p in range(2):
                 self.export_params[p].opt = self.eng.emb_params[p].opt
+                self.merge_params[p].opt = self.eng._opt(p)
         self._graphs = {}
 
     # ---- step phases ---------------------------------------------------------------------------
@@ -248,13 +270,8 @@ class FusedDataParallel:
         P = e.layout.total
         torch.sum(self.recv2d[:, :P], dim=0, out=self.mlp_sum)  # rank order: deterministic
         e.H.dense_apply(e.dense_apply_params[p], s)
-        counts = self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, :1]
-        keys = self.recv2d[:, self.off_keys:self.off_keys + self.cap].contiguous().view(torch.int32)
-        self.mkeys.view(self.world, self.cap).copy_(
-            torch.where(self.col[None, :] < counts, keys, torch.full_like(keys, e.V)))
-        e.H.sort_pairs_iota(self.merge_temp.data_ptr(), self.merge_temp.numel(), self.mkeys.data_ptr(),
-                            self.msk.data_ptr(), self.msv.data_ptr(), self.world * self.cap, self.merge_bits, s)
-        e.H.emb_rows_update(e.emb_params[p], s)
+        e.H.merge_scatter(self.merge_params[p], s)
+        e.H.merge_apply(self.merge_params[p], s)
 
     def _run(self, key, fn):
         if not self.use_graph or self._warm < 4:
@@ -279,6 +296,20 @@ class FusedDataParallel:
         self._run(("b", p), lambda: self._phase_b(p))
         self._warm += 1
         e._i += 1
+        if self.check_every and e._i % self.check_every == 0:
+            self.check()
+
+    def train_steps(self, n: int, steps_per_graph: int = 0) -> None:
+        for _ in range(n):
+            self.train_step()
+
+    def check(self) -> None:
+        """Raise if a rank exported more unique rows than the exchange capacity (rows past the
+        capacity would have been dropped from that step's update)."""
+        if self.overflowed():
+            c = int(self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, 0].max())
+            raise RuntimeError(f"DP exchange overflow: a rank exported {c} unique rows > capacity {self.cap}; "
+                               f"rebuild with capacity >= {c} (default capacity = batch_size*field_size never overflows)")
 
     def overflowed(self) -> bool:
         """True if any rank produced more unique rows than the exchange capacity (never with the default cap)."""

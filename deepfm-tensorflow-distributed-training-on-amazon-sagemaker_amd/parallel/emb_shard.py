@@ -15,8 +15,8 @@ of HBM).  Every step, synchronously:
             each lookup's received-row index as its id; the lookup gradients are reduced per
             received row (emb_update.hip mode 1)
     X3      all_to_all  row gradients back to owners   [W, cap, K+1] f32
-    update  owners sort the requests by local row, segment-sum over source ranks, apply lazy L2
-            once and the row optimizer (or, ``embedding_update=exact``, the dense full-table
+    update  owners sum each requested row's gradients over source ranks in rank order (direct-
+            addressed position maps, merge.hip — no sort), apply lazy L2 once and the row optimizer (or, ``embedding_update=exact``, the dense full-table
             update of the shard — the reference's full L2, with no dense traffic at all)
     X4      all_reduce  MLP gradients (one flat bucket), then the dense optimizer
 
@@ -435,13 +435,9 @@ class FusedRowShard:
         self.rows_in = torch.zeros(M, Kp, **f32)
         self.grad_stage = torch.zeros(M, Kp, **f32)
         self.grad_back = torch.zeros(M, Kp, **f32)
-        self.olk = torch.zeros(M, **i32)
-        self.osk = torch.zeros(M, **i32)
-        self.osv = torch.zeros(M, **i32)
-        self.owner_bits = max(1, math.ceil(math.log2(Vs + 1)))
-        self.osort_temp = torch.zeros(max(H.sort_pairs_temp_bytes(M, self.owner_bits), 16), dtype=torch.uint8,
-                                      device=dev)
-        self.osort_stream = torch.cuda.Stream(device=dev)
+        # owner merge maps (merge.hip): position of each local row in every source's request list
+        self.pos = torch.empty(W * Vs, **i32)
+        self.rep = torch.empty(Vs, **i32)
         # prediction routing (own buffers: never races the pipelined training route)
         self.pred_rsv = torch.zeros(n, **i32)
         self.pred_send = torch.full((M,), PAD, **i32)
@@ -451,6 +447,7 @@ class FusedRowShard:
         self._graphs: Dict = {}
         self._warm = 0
         self._build()
+        H.merge_init(self.owner_params[0], e.stream_ptr)
 
     # ---- kernel parameter blocks ------------------------------------------------------------------
     def _route_params(self, ids, rsv, send, local, skl, counts, n):
@@ -470,7 +467,7 @@ class FusedRowShard:
                                          self.counts[q], self.n) for q in range(2)]
         sv = H.ShardServeParams()
         sv.ids, sv.m, sv.W, sv.rank, sv.Vs = self.recv_ids.data_ptr(), self.M, self.W, self.rank, self.Vs
-        sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), self.olk.data_ptr()
+        sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
         sv.bad = self.bad.data_ptr()
         self.serve = sv
         pv = H.ShardServeParams()
@@ -485,14 +482,17 @@ class FusedRowShard:
             lp = e.emb_params[p]  # local: Σ lookup grads per received row → grad_stage
             lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
-            op = H.EmbUpdateParams()  # owner: Σ over source ranks per local row → optimizer
-            op.skeys, op.svals, op.n = self.osk.data_ptr(), self.osv.data_ptr(), self.M
-            op.contrib, op.K1, op.Kp = self.grad_back.data_ptr(), e.K1, e.Kp
+            op = H.MergeParams()  # owner: Σ over source ranks per local row → optimizer
+            op.keys, op.key_stride = self.recv_ids.data_ptr(), self.cap
+            op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
+            op.counts = 0
+            op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
+            op.key_div, op.Vmap = self.W, Vs
+            op.pos, op.rep = self.pos.data_ptr(), self.rep.data_ptr()
             op.emb = e.emb.data_ptr()
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
             op.opt, op.step = e._opt(p), e.steps[p:].data_ptr()
-            op.max_key = self.Vs
             if self.embedding_update == "exact":
                 op.mode, op.dense_grad = 1, e.dense_grad.data_ptr()
                 e.emb_dense_params[p].grad_scale = 1.0
@@ -558,21 +558,16 @@ class FusedRowShard:
         e, H = self.eng, self.H
         main = torch.cuda.current_stream(self.device)
         side = self._fork_next(p)
-        os_ = self.osort_stream
-        os_.wait_stream(main)
-        with torch.cuda.stream(os_):
-            H.sort_pairs_iota(self.osort_temp.data_ptr(), self.osort_temp.numel(), self.olk.data_ptr(),
-                              self.osk.data_ptr(), self.osv.data_ptr(), self.M, self.owner_bits, os_.cuda_stream)
         aux = e._enqueue_rows_then_fork_wgrad(p)
         H.emb_rows_update(e.emb_params[p], main.cuda_stream)
         e._join(aux)
-        e._join(os_)
         e._join(side)
 
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
         s = e.stream_ptr
-        H.emb_rows_update(self.owner_params[p], s)
+        H.merge_scatter(self.owner_params[p], s)
+        H.merge_apply(self.owner_params[p], s)
         if self.embedding_update == "exact":
             H.emb_dense_update(e.emb_dense_params[p], s)
         H.dense_apply(e.dense_apply_params[p], s)
