@@ -113,11 +113,12 @@ def main():
     pool_vals = torch.stack([x[1] for x in pool])
     pool_labels = torch.stack([x[2] for x in pool])
 
+    explicit_dp = a.parallelism in ("dp", "dense_dp")
     parallelism = a.parallelism
     if parallelism == "auto":
         parallelism = "dp" if a.embedding_update == "sparse" else "dense_dp"
     cap = None
-    if a.engine == "fused" and (world > 1 or parallelism == "rowshard") and parallelism != "dense_dp":
+    if a.engine == "fused" and (world > 1 or a.parallelism in ("dp", "rowshard")) and parallelism != "dense_dp":
         if a.capacity == "auto":
             from rocfm.parallel.dp import pool_exchange_capacity
 
@@ -130,7 +131,7 @@ def main():
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
                                 use_graph=not a.no_graph, capacity=cap)
-        elif world > 1:
+        elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
@@ -209,7 +210,7 @@ def main():
                      f"mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
             "global_batch": B * world,
             "seq_len": a.field_size,
-            "parallelism": f"{parallelism}{world}" if (world > 1 or parallelism == "rowshard") else "dp1",
+            "parallelism": f"{parallelism}{world}" if (world > 1 or a.parallelism != "auto") else "dp1",
             "engine": a.engine,
             "embedding_update": a.embedding_update,
             "exchange_capacity": cap,
@@ -221,6 +222,8 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    if hasattr(eng, "close"):
+        eng.close()  # graphs holding RCCL collectives must go before the process group
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -38,6 +38,7 @@ struct MergeParams {
   const int64_t* step;
   int mode;           // 0: lazy L2 + optimizer on the rows; 1: dense_grad[row] = Σ · grad_scale
   float* dense_grad;  // mode 1
+  int32_t* overflow;  // nullable: sticky flag, set when a source's count exceeds cap
 };
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);

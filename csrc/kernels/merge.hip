@@ -25,6 +25,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParam
   const int i = blockIdx.x * kMergeThreads + threadIdx.x;
   if (i >= p.W * p.cap) return;
   const int r = i / p.cap, j = i - r * p.cap;
+  if (j == 0 && p.overflow && p.counts && p.counts[(size_t)r * p.count_stride] > p.cap) *p.overflow = 1;
   const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
   if (!entry_valid(p, r, j, key)) return;
   const uint32_t row = key / p.key_div;

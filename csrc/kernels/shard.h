@@ -30,6 +30,7 @@ struct ShardRouteParams {
   uint32_t* skeys_local;  // [n] sorted order: the same rows (input of the local gradient reduction)
   int32_t* counts;        // [W] unique ids per owner this batch (> cap means overflow)
   int32_t* overflow;      // sticky flag: set to 1 when any owner needs more than cap rows
+  int32_t* scratch;       // [route_scratch_ints(n)] per-tile run-head counts
 };
 
 // Owner side: serve the requested rows and emit the local row keys of the requests.
@@ -47,6 +48,7 @@ struct ShardServeParams {
 
 void launch_shard_keys(const ShardKeysParams& p, hipStream_t stream);
 void launch_shard_route(const ShardRouteParams& p, hipStream_t stream);
+int route_scratch_ints(int n);
 void launch_shard_serve(const ShardServeParams& p, hipStream_t stream);
 
 }  // namespace rocfm

@@ -10,14 +10,17 @@
 //   shard_serve  owner: requested ids → table rows (forward) and local row keys (update)
 #include "shard.h"
 
+#include <algorithm>
+
 namespace rocfm {
 namespace {
 
-constexpr int kRouteThreads = 1024;
-constexpr int kRouteWaves = kRouteThreads / kWave;
+constexpr int kRT = 256;                 // route threads per workgroup
+constexpr int kRI = 4;                   // sorted entries per thread
+constexpr int kRTile = kRT * kRI;        // entries per workgroup
+constexpr int kRWaves = kRT / kWave;
 constexpr int kMaxOwners = 1024;
 constexpr uint32_t kPad = 0xFFFFFFFFu;
-constexpr int kUnroll = 8;
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int lane = threadIdx.x & 63;
@@ -29,23 +32,22 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-// Exclusive scan over the 1024 threads of the workgroup; `total` receives the sum.
+// Exclusive scan over the kRT threads of the workgroup; `total` receives the sum.
 __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int& total) {
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int inc = wave_incl_scan(v);
   if (lane == 63) s_w[wave] = inc;
   __syncthreads();
-  if (t < 64) {
-    const int x = t < kRouteWaves ? s_w[t] : 0;
-    const int xi = wave_incl_scan(x);
-    if (t < kRouteWaves) s_w[kRouteWaves + t] = xi - x;
-    if (t == kRouteWaves - 1) s_w[2 * kRouteWaves] = xi;
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kRWaves; ++w) {
+    const int x = s_w[w];
+    before += w < wave ? x : 0;
+    tot += x;
   }
   __syncthreads();
-  total = s_w[2 * kRouteWaves];
-  const int r = s_w[kRouteWaves + wave] + inc - v;
-  __syncthreads();
-  return r;
+  total = tot;
+  return before + inc - v;
 }
 
 __global__ __launch_bounds__(256) void shard_keys_kernel(ShardKeysParams p) {
@@ -55,91 +57,101 @@ __global__ __launch_bounds__(256) void shard_keys_kernel(ShardKeysParams p) {
   p.keys[i] = (id % (uint32_t)p.W) * p.Vs + id / (uint32_t)p.W;
 }
 
-// One workgroup: each thread owns a contiguous chunk of the sorted keys.  Pass 1 counts run heads
-// (unique ids) and, per owner, the unique ids it holds; two block scans give every chunk its first
-// unique rank and every owner its first unique rank; pass 2 assigns j = rank − first[owner].
-__global__ __launch_bounds__(kRouteThreads) void shard_route_kernel(ShardRouteParams p) {
-  __shared__ int s_cnt[kMaxOwners];
-  __shared__ int s_first[kMaxOwners];
-  __shared__ int s_w[2 * kRouteWaves + 1];
-  const int t = threadIdx.x;
-  const int W = p.W;
-  for (int o = t; o < W; o += kRouteThreads) s_cnt[o] = 0;
-  __syncthreads();
-  const int per = (p.n + kRouteThreads - 1) / kRouteThreads;
-  const int b = min(t * per, p.n), e = min(b + per, p.n);
+// Multi-workgroup routing of the sorted (key', lookup) pairs (tile = 1024 entries per workgroup).
+//   count  : per tile, the run heads (unique ids) it contains; per owner, its unique ids (atomics,
+//            one per owner change per thread)
+//   assign : every tile derives its first unique rank (Σ earlier tiles) and every owner's first
+//            unique rank (scan of the owner counts), then j = rank − first[owner] per entry;
+//            heads publish their global id to the owner's request list; pads the lists.
+__device__ __forceinline__ void load_tile(const ShardRouteParams& p, int i0, uint32_t (&k)[kRI], uint32_t& prev) {
+#pragma unroll
+  for (int u = 0; u < kRI; ++u) k[u] = (i0 + u < p.n) ? p.skeys[i0 + u] : kPad;
+  prev = (i0 > 0 && i0 <= p.n) ? p.skeys[i0 - 1] : kPad;
+}
 
-  // pass 1: heads in this chunk + per-owner unique counts (one LDS atomic per owner change)
+__global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams p) {
+  __shared__ int s_w[kRWaves];
+  const int i0 = blockIdx.x * kRTile + threadIdx.x * kRI;
+  uint32_t k[kRI], prev;
+  load_tile(p, i0, k, prev);
+  int heads = 0, cur_o = -1, cur_c = 0;
+#pragma unroll
+  for (int u = 0; u < kRI; ++u) {
+    if (i0 + u < p.n && k[u] != prev) {
+      ++heads;
+      const int o = (int)(k[u] / p.Vs);
+      if (o != cur_o) {
+        if (cur_c) atomicAdd(&p.counts[cur_o], cur_c);
+        cur_o = o;
+        cur_c = 0;
+      }
+      ++cur_c;
+    }
+    if (i0 + u < p.n) prev = k[u];
+  }
+  if (cur_c) atomicAdd(&p.counts[cur_o], cur_c);
+  int total;
+  block_excl_scan(heads, s_w, total);
+  if (threadIdx.x == 0) p.scratch[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kRT) void shard_route_assign_kernel(ShardRouteParams p) {
+  __shared__ int s_w[kRWaves];
+  __shared__ int s_first[kMaxOwners];
+  __shared__ int s_cnt[kMaxOwners];
+  const int t = threadIdx.x, W = p.W;
+  // first unique rank of this tile: Σ heads of the tiles before it
+  int acc = 0;
+  for (int g = t; g < (int)blockIdx.x; g += kRT) acc += p.scratch[g];
+  int tile_base;
+  block_excl_scan(acc, s_w, tile_base);
+  // first unique rank of every owner: exclusive scan of the owner counts
+  int carry = 0;
+  for (int o0 = 0; o0 < W; o0 += kRT) {
+    const int o = o0 + t;
+    const int c = o < W ? p.counts[o] : 0;
+    int tot;
+    const int f = block_excl_scan(c, s_w, tot);
+    if (o < W) {
+      s_first[o] = carry + f;
+      s_cnt[o] = c;
+      if (blockIdx.x == 0 && c > p.cap) *p.overflow = 1;
+    }
+    carry += tot;
+  }
+  const int i0 = blockIdx.x * kRTile + t * kRI;
+  uint32_t k[kRI], v[kRI], prev;
+  load_tile(p, i0, k, prev);
+#pragma unroll
+  for (int u = 0; u < kRI; ++u) v[u] = (i0 + u < p.n) ? p.svals[i0 + u] : 0u;
   int heads = 0;
   {
-    uint32_t prev = b > 0 ? p.skeys[b - 1] : kPad;
-    int cur_o = -1, cur_c = 0;
-    for (int i0 = b; i0 < e; i0 += kUnroll) {
-      uint32_t k[kUnroll];
+    uint32_t pv = prev;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) k[u] = (i0 + u < e) ? p.skeys[i0 + u] : kPad;
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (i0 + u < e && k[u] != prev) {
-          ++heads;
-          const int o = (int)(k[u] / p.Vs);
-          if (o != cur_o) {
-            if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
-            cur_o = o;
-            cur_c = 0;
-          }
-          ++cur_c;
-        }
-        prev = (i0 + u < e) ? k[u] : prev;
-      }
-    }
-    if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
-  }
-  int total;
-  const int base = block_excl_scan(heads, s_w, total);
-  for (int o0 = 0; o0 < W; o0 += kRouteThreads) {  // W <= kMaxOwners == kRouteThreads: one round
-    const int o = o0 + t;
-    const int c = o < W ? s_cnt[o] : 0;
-    int tot2;
-    const int f = block_excl_scan(c, s_w, tot2);
-    if (o < W) {
-      s_first[o] = f;
-      p.counts[o] = c;
-      if (c > p.cap) *p.overflow = 1;
+    for (int u = 0; u < kRI; ++u) {
+      if (i0 + u < p.n && k[u] != pv) ++heads;
+      if (i0 + u < p.n) pv = k[u];
     }
   }
-  __syncthreads();
-
-  // pass 2: row index of every lookup; run heads publish their id to the owner's request list
-  {
-    int urun = base - 1;
-    uint32_t prev = b > 0 ? p.skeys[b - 1] : kPad;
-    for (int i0 = b; i0 < e; i0 += kUnroll) {
-      uint32_t k[kUnroll], v[kUnroll];
+  int tot;
+  const int before = block_excl_scan(heads, s_w, tot);  // also orders s_first/s_cnt writes
+  int urun = tile_base + before - 1;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const bool in = i0 + u < e;
-        k[u] = in ? p.skeys[i0 + u] : kPad;
-        v[u] = in ? p.svals[i0 + u] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (i0 + u >= e) continue;
-        const bool head = k[u] != prev;
-        prev = k[u];
-        urun += head ? 1 : 0;
-        const int o = (int)(k[u] / p.Vs);
-        const int j = urun - s_first[o];
-        const uint32_t lk = (uint32_t)o * (uint32_t)p.cap + (uint32_t)min(j, p.cap - 1);
-        p.skeys_local[i0 + u] = lk;
-        p.local_idx[v[u]] = (int32_t)lk;
-        if (head && j < p.cap) p.send_ids[(size_t)o * p.cap + j] = (k[u] - (uint32_t)o * p.Vs) * (uint32_t)W + o;
-      }
-    }
+  for (int u = 0; u < kRI; ++u) {
+    if (i0 + u >= p.n) continue;
+    const bool head = k[u] != prev;
+    prev = k[u];
+    urun += head ? 1 : 0;
+    const int o = (int)(k[u] / p.Vs);
+    const int j = urun - s_first[o];
+    const uint32_t lk = (uint32_t)o * (uint32_t)p.cap + (uint32_t)min(j, p.cap - 1);
+    p.skeys_local[i0 + u] = lk;
+    p.local_idx[v[u]] = (int32_t)lk;
+    if (head && j < p.cap) p.send_ids[(size_t)o * p.cap + j] = (k[u] - (uint32_t)o * p.Vs) * (uint32_t)W + o;
   }
-  // pass 3: pad every owner's request list past its count
+  // pad every owner's request list past its count (grid-strided over all slots)
   const int tot_slots = W * p.cap;
-  for (int s = t; s < tot_slots; s += kRouteThreads) {
+  for (int s = blockIdx.x * kRT + t; s < tot_slots; s += gridDim.x * kRT) {
     const int o = s / p.cap, j = s - o * p.cap;
     if (j >= s_cnt[o]) p.send_ids[s] = kPad;
   }
@@ -176,9 +188,15 @@ void launch_shard_route(const ShardRouteParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxOwners, "shard_route: 1 <= world <= 1024");
   ROCFM_REQUIRE(p.cap >= 1, "shard_route: capacity must be positive");
   ROCFM_REQUIRE((unsigned long long)p.W * p.cap < (1ull << 31), "shard_route: W*cap overflows int32");
-  hipLaunchKernelGGL(shard_route_kernel, dim3(1), dim3(kRouteThreads), 0, stream, p);
+  ROCFM_REQUIRE(p.scratch != nullptr, "shard_route: scratch (>= route_scratch_ints(n)) required");
+  ROCFM_HIP_CHECK(hipMemsetAsync(p.counts, 0, sizeof(int32_t) * p.W, stream));
+  const int tiles = std::max(1, cdiv(p.n, kRTile));
+  if (p.n > 0) hipLaunchKernelGGL(shard_route_count_kernel, dim3(tiles), dim3(kRT), 0, stream, p);
+  hipLaunchKernelGGL(shard_route_assign_kernel, dim3(tiles), dim3(kRT), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
+
+int route_scratch_ints(int n) { return std::max(1, cdiv(n, kRTile)); }
 
 void launch_shard_serve(const ShardServeParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp > 0, "shard_serve: Kp must be a positive multiple of 4");

@@ -64,6 +64,7 @@ def run(cfg: Config) -> dict:
         out["infer"] = {"pred_path": path, "n": int(len(probs))}
     elif cfg.task_type == "export":
         out["export"] = est.export(cfg.servable_model_dir)
+    est.close()
     return out
 
 

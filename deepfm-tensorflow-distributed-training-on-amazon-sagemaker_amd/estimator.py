@@ -311,6 +311,14 @@ class Estimator:
         self._log({"event": "export", "path": path})
         return path
 
+    def close(self) -> None:
+        """Release engine resources (captured graphs holding collectives) and the metrics file."""
+        if hasattr(self.eng, "close"):
+            self.eng.close()
+        if self.metrics_fh:
+            self.metrics_fh.close()
+            self.metrics_fh = None
+
     # ---- logging ------------------------------------------------------------------------------------
     def _log(self, rec: dict) -> None:
         if not self.info.is_chief:

@@ -425,11 +425,22 @@ class FusedDeepFM:
         self._primed = True
 
     # ---- the step ------------------------------------------------------------------------------
-    def _fork_next(self, p: int):
+    def _fork_point(self):
+        """Event marking the current position of the main stream (fork point for side streams).
+        Forking from a recorded point lets the main stream's kernels be enqueued (and, in a
+        graph, submitted) before the side stream's, without making the side wait for them."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _fork_next(self, p: int, fork=None):
         """Side stream: fetch + sort batch i+1 (into parity 1-p buffers)."""
         main = torch.cuda.current_stream(self.device)
         side = self.sort_stream
-        side.wait_stream(main)
+        if fork is None:
+            side.wait_stream(main)
+        else:
+            side.wait_event(fork)
         with torch.cuda.stream(side):
             self.H.fetch_batch(self.fetch_params[p], side.cuda_stream)
             self._sort(1 - p, side)
@@ -461,6 +472,8 @@ class FusedDeepFM:
             self.H.emb_dense_update(self.emb_dense_params[p], s)
 
     def _enqueue_step(self, p: int) -> None:
+        # the side chain is forked first: in the captured graph it then gets its own hardware
+        # queue and starts at once (forked later it was serialised behind the embedding update)
         side = self._fork_next(p)
         aux = self._enqueue_rows_then_fork_wgrad(p)
         self._enqueue_emb_update(p)

@@ -24,6 +24,7 @@ Gradients are averaged over ranks and the learning rate is scaled by the world s
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -31,6 +32,14 @@ import torch.distributed as dist
 
 from ..models.deepfm import ModelSpec
 from ..optim import OptHParams
+
+
+def collectives_capturable() -> bool:
+    """RCCL collectives can be captured into HIP graphs (torch.distributed nccl backend); gloo's
+    host-side collectives cannot.  ROCFM_GRAPH_COLLECTIVES=0 forces per-phase graphs."""
+    if os.environ.get("ROCFM_GRAPH_COLLECTIVES", "1") == "0":
+        return False
+    return not dist.is_initialized() or dist.get_backend() == "nccl"
 
 
 def _world() -> int:
@@ -146,6 +155,7 @@ class FusedDataParallel:
                                dropout_seed=seed + 7919 * self.rank)
         e = self.eng
         self.use_graph = use_graph
+        self.graph_collectives = use_graph and collectives_capturable()
         self.check_every = int(check_every)
         self.device = e.device
         # replicas start identical: broadcast rank 0's variables (HVD:418)
@@ -183,6 +193,7 @@ class FusedDataParallel:
             # merge maps (merge.hip): position of each key in every rank's list, representative rank
             self.pos = torch.empty(self.world * e.V, dtype=torch.int32, device=e.device)
             self.rep = torch.empty(e.V, dtype=torch.int32, device=e.device)
+            self.overflow = torch.zeros(1, dtype=torch.int32, device=e.device)
             e._build_params()
             self.export_params, self.merge_params = [], []
             for p in range(2):
@@ -210,6 +221,7 @@ class FusedDataParallel:
                 mp_.l2, mp_.grad_scale = float(spec.l2_reg), 1.0 / self.world
                 mp_.opt, mp_.step = e._opt(p), e.steps[p:].data_ptr()
                 mp_.mode = 0
+                mp_.overflow = self.overflow.data_ptr()
                 self.merge_params.append(mp_)
                 e.dense_apply_params[p].apply = 1
                 e.dense_apply_params[p].grads = self.mlp_sum.data_ptr()
@@ -241,9 +253,9 @@ class FusedDataParallel:
         self._graphs = {}
 
     # ---- step phases ---------------------------------------------------------------------------
-    def _phase_a(self, p: int):
+    def _phase_a(self, p: int, join_side: bool = True):
         e = self.eng
-        side = e._fork_next(p)
+        side = e._fork_next(p)  # forked first: its own hardware queue in the graph (see FusedDeepFM)
         self.send_count.zero_() if self.mode == "dp" else None
         aux = e._enqueue_rows_then_fork_wgrad(p)
         s = e.stream_ptr
@@ -252,9 +264,15 @@ class FusedDataParallel:
         else:
             e.H.emb_rows_update(self.export_params[p], s)
         e._join(aux)
-        e._join(side)
+        if join_side:
+            e._join(side)
+        return side
 
     def _exchange(self):
+        if self.world == 1:  # single rank (profiling the DP step on one GPU): nothing to exchange
+            if self.mode == "dp":
+                self.recv.copy_(self.send)
+            return
         if self.mode == "dense_dp":
             _all_reduce(self.bucket)
         else:
@@ -273,7 +291,7 @@ class FusedDataParallel:
         e.H.merge_scatter(self.merge_params[p], s)
         e.H.merge_apply(self.merge_params[p], s)
 
-    def _run(self, key, fn):
+    def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:
             fn()
             return
@@ -281,42 +299,83 @@ class FusedDataParallel:
         if g is None:
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(g):
+            # graphs that contain RCCL collectives: other threads (the PG watchdog) may query
+            # events while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local" if collectives else "global"):
                 fn()
             self._graphs[key] = g
         g.replay()
+
+    def _step_body(self, p: int) -> None:
+        side = self._phase_a(p, join_side=False)  # next batch's fetch+sort overlaps the exchange
+        self._exchange()
+        self._phase_b(p)
+        self.eng._join(side)
+
+    def _after_steps(self, i0: int, i1: int) -> None:
+        if self.check_every and i1 // self.check_every != i0 // self.check_every:
+            self.check()
 
     def train_step(self) -> None:
         e = self.eng
         if not e._primed:
             e.prime()
         p = e._i % 2
-        self._run(("a", p), lambda: self._phase_a(p))
-        self._exchange()
-        self._run(("b", p), lambda: self._phase_b(p))
+        if self.graph_collectives:  # the whole step, collective included, is one graph
+            self._run(("step", p), lambda: self._step_body(p), collectives=True)
+        else:
+            self._run(("a", p), lambda: self._phase_a(p))
+            self._exchange()
+            self._run(("b", p), lambda: self._phase_b(p))
         self._warm += 1
         e._i += 1
-        if self.check_every and e._i % self.check_every == 0:
-            self.check()
+        self._after_steps(e._i - 1, e._i)
 
-    def train_steps(self, n: int, steps_per_graph: int = 0) -> None:
-        for _ in range(n):
-            self.train_step()
+    def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
+        """``n`` steps from the attached pool; with capturable collectives (RCCL), full step pairs
+        are replayed from one multi-step graph (``steps_per_graph`` steps per launch)."""
+        e = self.eng
+        S = max(2, steps_per_graph // 2 * 2)
+        while n > 0:
+            if (self.graph_collectives and self.use_graph and self._warm >= 4 and e._primed and n >= S
+                    and e._i % 2 == 0 and not e._ring):
+                key = ("multi", S)
+                g = self._graphs.get(key)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize(self.device)
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        for k in range(S):
+                            self._step_body(k % 2)
+                    self._graphs[key] = g
+                g.replay()
+                e._i += S
+                self._warm += S
+                n -= S
+                self._after_steps(e._i - S, e._i)
+            else:
+                self.train_step()
+                n -= 1
+
+    def close(self) -> None:
+        """Release the captured graphs (required before destroy_process_group when they hold
+        RCCL collectives)."""
+        torch.cuda.synchronize(self.device)
+        self._graphs = {}
 
     def check(self) -> None:
         """Raise if a rank exported more unique rows than the exchange capacity (rows past the
         capacity would have been dropped from that step's update)."""
         if self.overflowed():
-            c = int(self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, 0].max())
-            raise RuntimeError(f"DP exchange overflow: a rank exported {c} unique rows > capacity {self.cap}; "
-                               f"rebuild with capacity >= {c} (default capacity = batch_size*field_size never overflows)")
+            raise RuntimeError(f"DP exchange overflow: a rank exported more unique rows than capacity {self.cap}; "
+                               "rebuild with a larger capacity (default batch_size*field_size never overflows)")
 
     def overflowed(self) -> bool:
-        """True if any rank produced more unique rows than the exchange capacity (never with the default cap)."""
+        """True if, in any step so far, a rank produced more unique rows than the exchange capacity
+        (sticky device flag set by merge_scatter; never with the default capacity)."""
         if self.mode != "dp":
             return False
-        c = self.recv2d[:, self.off_cnt:self.off_cnt + 4].contiguous().view(torch.int32)[:, 0]
-        return bool((c > self.cap).any())
+        return bool(int(self.overflow.item()))
 
     # ---- delegation ----------------------------------------------------------------------------
     def __getattr__(self, name):

@@ -402,6 +402,9 @@ class FusedRowShard:
         del P
         self.H, self.device, self.embedding_update = e.H, e.device, embedding_update
         self.use_graph, self.check_every = use_graph, int(check_every)
+        from .dp import collectives_capturable
+
+        self.graph_collectives = use_graph and collectives_capturable()
         if W > 1:
             from .dist import broadcast_tensors
 
@@ -426,6 +429,7 @@ class FusedRowShard:
         self.counts = [torch.zeros(W, **i32) for _ in range(2)]
         self.overflow = torch.zeros(1, **i32)
         self.bad = torch.zeros(1, **i32)
+        self.route_scratch = torch.zeros(H.route_scratch_ints(n), **i32)
         self.route_temp = torch.zeros(max(H.sort_pairs_temp_bytes(n, self.route_bits), 16), dtype=torch.uint8,
                                       device=dev)
         # ---- exchange buffers ----
@@ -459,6 +463,7 @@ class FusedRowShard:
         rp.W, rp.Vs, rp.cap = self.W, self.Vs, self.cap
         rp.send_ids, rp.local_idx, rp.skeys_local = send.data_ptr(), local.data_ptr(), skl.data_ptr()
         rp.counts, rp.overflow = counts.data_ptr(), self.overflow.data_ptr()
+        rp.scratch = self.route_scratch.data_ptr()
         return kp, rp
 
     def _build(self):
@@ -487,7 +492,7 @@ class FusedRowShard:
             op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
-            op.key_div, op.Vmap = self.W, Vs
+            op.key_div, op.Vmap = self.W, self.Vs
             op.pos, op.rep = self.pos.data_ptr(), self.rep.data_ptr()
             op.emb = e.emb.data_ptr()
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
@@ -541,11 +546,14 @@ class FusedRowShard:
         self._route_launch(self.route[e._i % 2], self.n, torch.cuda.current_stream(self.device))
         e._primed = True
 
-    def _fork_next(self, p: int):
+    def _fork_next(self, p: int, fork=None):
         e = self.eng
         main = torch.cuda.current_stream(self.device)
         side = e.sort_stream
-        side.wait_stream(main)
+        if fork is None:
+            side.wait_stream(main)
+        else:
+            side.wait_event(fork)
         with torch.cuda.stream(side):
             e.H.fetch_batch(e.fetch_params[p], side.cuda_stream)
             self._route_launch(self.route[1 - p], self.n, side)
@@ -554,14 +562,15 @@ class FusedRowShard:
     def _phase_serve(self, p: int) -> None:
         self.H.shard_serve(self.serve, self.eng.stream_ptr)
 
-    def _phase_compute(self, p: int) -> None:
+    def _phase_compute(self, p: int, with_side: bool = True) -> None:
         e, H = self.eng, self.H
         main = torch.cuda.current_stream(self.device)
-        side = self._fork_next(p)
+        side = self._fork_next(p) if with_side else None  # forked first: own hardware queue in the graph
         aux = e._enqueue_rows_then_fork_wgrad(p)
         H.emb_rows_update(e.emb_params[p], main.cuda_stream)
         e._join(aux)
-        e._join(side)
+        if side is not None:
+            e._join(side)
 
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
@@ -572,7 +581,7 @@ class FusedRowShard:
             H.emb_dense_update(e.emb_dense_params[p], s)
         H.dense_apply(e.dense_apply_params[p], s)
 
-    def _run(self, key, fn):
+    def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:
             fn()
             return
@@ -580,7 +589,7 @@ class FusedRowShard:
         if g is None:
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local" if collectives else "global"):
                 fn()
             self._graphs[key] = g
         g.replay()
@@ -591,27 +600,72 @@ class FusedRowShard:
         else:
             out.copy_(inp)
 
+    def _step_body(self, p: int) -> None:
+        e = self.eng
+        side = self._fork_next(p)  # next batch's fetch + route overlaps the whole step
+        self._exchange(self.recv_ids, self.send_ids[p])                        # X1 requests
+        self._phase_serve(p)
+        self._exchange(self.rows_in, self.rows_out)                             # X2 rows
+        self._phase_compute(p, with_side=False)
+        self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
+        if self.W > 1:
+            all_reduce_(e.dense_grads_flat)                                     # X4 MLP grads
+        self._phase_update(p)
+        e._join(side)
+
     def train_step(self) -> None:
         e = self.eng
         if not e._primed:
             self.prime()
         p = e._i % 2
-        self._exchange(self.recv_ids, self.send_ids[p])                       # X1 requests
-        self._run(("serve", p), lambda: self._phase_serve(p))
-        self._exchange(self.rows_in, self.rows_out)                            # X2 rows
-        self._run(("compute", p), lambda: self._phase_compute(p))
-        self._exchange(self.grad_back, self.grad_stage)                        # X3 row grads
-        if self.W > 1:
-            all_reduce_(e.dense_grads_flat)                                    # X4 MLP grads
-        self._run(("update", p), lambda: self._phase_update(p))
+        if self.graph_collectives:  # one graph per step, collectives included
+            self._run(("step", p), lambda: self._step_body(p), collectives=True)
+        else:
+            self._exchange(self.recv_ids, self.send_ids[p])
+            self._run(("serve", p), lambda: self._phase_serve(p))
+            self._exchange(self.rows_in, self.rows_out)
+            self._run(("compute", p), lambda: self._phase_compute(p))
+            self._exchange(self.grad_back, self.grad_stage)
+            if self.W > 1:
+                all_reduce_(e.dense_grads_flat)
+            self._run(("update", p), lambda: self._phase_update(p))
         self._warm += 1
         e._i += 1
-        if self.check_every and e._i % self.check_every == 0:
+        self._after_steps(e._i - 1, e._i)
+
+    def _after_steps(self, i0: int, i1: int) -> None:
+        if self.check_every and i1 // self.check_every != i0 // self.check_every:
             self.check()
 
-    def train_steps(self, n: int, steps_per_graph: int = 0) -> None:
-        for _ in range(n):
-            self.train_step()
+    def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
+        e = self.eng
+        S = max(2, steps_per_graph // 2 * 2)
+        while n > 0:
+            if (self.graph_collectives and self.use_graph and self._warm >= 4 and e._primed and n >= S
+                    and e._i % 2 == 0 and not e._ring):
+                key = ("multi", S)
+                g = self._graphs.get(key)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize(self.device)
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        for k in range(S):
+                            self._step_body(k % 2)
+                    self._graphs[key] = g
+                g.replay()
+                e._i += S
+                self._warm += S
+                n -= S
+                self._after_steps(e._i - S, e._i)
+            else:
+                self.train_step()
+                n -= 1
+
+    def close(self) -> None:
+        """Release the captured graphs (required before destroy_process_group when they hold
+        RCCL collectives)."""
+        torch.cuda.synchronize(self.device)
+        self._graphs = {}
 
     def train_on(self, batches):
         it = iter(batches)

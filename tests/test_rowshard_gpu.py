@@ -45,6 +45,8 @@ def _route(ids, W, V, cap):
     rp.skeys, rp.svals, rp.n, rp.W, rp.Vs, rp.cap = sk.data_ptr(), sv.data_ptr(), n, W, Vs, cap
     rp.send_ids, rp.local_idx, rp.skeys_local = send.data_ptr(), local.data_ptr(), skl.data_ptr()
     rp.counts, rp.overflow = counts.data_ptr(), ov.data_ptr()
+    scratch = torch.zeros(H.route_scratch_ints(n), **i32)
+    rp.scratch = scratch.data_ptr()
     H.shard_route(rp, s)
     torch.cuda.synchronize()
     return send.cpu().numpy(), local.cpu().numpy(), counts.cpu().numpy(), int(ov.item()), skl, sv, local
