@@ -1,6 +1,7 @@
 // pybind11 bindings for the host runtime (module rocfm._rocfm_io).  Host-only: builds and runs on
 // CPU-only machines (tests) and feeds pinned buffers on the GPU box.
 #include <pybind11/numpy.h>
+#include <cstring>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -134,6 +135,26 @@ PYBIND11_MODULE(_rocfm_io, m) {
         return py::make_tuple(recs.size(), bad, lens);
       },
       py::arg("path"), py::arg("verify_crc") = true, py::arg("skip_bad") = false);
+
+  m.def(
+      "count_records",
+      [](const std::string& path) {
+        // framing walk only (u64 length, u32 crc, payload, u32 crc): no payload read, no CRC check
+        FILE* f = fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("cannot open " + path);
+        int64_t n = 0;
+        uint8_t hdr[12];
+        py::gil_scoped_release nogil;
+        while (fread(hdr, 1, 12, f) == 12) {
+          uint64_t len;
+          std::memcpy(&len, hdr, 8);
+          if (fseeko(f, (off_t)len + 4, SEEK_CUR) != 0) break;
+          ++n;
+        }
+        fclose(f);
+        return n;
+      },
+      py::arg("path"));
 
   m.def(
       "convert_libsvm",

@@ -116,6 +116,7 @@ class Config:
     on_bad_record: str = "fail"  # fail | skip
     max_steps: int = 0  # 0 → run num_epochs
     dist_timeout_s: int = 600
+    exchange_capacity: int = 0  # rows per rank (dp) / per owner (rowshard) in the exchange buffers; 0 = B*F (safe)
 
     # ------------------------------------------------------------------------------------
     @property
@@ -151,6 +152,8 @@ class Config:
             raise ValueError(f"unknown task_type {self.task_type!r}")
         if self.embedding_update not in ("sparse", "exact"):
             raise ValueError(f"unknown embedding_update {self.embedding_update!r}")
+        if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard"):
+            raise ValueError(f"unknown parallelism {self.parallelism!r}")
         if self.engine not in ("auto", "fused", "torch"):
             raise ValueError(f"unknown engine {self.engine!r}")
         return self

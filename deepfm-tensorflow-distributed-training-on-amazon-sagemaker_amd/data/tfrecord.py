@@ -199,6 +199,23 @@ class TFRecordDataset:
         finally:
             self.loader.stop()
 
+    def num_batches(self) -> Optional[int]:
+        """Batches this shard will yield over all epochs (file mode; None for a stream/FIFO source).
+
+        Counts records by walking the framing only (C++ ``count_records``), then applies the
+        record-index sharding and the per-epoch drop_remainder of the loader.  Upper bound when
+        ``skip_bad`` drops corrupt records."""
+        if self.kw["stream_mode"]:
+            return None
+        io = _io_mod()
+        if io is None:
+            raise RuntimeError("rocfm native IO module missing; run `python build.py`")
+        N = sum(int(io.count_records(f)) for f in self.files)
+        c, i = self.kw["shard_count"], self.kw["shard_index"]
+        n = (N - i + c - 1) // c if N > i else 0
+        per_epoch = n // self.B if self.kw["drop_remainder"] else (n + self.B - 1) // self.B
+        return per_epoch * self.kw["num_epochs"]
+
     @property
     def bad_records(self) -> int:
         return 0 if self.loader is None else int(self.loader.bad_records)

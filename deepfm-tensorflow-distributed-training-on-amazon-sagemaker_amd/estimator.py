@@ -53,7 +53,9 @@ class Estimator:
         self.world = _world()
         self.hp = OptHParams(name=cfg.optimizer, lr=cfg.learning_rate)
         self.engine_name = self._pick_engine()
-        P = params if params is not None else init_params(self.spec, cfg.seed)
+        if params is None and cfg.parallelism != "rowshard":
+            params = init_params(self.spec, cfg.seed)
+        P = params  # row-shard: None → every rank initialises only its own rows
         self.eng = self._build_engine(P)
         if self.world > 1 and cfg.lr_scaling == "linear":
             self.eng.set_lr_scale(float(self.world))  # HVD:171 learning_rate * hvd.size()
@@ -79,14 +81,24 @@ class Estimator:
 
     def _build_engine(self, P):
         cfg = self.cfg
+        cap = cfg.exchange_capacity or None
+        if cfg.parallelism == "rowshard":
+            from .parallel.emb_shard import FusedRowShard, TorchRowShard
+
+            if self.engine_name == "fused":
+                return FusedRowShard(self.spec, self.hp, cfg.batch_size, self.device, params=P,
+                                     embedding_update=cfg.embedding_update, seed=cfg.seed,
+                                     use_graph=cfg.use_hip_graph, capacity=cap)
+            return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
+                                 seed=cfg.seed)
         if self.engine_name == "fused":
-            if self.world > 1:
+            if self.world > 1 or cfg.parallelism in ("dp", "dense_dp"):
                 from .parallel.dp import FusedDataParallel
 
-                mode = "dense_dp" if cfg.embedding_update == "exact" else "dp"
+                mode = "dense_dp" if (cfg.embedding_update == "exact" or cfg.parallelism == "dense_dp") else "dp"
                 return FusedDataParallel(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                          embedding_update=cfg.embedding_update, mode=mode, seed=cfg.seed,
-                                         use_graph=cfg.use_hip_graph)
+                                         use_graph=cfg.use_hip_graph, capacity=cap)
             from .models.fused import FusedDeepFM
 
             return FusedDeepFM(self.spec, self.hp, cfg.batch_size, self.device, embedding_update=cfg.embedding_update,
@@ -143,8 +155,13 @@ class Estimator:
         cfg = self.cfg
         ds = self._dataset(files, num_epochs, training=True)
         batches = self._device_batches(ds)
+        limit = self._agreed_steps(ds)
         if max_steps:
-            batches = _take(batches, max_steps)
+            limit = max_steps if limit is None else min(limit, max_steps)
+        if limit is not None:
+            batches = _take(batches, limit)
+        elif self.world > 1:
+            batches = self._lockstep(batches)
         t0 = time.time()
         last_t, last_step = t0, self.global_step
         n0 = self.global_step
@@ -186,6 +203,36 @@ class Estimator:
         self._log({"event": "train_end", **out})
         return out
 
+    # ---- multi-rank step agreement -----------------------------------------------------------
+    def _ctrl_group(self):
+        """A gloo group for host-side control messages (never touches the GPU stream)."""
+        if getattr(self, "_ctrl", None) is None:
+            self._ctrl = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+        return self._ctrl
+
+    def _agreed_steps(self, ds) -> Optional[int]:
+        """Every rank must run the same number of synchronous steps (each step is a collective).
+        File mode: the minimum over ranks of the shard's batch count (records counted from the
+        framing); the surplus batches of longer shards are dropped, like drop_remainder."""
+        if self.world == 1:
+            return None
+        n = ds.num_batches() if self.cfg.on_bad_record != "skip" else None
+        t = torch.tensor([n if n is not None else -1], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctrl_group())
+        return int(t.item()) if int(t.item()) >= 0 else None
+
+    def _lockstep(self, batches):
+        """Stream mode (or skip_bad): agree per step, on the host control group, that every rank
+        still has a batch."""
+        it = iter(batches)
+        while True:
+            b = next(it, None)
+            t = torch.tensor([0 if b is None else 1], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctrl_group())
+            if int(t.item()) == 0:
+                return
+            yield b
+
     def _dp_train_on(self, batches):
         """FusedDataParallel: same one-batch-ahead ring protocol as FusedDeepFM.train_on."""
         it = iter(batches)
@@ -211,7 +258,25 @@ class Estimator:
     @torch.no_grad()
     def _predict_stream(self, files, training_shard: bool = False, drop_remainder: bool = True):
         ds = self._dataset(files, 1, training=training_shard, drop_remainder=drop_remainder)
-        for ids, vals, labels in self._device_batches(ds):
+        batches = self._device_batches(ds)
+        if getattr(self.eng, "collective_predict", False) and self.world > 1:
+            # row-shard inference is collective: ranks with no batch left join with empty ones
+            it = iter(batches)
+            while True:
+                b = next(it, None)
+                t = torch.tensor([0 if b is None else 1], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._ctrl_group())
+                if int(t.item()) == 0:
+                    return
+                if b is None:
+                    F = self.cfg.field_size
+                    b = (torch.zeros(0, F, dtype=torch.int32, device=self.device),
+                         torch.zeros(0, F, device=self.device), torch.zeros(0, device=self.device))
+                p, lr = self.eng.predict_batch(*b)
+                if len(p):
+                    yield p, lr, b[2]
+            return
+        for ids, vals, labels in batches:
             p, lr = self.eng.predict_batch(ids, vals, labels)
             yield p, lr, labels
 
@@ -279,11 +344,26 @@ class Estimator:
         if not self.model_dir:
             return None
         sd = self.eng.state_dict()  # every rank participates (collectives / sync), rank 0 writes
+        extra = {"config": {k: v for k, v in self.cfg.to_dict().items() if isinstance(v, (int, float, str, bool))}}
+        step = int(sd["global_step"])
+        if getattr(self.eng, "row_sharded", False) and self.world > 1:
+            # one shard per rank (its rows + their global ids); rank 0 writes the manifest last
+            rs = self.eng.row_sets()
+            if not self.info.is_chief:
+                ckpt.save_checkpoint(self.model_dir, sd, step, shard=(self.info.rank, self.world), row_sets=rs,
+                                     write_index=False)
+            dist.barrier(group=self._ctrl_group())
+            path = None
+            if self.info.is_chief:
+                path = ckpt.save_checkpoint(self.model_dir, sd, step, self.cfg.keep_checkpoint_max,
+                                            shard=(0, self.world), row_sets=rs, extra=extra,
+                                            global_rows={k: self.cfg.feature_size for k in rs})
+                self._log({"event": "checkpoint", "path": path})
+            dist.barrier(group=self._ctrl_group())
+            return path
         if not self.info.is_chief:
             return None
-        extra = {"config": {k: v for k, v in self.cfg.to_dict().items() if isinstance(v, (int, float, str, bool))}}
-        path = ckpt.save_checkpoint(self.model_dir, sd, int(sd["global_step"]), self.cfg.keep_checkpoint_max,
-                                    extra=extra)
+        path = ckpt.save_checkpoint(self.model_dir, sd, step, self.cfg.keep_checkpoint_max, extra=extra)
         self._log({"event": "checkpoint", "path": path})
         return path
 
@@ -291,7 +371,8 @@ class Estimator:
         prefix = prefix or ckpt.latest_checkpoint(self.model_dir)
         if not prefix:
             return None
-        sd = ckpt.load_checkpoint(prefix)
+        rows_for = self.eng.row_sets() if getattr(self.eng, "row_sharded", False) else None
+        sd = ckpt.load_checkpoint(prefix, rows_for=rows_for)
         self.eng.load_state_dict(sd, strict=False)
         self._log({"event": "restore", "path": prefix, "global_step": self.global_step})
         return prefix

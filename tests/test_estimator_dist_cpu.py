@@ -1,0 +1,92 @@
+"""Multi-rank Estimator on CPU (gloo, 2 ranks): unequal data shards still run in lockstep (agreed
+step count), eval/predict are collective for the row-sharded table, sharded checkpoints are written
+by every rank and restore on one process (reshard 2 → 1)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _argv(data_dir, model_dir, par):
+    return ["--feature_size", "2000", "--field_size", "39", "--embedding_size", "8", "--deep_layers", "32,16",
+            "--dropout", "1.0,1.0", "--batch_size", "128", "--learning_rate", "0.005", "--l2_reg", "0.00001",
+            "--training_data_dir", data_dir, "--val_data_dir", data_dir, "--model_dir", model_dir,
+            "--log_steps", "5", "--engine", "torch", "--num_threads", "2", "--save_checkpoints_secs", "0",
+            "--parallelism", par]
+
+
+def _worker(rank, world, port, data_dir, model_dir, par, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rocfm.config import parse_flags
+    from rocfm.estimator import Estimator
+
+    est = Estimator(parse_flags(_argv(data_dir, model_dir, par)))
+    tr = est.train([os.path.join(data_dir, "tr.tfrecords")], num_epochs=1)
+    ev = est.evaluate([os.path.join(data_dir, "va.tfrecords")])
+    probs = est.predict([os.path.join(data_dir, "te.tfrecords")])
+    full = est.eng.parameters_tf()
+    if rank == 0:
+        torch.save({"tr": tr, "ev": ev, "probs": probs, "fm_v": full["fm_v"], "step": est.global_step}, out)
+    est.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("par", ["rowshard", "dp"])
+def test_estimator_two_ranks(tmp_path, par):
+    from rocfm import checkpoint as ckpt
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+
+    d = tmp_path / "data"
+    d.mkdir()
+    # 1700 records → shard sizes 850/850 → 6 batches each; 700 test records → 350 each → 2 + 2 batches
+    write_synthetic_tfrecord(str(d / "tr.tfrecords"), 1700, 2000, seed=1)
+    write_synthetic_tfrecord(str(d / "va.tfrecords"), 600, 2000, seed=2)
+    write_synthetic_tfrecord(str(d / "te.tfrecords"), 700, 2000, seed=3)
+    md = str(tmp_path / "m")
+    out = str(tmp_path / "o.pt")
+    mp.start_processes(_worker, args=(2, _port(), str(d), md, par, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    assert got["step"] == 1700 // 2 // 128
+    assert got["ev"]["examples"] == 2 * (300 // 128) * 128
+    assert len(got["probs"]) == 2 * (350 // 128) * 128
+    prefix = ckpt.latest_checkpoint(md)
+    assert prefix and ckpt.checkpoint_step(prefix) == got["step"]
+    sd = ckpt.load_checkpoint(prefix)  # both shards reassembled (row-shard) or the replicated table (dp)
+    torch.testing.assert_close(sd["fm_v"], got["fm_v"])
+    # a single-process estimator restores it
+    from rocfm.config import parse_flags
+    from rocfm.estimator import Estimator
+
+    one = Estimator(parse_flags(_argv(str(d), md, "auto")))
+    assert one.global_step == got["step"]
+    torch.testing.assert_close(one.eng.P["fm_v"], got["fm_v"])
+
+
+def test_unequal_shards_lockstep(tmp_path):
+    """Shards of different length: ranks agree on the shorter count (no hang)."""
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+
+    d = tmp_path / "data"
+    d.mkdir()
+    write_synthetic_tfrecord(str(d / "tr.tfrecords"), 1023, 2000, seed=1)  # 512 / 511 records: 4 vs 3 batches
+    write_synthetic_tfrecord(str(d / "va.tfrecords"), 300, 2000, seed=2)
+    write_synthetic_tfrecord(str(d / "te.tfrecords"), 300, 2000, seed=3)
+    out = str(tmp_path / "o.pt")
+    mp.start_processes(_worker, args=(2, _port(), str(d), str(tmp_path / "m"), "rowshard", out), nprocs=2,
+                       join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    assert got["step"] == 3
