@@ -53,7 +53,12 @@ def run(cfg: Config) -> dict:
         if va_files and cfg.eval_every_epoch:
             out["epochs"] = est.train_and_evaluate(tr_files, va_files, cfg.num_epochs)
         else:
-            out["train"] = est.train(tr_files, cfg.num_epochs, max_steps=cfg.max_steps or None)
+            ep0, skip = est.resume_point(tr_files, cfg.num_epochs)  # restarted job: fast-forward
+            max_steps = (cfg.max_steps - est.global_step) if cfg.max_steps else None
+            if max_steps is not None and max_steps <= 0:
+                out["train"] = {"global_step": est.global_step, "steps": 0}
+            else:
+                out["train"] = est.train(tr_files, cfg.num_epochs - ep0, max_steps=max_steps, skip_batches=skip)
         if cfg.servable_model_dir:
             out["export"] = est.export(cfg.servable_model_dir)
     elif cfg.task_type == "eval":

@@ -116,6 +116,7 @@ class Config:
     on_bad_record: str = "fail"  # fail | skip
     max_steps: int = 0  # 0 → run num_epochs
     dist_timeout_s: int = 600
+    watchdog_s: int = 0  # >0: dump stacks and exit(3) when no step completes for this long (§5.3)
     exchange_capacity: int = 0  # rows per rank (dp) / per owner (rowshard) in the exchange buffers; 0 = B*F (safe)
 
     # ------------------------------------------------------------------------------------

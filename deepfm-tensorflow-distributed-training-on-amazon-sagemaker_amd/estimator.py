@@ -33,6 +33,10 @@ from .models.deepfm import ModelSpec, init_params
 from .ops import has_hip
 from .optim import OptHParams
 from .parallel.dist import RankInfo, rank_info_from_env
+from .utils.fault import FaultInjector
+from .utils.numerics import check_finite, check_ids, ids_check_enabled, numerics_check_enabled
+from .utils.profiling import StepProfiler, StepTimer, trace_range
+from .utils.watchdog import Watchdog
 
 log = logging.getLogger("rocfm")
 
@@ -57,8 +61,10 @@ class Estimator:
             params = init_params(self.spec, cfg.seed)
         P = params  # row-shard: None → every rank initialises only its own rows
         self.eng = self._build_engine(P)
+        self._lr_scale = 1.0
         if self.world > 1 and cfg.lr_scaling == "linear":
-            self.eng.set_lr_scale(float(self.world))  # HVD:171 learning_rate * hvd.size()
+            self._lr_scale = float(self.world)
+            self.eng.set_lr_scale(self._lr_scale)  # HVD:171 learning_rate * hvd.size()
         self.model_dir = cfg.effective_model_dir
         self._last_save_t = time.time()
         self.metrics_fh = None
@@ -67,6 +73,8 @@ class Estimator:
             self.metrics_fh = open(cfg.metrics_file, "a")
         if restore and self.model_dir:
             self.restore()
+        # steps already trained by the job this estimator resumes (fast-forward on restart, below)
+        self._resume_step = self.global_step
 
     # ---- construction -------------------------------------------------------------------------
     def _pick_engine(self) -> str:
@@ -133,7 +141,10 @@ class Estimator:
         """Host (pinned) batches → device tensors; waits for each H2D copy before the loader may
         recycle its pinned slot (the iterator releases the previous slot on advance)."""
         prev_ev = None
+        chk = ids_check_enabled()
         for ids, vals, labels in ds:
+            if chk:
+                check_ids(ids, self.cfg.feature_size)
             if prev_ev is not None:
                 prev_ev.synchronize()
             if self.device.type == "cuda":
@@ -151,11 +162,16 @@ class Estimator:
         return self.eng.global_step()
 
     def train(self, files: Sequence[str], num_epochs: int = 1, max_steps: Optional[int] = None,
-              hooks: Sequence[Callable] = ()) -> Dict[str, float]:
+              hooks: Sequence[Callable] = (), skip_batches: int = 0) -> Dict[str, float]:
+        """Train over ``num_epochs`` passes of ``files`` (this rank's shard).  ``skip_batches``
+        fast-forwards the input stream (resume after a restart without re-training consumed data;
+        the reference re-reads from the start, an Estimator limitation rocfm does not copy)."""
         cfg = self.cfg
         ds = self._dataset(files, num_epochs, training=True)
-        batches = self._device_batches(ds)
+        batches = self._device_batches(_skip(ds, skip_batches))
         limit = self._agreed_steps(ds)
+        if limit is not None:
+            limit = max(0, limit - skip_batches)
         if max_steps:
             limit = max_steps if limit is None else min(limit, max_steps)
         if limit is not None:
@@ -166,32 +182,59 @@ class Estimator:
         last_t, last_step = t0, self.global_step
         n0 = self.global_step
         loss = float("nan")
+        timer = StepTimer()
+        prof = StepProfiler(cfg.profile_steps, os.path.join(self.model_dir or ".", "profile")) \
+            if cfg.profile_steps else None
+        faults = FaultInjector(self.info.rank)
+        wd = Watchdog(cfg.watchdog_s).start() if cfg.watchdog_s > 0 else None
+        batches = _timed(batches, timer)
 
         def after_step():
             nonlocal last_t, last_step, loss
             step = self.global_step
+            if wd is not None:
+                wd.beat()
+            if prof is not None:
+                prof.step(step)
             if cfg.log_steps and step % cfg.log_steps == 0:
                 loss = self.batch_loss()
+                if faults.corrupt_loss(step):
+                    loss = float("nan")
+                if numerics_check_enabled():
+                    check_finite(loss, step)
                 now = time.time()
                 eps = (step - last_step) * cfg.batch_size * self.world / max(now - last_t, 1e-9)
+                _, stall = timer.lap()
                 last_t, last_step = now, step
-                self._log({"event": "train", "global_step": step, "loss": loss, "examples_per_sec": eps})
+                self._log({"event": "train", "global_step": step, "loss": loss, "examples_per_sec": eps,
+                           "examples_per_sec_per_gpu": eps / self.world, "lr": self.hp.lr * self._lr_scale,
+                           "input_stall": round(stall, 4)})
             if cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0:
                 self.save()
             elif cfg.save_checkpoints_secs and time.time() - self._last_save_t > cfg.save_checkpoints_secs:
                 self.save()
             for h in hooks:
                 h(self, step)
+            if faults:
+                faults.after_step(step)
 
-        if self.engine_name == "fused":
-            for _ in self.eng.train_on(batches) if not hasattr(self.eng, "eng") else self._dp_train_on(batches):
-                after_step()
-        else:
-            for ids, vals, labels in batches:
-                self.eng.train_step(ids, vals, labels)
-                after_step()
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+        try:
+            with trace_range("train"):
+                if self.engine_name == "fused":
+                    it = self.eng.train_on(batches) if not hasattr(self.eng, "eng") else self._dp_train_on(batches)
+                    for _ in it:
+                        after_step()
+                else:
+                    for ids, vals, labels in batches:
+                        self.eng.train_step(ids, vals, labels)
+                        after_step()
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+        finally:
+            if wd is not None:
+                wd.stop()
+            if prof is not None:
+                prof.close()
         steps = self.global_step - n0
         dt = time.time() - t0
         out = {"global_step": self.global_step, "steps": steps,
@@ -326,11 +369,22 @@ class Estimator:
                     f.write("%f\n" % v)  # PS:531-533
         return probs
 
+    def resume_point(self, files: Sequence[str], num_epochs: int):
+        """(first epoch, batches to skip in it) for a job restored at ``_resume_step`` (file mode)."""
+        done = self._resume_step
+        if not done:
+            return 0, 0
+        per_epoch = self._dataset(files, 1, training=True).num_batches()
+        if not per_epoch:
+            return 0, 0
+        return min(done // per_epoch, num_epochs), done % per_epoch
+
     def train_and_evaluate(self, train_files, eval_files, num_epochs: Optional[int] = None):
         num_epochs = num_epochs or self.cfg.num_epochs
         results = []
-        for ep in range(num_epochs):
-            tr = self.train(train_files, 1)
+        ep0, skip = self.resume_point(train_files, num_epochs)
+        for ep in range(ep0, num_epochs):
+            tr = self.train(train_files, 1, skip_batches=skip if ep == ep0 else 0)
             ev = self.evaluate(eval_files) if eval_files and self.cfg.eval_every_epoch else {}
             results.append({"epoch": ep, **tr, **{f"eval_{k}": v for k, v in ev.items()}})
         return results
@@ -340,6 +394,10 @@ class Estimator:
         return self.eng.state_dict()
 
     def save(self) -> Optional[str]:
+        with trace_range("checkpoint"):
+            return self._save()
+
+    def _save(self) -> Optional[str]:
         self._last_save_t = time.time()
         if not self.model_dir:
             return None
@@ -408,6 +466,26 @@ class Estimator:
         if self.metrics_fh:
             self.metrics_fh.write(json.dumps({"time": time.time(), **rec}) + "\n")
             self.metrics_fh.flush()
+
+
+def _skip(it, n):
+    """Drop the first ``n`` items (host batches: the loader recycles their slots at once)."""
+    it = iter(it)
+    for _ in range(n):
+        if next(it, None) is None:
+            break
+    return it
+
+
+def _timed(it, timer):
+    """Yield from ``it`` while accounting the time spent waiting for each item (input stall)."""
+    it = iter(it)
+    while True:
+        with timer.waiting():
+            x = next(it, None)
+        if x is None:
+            return
+        yield x
 
 
 def _take(it, n):
