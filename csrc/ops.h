@@ -10,6 +10,7 @@
 #include "kernels/optim.h"
 #include "kernels/shard.h"
 #include "kernels/merge.h"
+#include "kernels/metrics.h"
 
 namespace rocfm {
 

@@ -28,7 +28,7 @@ from . import checkpoint as ckpt
 from .config import Config
 from .data.sharding import eval_shard, train_shard
 from .data.tfrecord import TFRecordDataset
-from .metrics import LossMean, TFStreamingAUC, exact_auc
+from .metrics import DeviceAUC, LossMean, TFStreamingAUC, exact_auc
 from .models.deepfm import ModelSpec, init_params
 from .ops import has_hip
 from .optim import OptHParams
@@ -326,15 +326,25 @@ class Estimator:
     @torch.no_grad()
     def evaluate(self, files: Sequence[str], exact: bool = True) -> Dict[str, float]:
         """AUC (TF 200-threshold + exact) and mean loss over the eval files, sharded over all ranks."""
-        auc = TFStreamingAUC()
+        on_gpu = self.device.type == "cuda" and has_hip()
+        auc = DeviceAUC(self.device) if on_gpu else TFStreamingAUC()
         lm = LossMean()
         preds, labs = [], []
-        for p, lr, labels in self._predict_stream(files):
-            auc.update(labels, p)
-            lm.update(float(lr.double().mean()), len(p))
-            if exact:
-                preds.append(p.float().cpu())
-                labs.append(labels.float().cpu())
+        with trace_range("evaluate"):
+            for p, lr, labels in self._predict_stream(files):
+                if on_gpu:  # histogram + loss sums on the device: no per-batch host sync
+                    auc.update(labels, p, lr)
+                else:
+                    auc.update(labels, p)
+                    lm.update(float(lr.double().mean()), len(p))
+                if exact:
+                    preds.append(p.float())
+                    labs.append(labels.float().to(p.device))
+        if on_gpu:
+            lm.total, lm.count = auc.loss_total()
+            auc = auc.streaming()
+        preds = [torch.cat(preds).cpu()] if preds else []
+        labs = [torch.cat(labs).cpu()] if labs else []
         l2 = self.eng.l2_value()
         state = auc.state()
         tot = np.array([lm.total, lm.count], np.float64)

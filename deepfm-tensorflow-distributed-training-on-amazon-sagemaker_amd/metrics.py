@@ -10,6 +10,8 @@
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import numpy as np
 import torch
 
@@ -23,7 +25,7 @@ def tf_thresholds(num_thresholds: int = 200) -> np.ndarray:
 
 class TFStreamingAUC:
     def __init__(self, num_thresholds: int = 200):
-        self.thr = tf_thresholds(num_thresholds)
+        self.thr = tf_thresholds(num_thresholds).astype(np.float32)
         self.tp = np.zeros(num_thresholds, np.float64)
         self.fp = np.zeros(num_thresholds, np.float64)
         self.tn = np.zeros(num_thresholds, np.float64)
@@ -31,7 +33,8 @@ class TFStreamingAUC:
 
     def update(self, labels, preds) -> None:
         labels = _np(labels).astype(bool).reshape(-1)
-        preds = np.clip(_np(preds).astype(np.float64).reshape(-1), 0.0, 1.0)
+        # float32 compares, like TF's `predictions > thresholds` on float32 tensors
+        preds = np.clip(_np(preds).astype(np.float32).reshape(-1), 0.0, 1.0)
         # pred > thr counts via a sorted search: for each threshold, #preds strictly greater
         pos = np.sort(preds[labels])
         neg = np.sort(preds[~labels])
@@ -52,6 +55,53 @@ class TFStreamingAUC:
         tpr = (self.tp + _EPS) / (self.tp + self.fn + _EPS)
         fpr = self.fp / (self.fp + self.tn + _EPS)
         return float(np.sum((fpr[:-1] - fpr[1:]) * (tpr[:-1] + tpr[1:]) / 2.0))
+
+
+class DeviceAUC:
+    """``TFStreamingAUC`` counts accumulated on the GPU by one histogram kernel per batch
+    (metrics.hip) — no host synchronisation until ``result()``.  Also sums the
+    per-example losses.  ``state()`` has TFStreamingAUC's layout (ranks all-reduce it)."""
+
+    def __init__(self, device, num_thresholds: int = 200):
+        from .ops import require_hip
+
+        self.H = require_hip()
+        self.device = torch.device(device)
+        self.nt = num_thresholds
+        self.thr = torch.from_numpy(tf_thresholds(num_thresholds).astype(np.float32)).to(self.device)
+        self.hist = torch.zeros(2, num_thresholds + 1, dtype=torch.int64, device=self.device)
+        self.loss = torch.zeros(2, dtype=torch.float64, device=self.device)
+
+    def update(self, labels: torch.Tensor, preds: torch.Tensor, losses: Optional[torch.Tensor] = None) -> None:
+        n = int(preds.numel())
+        if n == 0:
+            return
+        preds = preds.reshape(-1).float().contiguous()
+        labels = labels.reshape(-1).to(self.device, torch.float32).contiguous()
+        p = self.H.AucHistParams()
+        p.prob, p.labels, p.n = preds.data_ptr(), labels.data_ptr(), n
+        p.thr, p.nt, p.hist = self.thr.data_ptr(), self.nt, self.hist.data_ptr()
+        if losses is not None:
+            losses = losses.reshape(-1).float().contiguous()
+            p.loss, p.loss_sum = losses.data_ptr(), self.loss.data_ptr()
+        self.H.auc_hist(p, torch.cuda.current_stream(self.device).cuda_stream)
+        self._keep = (preds, labels, losses)  # alive until the kernel has consumed them
+
+    def state(self) -> np.ndarray:
+        h = self.hist.cpu().numpy().astype(np.float64)
+        neg, pos = h[0], h[1]
+        tp = np.cumsum(pos[::-1])[::-1][1:]  # tp[i] = Σ_{k>i} pos[k]
+        fp = np.cumsum(neg[::-1])[::-1][1:]
+        return np.stack([tp, fp, neg.sum() - fp, pos.sum() - tp])
+
+    def streaming(self) -> "TFStreamingAUC":
+        a = TFStreamingAUC(self.nt)
+        a.load_state(self.state())
+        return a
+
+    def loss_total(self):
+        s = self.loss.cpu().numpy()
+        return float(s[0]), int(s[1])
 
 
 def exact_auc(labels, preds) -> float:

@@ -1,4 +1,5 @@
 """Numerics of the fused HIP kernels vs the plain-PyTorch fp32 oracle (rocfm/ops/reference.py)."""
+import numpy as np
 import pytest
 import torch
 
@@ -127,3 +128,24 @@ def test_fused_adam_matches_tf_formula_one_step():
         p = before[name].clone()
         apply_dense(hp, p, grads[name], init_slots(hp, p), 1)
         torch.testing.assert_close(got[name], p, rtol=1e-3, atol=1e-5)
+
+
+def test_device_auc_matches_streaming_auc():
+    from rocfm.metrics import DeviceAUC, TFStreamingAUC
+
+    g = torch.Generator().manual_seed(5)
+    ref = TFStreamingAUC()
+    dev = DeviceAUC("cuda")
+    tot = 0.0
+    for n in (1000, 4097, 1):
+        p = torch.rand(n, generator=g)
+        p[: n // 10] = torch.round(p[: n // 10] * 199) / 199  # exactly on thresholds
+        y = (torch.rand(n, generator=g) < p).float()
+        l = torch.rand(n, generator=g)
+        tot += float(l.double().sum())
+        ref.update(y, p)
+        dev.update(y.cuda(), p.cuda(), l.cuda())
+    np.testing.assert_array_equal(dev.state(), ref.state())
+    assert abs(dev.streaming().result() - ref.result()) < 1e-12
+    s, c = dev.loss_total()
+    assert c == 5098 and abs(s - tot) < 1e-3
