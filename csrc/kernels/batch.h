@@ -27,4 +27,34 @@ struct FetchParams {
 
 void launch_fetch_batch(const FetchParams& p, hipStream_t stream);
 
+// Batch preparation for a multi-step graph (S steps per replay): copies the next graph's S batches
+// into static slots in one launch, writes each lookup's composite sort key (slot << id_bits | id),
+// and the per-step global_step / Adam lr_t arrays.  Counters are double-buffered by graph parity:
+// batches start at *cur_src + advance (advance = the size of the graph running concurrently);
+// *cur_dst / *step_dst receive that start for the next preparation.
+struct FetchMultiParams {
+  const int32_t* ids_pool;
+  const float* vals_pool;
+  const float* labels_pool;
+  long long pool_batches;
+  int B, F, Bp;
+  int S;        // batches to prepare
+  int advance;  // steps of the graph this preparation runs beside
+  const int64_t* cur_src;
+  int64_t* cur_dst;
+  const int64_t* step_src;
+  int64_t* step_dst;
+  int32_t* ids;     // [S][Bp][F]
+  float* vals;      // [S][Bp][F]
+  float* labels;    // [S][Bp]
+  uint32_t* keys;   // [S][B*F] composite sort keys (nullable)
+  int id_bits;
+  int64_t* steps;   // [S] global_step of each prepared step
+  float* lrt;       // [S] lr_t of each prepared step
+  float lr, beta1, beta2;
+  int opt_type;
+};
+
+void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream);
+
 }  // namespace rocfm

@@ -48,4 +48,48 @@ void launch_fetch_batch(const FetchParams& p, hipStream_t stream) {
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 
+// grid: (blocks per batch, S)
+__global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams p) {
+  const int k = blockIdx.y;
+  const long long nb = p.pool_batches;
+  const long long start = *p.cur_src + p.advance;
+  long long b = (start + k) % nb;
+  if (b < 0) b += nb;
+  const long long n = (long long)p.B * p.F;
+  const int32_t* si = p.ids_pool + b * n;
+  const float* sv = p.vals_pool + b * n;
+  int32_t* di = p.ids + (long long)k * p.Bp * p.F;
+  float* dv = p.vals + (long long)k * p.Bp * p.F;
+  uint32_t* dk = p.keys ? p.keys + (long long)k * n : nullptr;
+  const uint32_t kb = (uint32_t)k << p.id_bits;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int32_t id = si[i];
+    di[i] = id;
+    dv[i] = sv[i];
+    if (dk) dk[i] = kb | (uint32_t)id;
+  }
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.B; i += (long long)gridDim.x * 256)
+    p.labels[(long long)k * p.Bp + i] = p.labels_pool[b * p.B + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t st = *p.step_src + p.advance + k;
+    p.steps[k] = st;
+    p.lrt[k] = p.opt_type == kAdam ? adam_lr_t(p.lr, p.beta1, p.beta2, st) : p.lr;
+    if (k == 0) {
+      *p.cur_dst = start;
+      *p.step_dst = *p.step_src + p.advance;
+    }
+  }
+}
+
+void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.pool_batches > 0 && p.S > 0, "fetch_multi: empty pool / S");
+  ROCFM_REQUIRE(p.cur_dst != p.cur_src && p.step_dst != p.step_src, "fetch_multi: counters must differ");
+  ROCFM_REQUIRE(p.keys == nullptr || ((unsigned long long)p.S << p.id_bits) <= (1ull << 32),
+                "fetch_multi: S << id_bits must fit in 32 bits");
+  const long long n = (long long)p.B * p.F;
+  const int gx = (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 64));
+  hipLaunchKernelGGL(fetch_multi_kernel, dim3(gx, p.S), dim3(256), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace rocfm

@@ -87,6 +87,8 @@ struct DenseApplyParams {
   OptParams opt;
   const int64_t* step;
   float grad_scale;
+  int nseg;                // > 1: grads are nseg rank segments (DP all-gather), summed in rank order
+  long long seg_stride;    // floats between segments
 };
 
 }  // namespace rocfm

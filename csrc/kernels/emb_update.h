@@ -24,13 +24,14 @@ struct EmbUpdateParams {
   uint32_t* out_keys;  // mode 2
   float* out_rows;     // mode 2: [cap][Kp]
   int* out_count;      // mode 2
-  int id_offset;       // subtracted from keys before indexing emb (row-shard local index)
+  uint32_t id_offset;  // subtracted from keys before indexing emb (multi-batch sort segment prefix)
   int id_stride;       // keys are mapped to local rows by (key - id_offset) / id_stride
   uint32_t max_key;    // runs with key >= max_key are skipped (padding sentinels); 0 = no limit
   int contrib_seg;     // if > 0: lookup j lives at contrib + (j/seg)*seg_stride + (j%seg)*Kp
   long long contrib_seg_stride;  // floats between segments (per-rank blocks of a gathered buffer)
   int out_cap;         // mode 2: capacity of out_keys/out_rows (rows past it are dropped, count kept)
   unsigned long long* stamps;  // diagnostic (nullable)
+  uint32_t val_base;   // subtracted from svals (a batch's segment of a multi-batch sort)
 };
 
 struct EmbDenseParams {

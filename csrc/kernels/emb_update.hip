@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
     key = p.skeys[i];
     head = (i == 0) || (p.skeys[i - 1] != key);
     const bool skip = p.max_key && key >= p.max_key;
-    const float4* src = contrib_row4(p, p.svals[i]);
+    const float4* src = contrib_row4(p, p.svals[i] - p.val_base);
 #pragma unroll
     for (int u = 0; u < KP4; ++u) v[u] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : src[u];
   } else {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdate
       const int j = k0 + t;
       float4 w[KP4];
       if (j < last_end) {
-        const float4* src = contrib_row4(p, p.svals[j]);
+        const float4* src = contrib_row4(p, p.svals[j] - p.val_base);
 #pragma unroll
         for (int u = 0; u < KP4; ++u) w[u] = src[u];
       } else {

@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256) void dense_apply_kernel(const DenseApplyParams
     float w = p.params[idx];
     if (p.apply) {
       float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
-      opt_apply(p.opt, st, w, p.grads[idx] * p.grad_scale, a, b);
+      float g = p.grads[idx];
+      for (int r = 1; r < p.nseg; ++r) g += p.grads[(size_t)r * p.seg_stride + idx];  // rank order
+      opt_apply(p.opt, st, w, g * p.grad_scale, a, b);
       p.params[idx] = w;
       if (p.s0) p.s0[idx] = a;
       if (p.s1) p.s1[idx] = b;

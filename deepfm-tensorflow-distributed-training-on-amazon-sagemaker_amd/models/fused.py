@@ -179,15 +179,17 @@ class FusedDeepFM:
 
         self._i = 0  # completed steps (host mirror of global_step)
         self._primed = False
+        self._m_primed = False
+        self.mS = None
         self._graphs = [None, None]
         self._warm = 0
         self._build_params()
         self.refresh_bf16()
 
     # ------------------------------------------------------------------------------------------
-    def _opt(self, p: int = 0):
+    def _opt(self, p: int = 0, lrt_ptr: Optional[int] = None):
         o = self.H.OptParams()
-        o.lrt = self.lrt[p:].data_ptr()
+        o.lrt = self.lrt[p:].data_ptr() if lrt_ptr is None else lrt_ptr
         hp = self.hp
         o.type = OPT_ID[hp.name]
         o.lr = hp.lr * self.lr_scale
@@ -229,67 +231,77 @@ class FusedDeepFM:
             raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
         return rp
 
-    def _build_params(self):
+    def _step_param_set(self, ids, vals, labels, step_ptr: int, lrt_ptr: int, skeys_ptr: int, svals_ptr: int,
+                        val_base: int = 0, id_offset: int = 0):
+        """Kernel parameter blocks of one step: (rows, wgrad, dense_apply, emb_update, emb_dense)."""
         H, L = self.H, self.layout
+        rows = self._rows_params(ids, vals, labels, self.prob, self.loss_rows, step_ptr, True)
+        wp = H.WgradParams()
+        wp.g = self.g.data_ptr()
+        wp.params = self.dense.data_ptr()
+        wp.grads = self.dense_grads_flat.data_ptr()
+        wp.s0, wp.s1 = self._slot_ptrs(self.dense_slots)
+        wp.step = step_ptr
+        wp.nl, wp.Bp = L.nl, self.Bp
+        wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
+        wp.fuse_opt = 1 if self.fuse_dense_opt else 0
+        wp.opt = self._opt(lrt_ptr=lrt_ptr)
+        wp.grad_scale = 1.0
+        wp.set_dims(L.dims)
+        for a in range(L.nl + 1):
+            wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
+        for l in range(L.nl):
+            wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+        dp = H.DenseApplyParams()
+        dp.params = self.dense.data_ptr()
+        dp.grads = self.dense_grads_flat.data_ptr()
+        dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
+        dp.step = step_ptr
+        dp.n, dp.nl = L.total, L.nl
+        dp.opt = self._opt(lrt_ptr=lrt_ptr)
+        dp.set_dims(L.dims)
+        for l in range(L.nl):
+            dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+        ep = H.EmbUpdateParams()
+        ep.skeys, ep.svals = skeys_ptr, svals_ptr
+        ep.n = self.n_lookup
+        ep.val_base, ep.id_offset = val_base, id_offset
+        ep.contrib = self.contrib.data_ptr()
+        ep.K1, ep.Kp = self.K1, self.Kp
+        ep.emb = self.emb.data_ptr()
+        ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
+        ep.l2 = float(self.spec.l2_reg)
+        ep.grad_scale = 1.0
+        ep.opt = self._opt(lrt_ptr=lrt_ptr)
+        ep.step = step_ptr
+        ep.mode = 1 if self.embedding_update == "exact" else 0
+        if self.dense_grad is not None:
+            ep.dense_grad = self.dense_grad.data_ptr()
+        ed = None
+        if self.embedding_update == "exact":
+            ed = H.EmbDenseParams()
+            ed.emb = self.emb.data_ptr()
+            ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
+            ed.dense_grad = self.dense_grad.data_ptr()
+            ed.step = step_ptr
+            ed.n4 = self.V * self.Kp // 4
+            ed.Kp, ed.K1 = self.Kp, self.K1
+            ed.l2 = float(self.spec.l2_reg)
+            ed.opt = self._opt(lrt_ptr=lrt_ptr)
+        return rows, wp, dp, ep, ed
+
+    def _build_params(self):
         self.rows_params, self.wgrad_params, self.dense_apply_params = [], [], []
         self.emb_params, self.emb_dense_params = [], []
         for p in range(2):
-            step_ptr = self.steps[p:].data_ptr()
-            self.rows_params.append(self._rows_params(self.slot_ids[p], self.slot_vals[p], self.slot_labels[p],
-                                                      self.prob, self.loss_rows, step_ptr, True))
-            wp = H.WgradParams()
-            wp.g = self.g.data_ptr()
-            wp.params = self.dense.data_ptr()
-            wp.grads = self.dense_grads_flat.data_ptr()
-            wp.s0, wp.s1 = self._slot_ptrs(self.dense_slots)
-            wp.step = step_ptr
-            wp.nl, wp.Bp = L.nl, self.Bp
-            wp.off_wout, wp.off_bout, wp.off_fmb = L.off_wout, L.off_bout, L.off_fmb
-            wp.fuse_opt = 1 if self.fuse_dense_opt else 0
-            wp.opt = self._opt(p)
-            wp.grad_scale = 1.0
-            wp.set_dims(L.dims)
-            for a in range(L.nl + 1):
-                wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
-            for l in range(L.nl):
-                wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+            rows, wp, dp, ep, ed = self._step_param_set(
+                self.slot_ids[p], self.slot_vals[p], self.slot_labels[p], self.steps[p:].data_ptr(),
+                self.lrt[p:].data_ptr(), self.skeys[p].data_ptr(), self.svals[p].data_ptr())
+            self.rows_params.append(rows)
             self.wgrad_params.append(wp)
-            dp = H.DenseApplyParams()
-            dp.params = self.dense.data_ptr()
-            dp.grads = self.dense_grads_flat.data_ptr()
-            dp.s0, dp.s1 = self._slot_ptrs(self.dense_slots)
-            dp.step = step_ptr
-            dp.n, dp.nl = L.total, L.nl
-            dp.opt = self._opt(p)
-            dp.set_dims(L.dims)
-            for l in range(L.nl):
-                dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
             self.dense_apply_params.append(dp)
-            ep = H.EmbUpdateParams()
-            ep.skeys, ep.svals = self.skeys[p].data_ptr(), self.svals[p].data_ptr()
-            ep.n = self.n_lookup
-            ep.contrib = self.contrib.data_ptr()
-            ep.K1, ep.Kp = self.K1, self.Kp
-            ep.emb = self.emb.data_ptr()
-            ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
-            ep.l2 = float(self.spec.l2_reg)
-            ep.grad_scale = 1.0
-            ep.opt = self._opt(p)
-            ep.step = step_ptr
-            ep.mode = 1 if self.embedding_update == "exact" else 0
-            if self.dense_grad is not None:
-                ep.dense_grad = self.dense_grad.data_ptr()
             self.emb_params.append(ep)
-            if self.embedding_update == "exact":
-                ed = H.EmbDenseParams()
-                ed.emb = self.emb.data_ptr()
-                ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
-                ed.dense_grad = self.dense_grad.data_ptr()
-                ed.step = step_ptr
-                ed.n4 = self.V * self.Kp // 4
-                ed.Kp, ed.K1 = self.Kp, self.K1
-                ed.l2 = float(self.spec.l2_reg)
-                ed.opt = self._opt(p)
+            if ed is not None:
                 self.emb_dense_params.append(ed)
         self.pred_params = self._rows_params(self.pred_ids, self.pred_vals, self.pred_labels, self.pred_prob,
                                              self.pred_loss, self.steps.data_ptr(), False)
@@ -329,6 +341,7 @@ class FusedDeepFM:
         self._graphs = [None, None]
         self._multi_graph = None
         self._primed = False
+        self._m_primed = False
         self._start_batch = start
 
     def push_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor) -> None:
@@ -387,6 +400,8 @@ class FusedDeepFM:
             f.lr = self.hp.lr * self.lr_scale
         self._graphs = [None, None]
         self._primed = False
+        if getattr(self, "mS", None) is not None:
+            self._build_multi(self.mS)  # rebuild the multi-step parameter blocks with the new lr
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -480,9 +495,152 @@ class FusedDeepFM:
         self._join(aux)
         self._join(side)
 
+    def _enqueue_pipelined(self, S: int) -> None:
+        """S consecutive steps for one multi-step graph, with the side chain decoupled from the
+        step boundary: step k's side chain (fetch + sort of batch k+1) forks at the start of
+        step k; step k+1's rows kernel waits only for that fetch and its embedding update only
+        for that sort, so the sort overlaps the rest of step k AND the rows kernel of step k+1."""
+        main = torch.cuda.current_stream(self.device)
+        side = self.sort_stream
+        prev = None
+        for k in range(S):
+            p = k % 2
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.H.fetch_batch(self.fetch_params[p], side.cuda_stream)
+                ev_fetch = torch.cuda.Event()
+                ev_fetch.record(side)
+                self._sort(1 - p, side)
+                ev_sort = torch.cuda.Event()
+                ev_sort.record(side)
+            if prev is not None:
+                main.wait_event(prev[0])
+            aux = self._enqueue_rows_then_fork_wgrad(p)
+            if prev is not None:
+                main.wait_event(prev[1])
+            self._enqueue_emb_update(p)
+            self._join(aux)
+            prev = (ev_fetch, ev_sort)
+        main.wait_stream(side)
+
+    # ---- multi-step graphs (pool mode) ------------------------------------------------------------
+    # One graph replays S steps whose main stream is strictly serial (rows → wgrad → emb_update per
+    # step: cross-stream waits inside a graph cost more than the concurrency they buy — measured
+    # 47 vs 55 µs/step); ONE side chain per graph prepares the NEXT graph's S batches (one copy
+    # kernel) and sorts all S·B·F lookups at once (composite key batch << id_bits | id), joined
+    # at the graph's end.
+    def _build_multi(self, Smax: int) -> None:
+        H, dev = self.H, self.device
+        Bp, F, n = self.Bp, self.F, self.n_lookup
+        idbits = max(1, math.ceil(math.log2(max(self.V, 2))))
+        Smax = max(1, min(int(Smax), 1 << max(0, 32 - idbits)))
+        sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
+        self.mS, self.m_idbits, self.m_bits = Smax, idbits, idbits + sbits
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.m_ids = torch.zeros(2, Smax, Bp, F, **i32)
+        self.m_vals = torch.zeros(2, Smax, Bp, F, dtype=torch.float32, device=dev)
+        self.m_labels = torch.zeros(2, Smax, Bp, dtype=torch.float32, device=dev)
+        self.m_keys = torch.zeros(Smax * n, **i32)
+        self.m_sk = torch.zeros(2, Smax * n, **i32)
+        self.m_sv = torch.zeros(2, Smax * n, **i32)
+        self.m_temp = torch.zeros(max(H.sort_pairs_temp_bytes(Smax * n, self.m_bits), 16), dtype=torch.uint8,
+                                  device=dev)
+        self.m_steps = torch.zeros(2, Smax, dtype=torch.int64, device=dev)
+        self.m_lrt = torch.zeros(2, Smax, dtype=torch.float32, device=dev)
+        self.m_cur = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.m_step = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.m_params = [[self._step_param_set(self.m_ids[q, k], self.m_vals[q, k], self.m_labels[q, k],
+                                               self.m_steps[q, k:].data_ptr(), self.m_lrt[q, k:].data_ptr(),
+                                               self.m_sk[q, k * n:].data_ptr(), self.m_sv[q, k * n:].data_ptr(),
+                                               val_base=k * n, id_offset=k << idbits)
+                          for k in range(Smax)] for q in range(2)]
+        self._m_graphs = {}
+        self._m_primed = False
+        self._m_warm = 0
+        self._mq = 0
+
+    def _fetch_multi_params(self, q: int, advance: int):
+        """Preparation run beside a graph of parity q and ``advance`` steps: batches start at
+        m_cur[q] + advance, written to the parity 1-q slots."""
+        f = self.H.FetchMultiParams()
+        f.ids_pool, f.vals_pool, f.labels_pool = (self.pool_ids.data_ptr(), self.pool_vals.data_ptr(),
+                                                  self.pool_labels.data_ptr())
+        f.pool_batches = self.pool_ids.shape[0]
+        f.B, f.F, f.Bp, f.S, f.advance = self.B, self.F, self.Bp, self.mS, advance
+        f.cur_src, f.cur_dst = self.m_cur[q:].data_ptr(), self.m_cur[1 - q:].data_ptr()
+        f.step_src, f.step_dst = self.m_step[q:].data_ptr(), self.m_step[1 - q:].data_ptr()
+        f.ids, f.vals, f.labels = (self.m_ids[1 - q].data_ptr(), self.m_vals[1 - q].data_ptr(),
+                                   self.m_labels[1 - q].data_ptr())
+        f.keys, f.id_bits = self.m_keys.data_ptr(), self.m_idbits
+        f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
+        f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
+        f.opt_type = OPT_ID[self.hp.name]
+        return f
+
+    def _prepare_multi(self, q: int, advance: int, stream) -> None:
+        H = self.H
+        H.fetch_multi(self._fetch_multi_params(q, advance), stream.cuda_stream)
+        H.sort_pairs_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys.data_ptr(),
+                          self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
+                          self.m_bits, stream.cuda_stream)
+
+    def _prime_multi(self) -> None:
+        base = 0 if self._ring else getattr(self, "_start_batch", 0)
+        self.m_cur[1] = base + self._i
+        self.m_step[1] = self._i
+        self._prepare_multi(1, 0, torch.cuda.current_stream(self.device))  # → parity-0 buffers
+        self._mq = 0
+        self._m_primed = True
+
+    def _enqueue_multi(self, q: int, S: int) -> None:
+        H = self.H
+        main = torch.cuda.current_stream(self.device)
+        side = self.sort_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._prepare_multi(q, S, side)
+        s = main.cuda_stream
+        for k in range(S):
+            rows, wp, _, ep, ed = self.m_params[q][k]
+            H.deepfm_rows(rows, s)
+            H.mlp_wgrad(wp, s)
+            H.emb_rows_update(ep, s)
+            if ed is not None:
+                H.emb_dense_update(ed, s)
+        main.wait_stream(side)
+
+    def _train_steps_multi(self, n: int, Smax: int) -> None:
+        if getattr(self, "mS", None) is None or self.mS != Smax or getattr(self, "_m_pool", None) is not self.pool_ids:
+            self._build_multi(Smax)
+            self._m_pool = self.pool_ids
+        if not self._m_primed:
+            self._prime_multi()
+        while n > 0:
+            S = min(n, self.mS)
+            q = self._mq
+            if self._m_warm < 1:
+                self._enqueue_multi(q, S)  # first run eager (code objects load outside capture)
+            else:
+                g = self._m_graphs.get((q, S))
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize(self.device)
+                    with torch.cuda.graph(g):
+                        self._enqueue_multi(q, S)
+                    self._m_graphs[(q, S)] = g
+                g.replay()
+            self._m_warm += 1
+            self._mq ^= 1
+            self._i += S
+            n -= S
+        self._primed = False  # the per-step path re-primes from the global step if used next
+
     def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
         """``n`` optimisation steps from the attached pool; full step-pairs are replayed from one
         multi-step HIP graph (``steps_per_graph`` steps per launch) to amortise launch overhead."""
+        if self.use_graph and not self._ring and self.fuse_dense_opt and steps_per_graph > 1:
+            self._train_steps_multi(n, steps_per_graph)
+            return
         S = max(2, steps_per_graph // 2 * 2)
         while n > 0:
             if (self.use_graph and self._primed and self._warm >= 2 and n >= S and self._i % 2 == 0
@@ -492,8 +650,7 @@ class FusedDeepFM:
                     g = torch.cuda.CUDAGraph()
                     torch.cuda.synchronize(self.device)
                     with torch.cuda.graph(g):
-                        for k in range(S):
-                            self._enqueue_step(k % 2)
+                        self._enqueue_pipelined(S)
                     self._multi_graph, self._multi_S = g, S
                 g.replay()
                 self._i += S
@@ -506,6 +663,7 @@ class FusedDeepFM:
         """One optimisation step on the current batch (asynchronous)."""
         if not self.fuse_dense_opt:
             raise RuntimeError("train_step() is the single-GPU step; distributed steps live in rocfm.parallel")
+        self._m_primed = False
         if not self._primed:
             self.prime()
         p = self._i % 2
@@ -591,6 +749,7 @@ class FusedDeepFM:
         self.refresh_bf16()
         self._graphs = [None, None]
         self._primed = False
+        self._m_primed = False
         self._pushed = self._i
 
     def _tf_views(self, emb_like: torch.Tensor, dense_like: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":

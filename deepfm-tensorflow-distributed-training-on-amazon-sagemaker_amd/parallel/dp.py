@@ -189,7 +189,6 @@ class FusedDataParallel:
             self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
-            self.mlp_sum = torch.zeros(P, dtype=torch.float32, device=e.device)
             # merge maps (merge.hip): position of each key in every rank's list, representative rank
             self.pos = torch.empty(self.world * e.V, dtype=torch.int32, device=e.device)
             self.rep = torch.empty(e.V, dtype=torch.int32, device=e.device)
@@ -223,9 +222,9 @@ class FusedDataParallel:
                 mp_.mode = 0
                 mp_.overflow = self.overflow.data_ptr()
                 self.merge_params.append(mp_)
-                e.dense_apply_params[p].apply = 1
-                e.dense_apply_params[p].grads = self.mlp_sum.data_ptr()
-                e.dense_apply_params[p].grad_scale = 1.0 / self.world
+                da = e.dense_apply_params[p]
+                da.apply, da.grads, da.grad_scale = 1, self.recv.data_ptr(), 1.0 / self.world
+                da.nseg, da.seg_stride = self.world, self.S
             H.merge_init(self.merge_params[0], e.stream_ptr)
             self.recv2d = self.recv.view(self.world, self.S)
         for p in range(2):
@@ -285,11 +284,16 @@ class FusedDataParallel:
             e.H.dense_apply(e.dense_apply_params[p], s)
             e.H.emb_dense_update(e.emb_dense_params[p], s)
             return
-        P = e.layout.total
-        torch.sum(self.recv2d[:, :P], dim=0, out=self.mlp_sum)  # rank order: deterministic
-        e.H.dense_apply(e.dense_apply_params[p], s)
+        # MLP: Σ over the gathered rank segments (rank order) + optimizer, on the aux stream,
+        # concurrently with the embedding merge on the main stream
+        main = torch.cuda.current_stream(self.device)
+        aux = e.aux_stream
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            e.H.dense_apply(e.dense_apply_params[p], aux.cuda_stream)
         e.H.merge_scatter(self.merge_params[p], s)
         e.H.merge_apply(self.merge_params[p], s)
+        e._join(aux)
 
     def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:

@@ -575,11 +575,16 @@ class FusedRowShard:
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
         s = e.stream_ptr
+        main = torch.cuda.current_stream(self.device)
+        aux = e.aux_stream  # MLP optimizer concurrently with the owner's row update
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            H.dense_apply(e.dense_apply_params[p], aux.cuda_stream)
         H.merge_scatter(self.owner_params[p], s)
         H.merge_apply(self.owner_params[p], s)
         if self.embedding_update == "exact":
             H.emb_dense_update(e.emb_dense_params[p], s)
-        H.dense_apply(e.dense_apply_params[p], s)
+        e._join(aux)
 
     def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:

@@ -149,3 +149,34 @@ def test_device_auc_matches_streaming_auc():
     assert abs(dev.streaming().result() - ref.result()) < 1e-12
     s, c = dev.loss_total()
     assert c == 5098 and abs(s - tot) < 1e-3
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_multi_step_graph_equals_per_step(update):
+    """The multi-step pipeline (S steps per graph, one batched sort per graph, eager first graph,
+    tail graph of S' < S) trains bit-identically to per-step eager training."""
+    spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[0.7, 0.8],
+                     l2_reg=1e-3)
+    hp = OptHParams(name="Adam", lr=2e-3)
+    g = torch.Generator().manual_seed(9)
+    NB, B = 5, 128
+    pool = [_batch(B, 39, 3000, g) for _ in range(NB)]
+    ids = torch.stack([p[0] for p in pool]).cuda()
+    vals = torch.stack([p[1] for p in pool]).cuda()
+    labels = torch.stack([p[2] for p in pool]).cuda()
+    a = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), embedding_update=update, use_graph=True)
+    b = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), embedding_update=update, use_graph=False)
+    a.attach_pool(ids, vals, labels)
+    b.attach_pool(ids, vals, labels)
+    a.train_steps(21, 8)  # 8 eager + 8 graph + 5 tail graph
+    for _ in range(21):
+        b.train_step()
+    torch.cuda.synchronize()
+    assert a.global_step() == b.global_step() == 21
+    assert torch.equal(a.emb, b.emb) and torch.equal(a.dense, b.dense)
+    assert torch.equal(a.emb_slots[1], b.emb_slots[1])
+    # switching back to per-step training continues from the same global step / batch
+    a.train_step()
+    b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.emb, b.emb)
