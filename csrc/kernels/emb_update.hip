@@ -14,231 +14,18 @@
 // mode 1 (exact) : write Σ grads into a dense grad table; emb_dense_update_kernel then applies
 //                  λ·θ + optimizer to EVERY row, as TF does for the dense gradient (Q1)
 // mode 2 (export): emit (id, Σ grad row) compacted, for cross-rank exchange (DP / row-shard)
-#include "emb_update.h"
+#include "emb_body.h"
 
 namespace rocfm {
 
-namespace {
-
-constexpr int kChunk = 256;
-
-__device__ __forceinline__ const float4* contrib_row4(const EmbUpdateParams& p, uint32_t j) {
-  const float* r = (p.contrib_seg > 0) ? p.contrib + (size_t)(j / (uint32_t)p.contrib_seg) * p.contrib_seg_stride +
-                                             (size_t)(j % (uint32_t)p.contrib_seg) * p.Kp
-                                       : p.contrib + (size_t)j * p.Kp;
-  return reinterpret_cast<const float4*>(r);
-}
-
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-__device__ __forceinline__ float4 f4shfl_up(float4 v, int d) {
-  return make_float4(__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64), __shfl_up(v.z, d, 64), __shfl_up(v.w, d, 64));
-}
-__device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
-  return make_float4(__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64), __shfl_xor(v.z, d, 64), __shfl_xor(v.w, d, 64));
-}
-
-}  // namespace
-
-// One workgroup per 256 consecutive sorted entries.  Every thread loads ONE entry's gradient row
-// (Kp floats, float4 loads) into LDS, so the chunk's rows arrive in one memory latency; run pieces
-// are summed by a wave-level segmented scan (shfl_up, fixed order); each run owned by the chunk
-// (its first entry lies here) adds its ≤4 wave pieces and, for the chunk's last run, the
-// continuation chunks; then one 16-lane group per run applies the optimizer to the table row.
 template <int KP4>
-__global__ __launch_bounds__(kChunk) void emb_rows_update_kernel(const EmbUpdateParams p) {
-  __shared__ float4 s_rows[kChunk * KP4];
-  __shared__ float4 s_cont[4 * KP4];
-  __shared__ int s_head[kChunk + 1];
-  __shared__ int s_wcnt[4];
-  __shared__ int s_nh, s_last_end, s_out_base;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int c0 = blockIdx.x * kChunk;
-  const int cend = min(c0 + kChunk, p.n);
-  const int i = c0 + t;
-  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
-  ROCFM_STAMP(p.stamps, 0);
-
-  // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
-  uint32_t key = 0xffffffffu;
-  bool head = false;
-  float4 v[KP4];
-  if (i < p.n) {
-    key = p.skeys[i];
-    head = (i == 0) || (p.skeys[i - 1] != key);
-    const bool skip = p.max_key && key >= p.max_key;
-    const float4* src = contrib_row4(p, p.svals[i] - p.val_base);
-#pragma unroll
-    for (int u = 0; u < KP4; ++u) v[u] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : src[u];
-  } else {
-#pragma unroll
-    for (int u = 0; u < KP4; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // 2. wave-level segmented inclusive scan (segments: runs, cut at wave boundaries)
-  {
-    const unsigned long long hm = __ballot(head || lane == 0 || i >= p.n);
-    const unsigned long long below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-    const int seg = 63 - __clzll(hm & below);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-      for (int u = 0; u < KP4; ++u) {
-        const float4 o = f4shfl_up(v[u], d);
-        if (lane - d >= seg) v[u] = f4add(v[u], o);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
-  }
-  // 3. compact the heads in order
-  const unsigned long long m = __ballot(head);
-  const int before = __popcll(m & ((1ull << lane) - 1ull));
-  if (lane == 0) s_wcnt[wave] = __popcll(m);
-  __syncthreads();
-  {
-    int base = 0;
-    for (int w = 0; w < wave; ++w) base += s_wcnt[w];
-    if (head) s_head[base + before] = i;
-  }
-  if (t == 0) s_nh = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
-  __syncthreads();
-  ROCFM_STAMP(p.stamps, 1);
-  const int nh = s_nh;
-  if (nh == 0) return;
-  // 4. end of the last run (all 256 threads probe 256 entries per round); mode 2 reserves slots
-  {
-    const int last = s_head[nh - 1];
-    const uint32_t lk = p.skeys[last];
-    const bool sentinel = p.max_key && lk >= p.max_key;  // sentinel padding sorts last: runs to n
-    int pos = sentinel ? p.n : cend;
-    if (t == 0) s_last_end = p.n;
-    __syncthreads();
-    while (pos < p.n) {
-      const int j = pos + t;
-      const bool diff = (j >= p.n) || (p.skeys[j] != lk);
-      const unsigned long long dm = __ballot(diff);
-      if (lane == 0) s_wcnt[wave] = dm ? (__ffsll((long long)dm) - 1) : 64;
-      __syncthreads();
-      int found = -1;
-      for (int w = 0; w < 4; ++w)
-        if (s_wcnt[w] < 64) {
-          found = pos + 64 * w + s_wcnt[w];
-          break;
-        }
-      __syncthreads();
-      if (found >= 0) {
-        if (t == 0) s_last_end = min(found, p.n);
-        break;
-      }
-      pos += kChunk;
-    }
-    if (t == 0 && p.mode == 2) s_out_base = atomicAdd(p.out_count, nh);
-  }
-  __syncthreads();
-  ROCFM_STAMP(p.stamps, 2);
-  if (t == 0) s_head[nh] = min(s_last_end, cend);
-  // 5. continuation of the last run past the chunk: full reductions over following chunks
-  const int last_end = s_last_end;
-  const bool cont = last_end > cend && !(p.max_key && p.skeys[s_head[nh - 1]] >= p.max_key);
-  if (cont) {
-    float4 tot[KP4];
-#pragma unroll
-    for (int u = 0; u < KP4; ++u) tot[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k0 = cend; k0 < last_end; k0 += kChunk) {
-      const int j = k0 + t;
-      float4 w[KP4];
-      if (j < last_end) {
-        const float4* src = contrib_row4(p, p.svals[j] - p.val_base);
-#pragma unroll
-        for (int u = 0; u < KP4; ++u) w[u] = src[u];
-      } else {
-#pragma unroll
-        for (int u = 0; u < KP4; ++u) w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < KP4; ++u) {
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) w[u] = f4add(w[u], f4shfl_xor(w[u], d));
-        tot[u] = f4add(tot[u], w[u]);
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int u = 0; u < KP4; ++u) s_cont[wave * KP4 + u] = tot[u];
-    }
-  }
-  __syncthreads();
-  ROCFM_STAMP(p.stamps, 3);
-  // 6. (run, column) items over all threads: add the run's wave pieces (+ continuation), then the
-  //    optimizer; every thread issues its table/slot loads for up to 4 items before using any.
-  constexpr int Kp = KP4 * 4;
-  const int nitems = nh * Kp;
-  for (int base = 0; base < nitems; base += kChunk * 4) {
-    float w[4], a[4], b[4], g[4];
-    uint32_t kk[4];
-    size_t idx[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = min(base + u * kChunk + t, nitems - 1);
-      const int r = it / Kp, col = it - r * Kp;
-      const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
-      kk[u] = p.skeys[s];
-      const bool skip = p.max_key && kk[u] >= p.max_key;
-      const int u4 = col >> 2, comp = col & 3;
-      float acc = 0.f;
-      const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
-      for (int ww = w0; ww <= w1; ++ww) {
-        const int lastw = min(e, c0 + 64 * (ww + 1)) - 1 - c0;
-        const float4 x = s_rows[lastw * KP4 + u4];
-        acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
-      }
-      if (cont && r == nh - 1) {
-#pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
-          const float4 x = s_cont[ww * KP4 + u4];
-          acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
-        }
-      }
-      g[u] = acc * p.grad_scale;
-      const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
-      idx[u] = row * Kp + col;
-      if (p.mode == 0) {  // issue the row's parameter + slot loads now
-        w[u] = p.emb[idx[u]];
-        a[u] = p.s0 ? p.s0[idx[u]] : 0.f;
-        b[u] = p.s1 ? p.s1[idx[u]] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = base + u * kChunk + t;
-      if (it >= nitems) continue;
-      const int r = it / Kp, col = it - r * Kp;
-      if ((p.max_key && kk[u] >= p.max_key) || col >= p.K1) continue;
-      if (p.mode == 2) {
-        const int slot = s_out_base + r;
-        if (slot < p.out_cap) {
-          p.out_rows[(size_t)slot * Kp + col] = g[u];
-          if (col == 0) p.out_keys[slot] = kk[u];
-        }
-      } else if (p.mode == 1) {
-        p.dense_grad[idx[u]] = g[u];
-      } else {
-        float ww = w[u], aa = a[u], bb = b[u];
-        opt_apply(p.opt, st, ww, g[u] + p.l2 * ww, aa, bb);
-        p.emb[idx[u]] = ww;
-        if (p.s0) p.s0[idx[u]] = aa;
-        if (p.s1) p.s1[idx[u]] = bb;
-      }
-    }
-  }
-  __syncthreads();
-  ROCFM_STAMP(p.stamps, 4);
+__global__ __launch_bounds__(kEmbChunk) void emb_rows_update_kernel(const EmbUpdateParams p) {
+  emb_rows_body<KP4, kEmbChunk>(p, blockIdx.x);
 }
 
 template <int KP4>
 static void launch_rows_update_t(const EmbUpdateParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(emb_rows_update_kernel<KP4>, dim3(cdiv(p.n, kChunk)), dim3(kChunk), 0, stream, p);
+  hipLaunchKernelGGL(emb_rows_update_kernel<KP4>, dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream, p);
 }
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {

@@ -1,0 +1,46 @@
+// The tail of a training step in ONE launch: the MLP weight gradients + fused optimizer
+// (wgrad_body, mlp_wgrad.hip) and the embedding-row update (emb_rows_body, emb_update.hip) are
+// independent — one reads the transposed activations / output gradients, the other the per-lookup
+// gradient rows and the sorted keys — so they run as disjoint workgroup roles of one grid
+// (≈70 wgrad + ⌈B·F/512⌉ embedding workgroups, all co-resident on 256 CUs).  This replaces two
+// serial launches (≈10 + 15 µs) or a second stream (whose fork/join inside a HIP graph costs more
+// than it overlaps) with ≈max of the two.
+#include "emb_body.h"
+#include "wgrad_body.h"
+
+namespace rocfm {
+
+constexpr int kTailThreads = 512;
+static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
+
+template <int KP4>
+__global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
+                                                                 const int n_emb) {
+  const int bid = blockIdx.x;
+  if (bid < n_emb)
+    emb_rows_body<KP4, kTailThreads>(e, bid);  // the longer role first: its workgroups dispatch first
+  else
+    wgrad_body(w, bid - n_emb);
+}
+
+void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
+  ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= 32 && e.K1 <= e.Kp, "step_tail: Kp must be a multiple of 4 and <= 32");
+  ROCFM_REQUIRE(e.mode != 2, "step_tail: export mode needs a zeroed counter; use emb_rows_update");
+  if (e.id_stride <= 0) e.id_stride = 1;
+  const int n_wg = wgrad_prepare(w);
+  const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
+  const dim3 grid(n_emb + n_wg), block(kTailThreads);
+  switch (e.Kp / 4) {
+#define ROCFM_KP4(N)                                                              \
+  case N:                                                                         \
+    hipLaunchKernelGGL(step_tail_kernel<N>, grid, block, 0, stream, w, e, n_emb); \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+#undef ROCFM_KP4
+    default:  // the 512-entry row staging of larger rows + the wgrad tiles exceed 160 KiB of LDS
+      throw std::invalid_argument("step_tail: Kp > 32 unsupported (use mlp_wgrad + emb_rows_update)");
+  }
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace rocfm

@@ -1,0 +1,194 @@
+// Device body of the MLP weight-gradient kernel (mlp_wgrad.hip; also fused into step_tail.hip).
+#pragma once
+#include "deepfm_rows.h"
+
+namespace rocfm {
+
+namespace {
+
+__device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, int idx, float g) {
+  if (p.fuse_opt) {
+    float w = p.params[idx], a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
+    opt_apply(p.opt, st, w, g, a, b);
+    p.params[idx] = w;
+    if (p.s0) p.s0[idx] = a;
+    if (p.s1) p.s1[idx] = b;
+  } else {
+    p.grads[idx] = g;
+  }
+}
+
+__device__ __forceinline__ float sum_bf16x8(uint4 v) {
+  return bf2f(v.x & 0xffff) + bf2f(v.x >> 16) + bf2f(v.y & 0xffff) + bf2f(v.y >> 16) + bf2f(v.z & 0xffff) +
+         bf2f(v.z >> 16) + bf2f(v.w & 0xffff) + bf2f(v.w >> 16);
+}
+__device__ __forceinline__ float dot_bf16x8_f32(uint4 v, const float* g) {
+  return bf2f(v.x & 0xffff) * g[0] + bf2f(v.x >> 16) * g[1] + bf2f(v.y & 0xffff) * g[2] + bf2f(v.y >> 16) * g[3] +
+         bf2f(v.z & 0xffff) * g[4] + bf2f(v.z >> 16) * g[5] + bf2f(v.w & 0xffff) * g[6] + bf2f(v.w >> 16) * g[7];
+}
+
+}  // namespace
+
+constexpr int kWgThreads = 512;  // 8 waves: each takes 1/8 of the batch
+
+__device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) {
+  __shared__ __attribute__((aligned(16))) float s_red[(kWgThreads / 64) * 16 * 64];
+  __shared__ uint16_t s_T[32 * 34];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
+  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  const int Bp = p.Bp;
+  ROCFM_STAMP(p.stamps, 0);
+
+  if (bid < n_tiles) {
+    int li = 0;
+    while (bid >= p.tile_start[li + 1]) ++li;
+    const int Din = p.dims[li], Dout = p.dims[li + 1];
+    const int local = bid - p.tile_start[li];
+    const int nto = Dout >> 5;
+    const int ti = local / nto, to = local % nto;
+    const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
+    const uint16_t* Bm = p.dzT[li + 1] + (size_t)(to * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
+    const int q = Bp >> 3;  // batch eighth per wave (Bp % 64 == 0 → q % 8 == 0, a multiple of 16 for Bp >= 128)
+    f32x16 acc = {};
+    const int bs = wave * q, be = bs + q;
+    const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b0 = bs; b0 < be; b0 += 16 * 8) {  // 8 k-steps of loads in flight per batch
+      bf16x8 fa[8], fb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = max(bs, min(b0 + 16 * u, be - 16));
+        fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
+        fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (b0 + 16 * u >= be) fa[u] = zero;
+        acc = mfma32x32x16(fa[u], fb[u], acc);
+      }
+    }
+    // every wave parks its partial tile in LDS; then all 512 threads own 2 tile elements each
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s_red[(wave * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    ROCFM_STAMP(p.stamps, 1);
+    float g[2], w[2], a[2], b[2];
+    int idx[2], il[2], ol[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int el = t + kWgThreads * e, r = el >> 6, ln = el & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < kWgThreads / 64; ++ww) v += s_red[(ww * 16 + r) * 64 + ln];
+      g[e] = v * p.grad_scale;
+      il[e] = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+      ol[e] = ln & 31;
+      idx[e] = p.offW[li] + (ti * 32 + il[e]) * Dout + to * 32 + ol[e];
+    }
+    if (!p.fuse_opt) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) p.grads[idx[e]] = g[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        w[e] = p.params[idx[e]];
+        a[e] = p.s0 ? p.s0[idx[e]] : 0.f;
+        b[e] = p.s1 ? p.s1[idx[e]] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        opt_apply(p.opt, st, w[e], g[e], a[e], b[e]);
+        p.params[idx[e]] = w[e];
+        if (p.s0) p.s0[idx[e]] = a[e];
+        if (p.s1) p.s1[idx[e]] = b[e];
+        const uint16_t hw = f2bf(w[e]);
+        p.Wb[li][(size_t)(ti * 32 + il[e]) * Dout + to * 32 + ol[e]] = hw;  // 64-B runs along o
+        s_T[ol[e] * 34 + il[e]] = hw;
+      }
+      __syncthreads();
+      {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
+        const int o = t >> 4, ip = (t & 15) * 2;
+        const uint32_t v2 = (uint32_t)s_T[o * 34 + ip] | ((uint32_t)s_T[o * 34 + ip + 1] << 16);
+        *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)(to * 32 + o) * Din + ti * 32 + ip) = v2;
+      }
+    }
+    ROCFM_STAMP(p.stamps, 2);
+    return;
+  }
+  // column reductions over the batch: 16 threads per column, 8 chunks (64 rows) in flight each
+  const int sub = t & 15;
+  if (bid < n_tiles + n_bias) {  // bias gradients: Σ_b dz[o][b] for 32 columns
+    const int lb = bid - n_tiles;
+    int li = 0;
+    while (lb >= p.bias_start[li + 1]) ++li;
+    const int cb = lb - p.bias_start[li];
+    const int o = cb * 32 + (t >> 4);
+    const uint16_t* row = p.dzT[li + 1] + (size_t)o * Bp;
+    float s = 0.f;
+    for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + 128 * u < Bp) s += sum_bf16x8(v[u]);
+    }
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
+    if (sub == 0) emit(p, st, p.offb[li] + o, s * p.grad_scale);
+    return;
+  }
+  // output layer: dW_out[c] = Σ_b h[c][b]·g[b]; d b_out = d fm_bias = Σ_b g[b]
+  {
+    const int Dn = p.dims[p.nl];
+    const uint16_t* H = p.actT[p.nl];
+    for (int c0 = 0; c0 < Dn; c0 += 32) {
+      const int c = min(c0 + (t >> 4), Dn - 1);
+      const uint16_t* row = H + (size_t)c * Bp;
+      float s = 0.f;
+      for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (b0 + 128 * u < Bp) s += dot_bf16x8_f32(v[u], p.g + b0 + 128 * u);
+      }
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
+      if (sub == 0 && c0 + (t >> 4) < Dn) emit(p, st, p.off_wout + c, s * p.grad_scale);
+    }
+    float s = 0.f;
+    for (int b = t; b < Bp; b += kWgThreads) s += p.g[b];
+    s = wave_sum(s);
+    if (lane == 0) s_red[wave] = s;
+    __syncthreads();
+    if (t == 0) {
+      float tot = 0.f;
+      for (int w = 0; w < kWgThreads / 64; ++w) tot += s_red[w];
+      tot *= p.grad_scale;
+      emit(p, st, p.off_bout, tot);
+      emit(p, st, p.off_fmb, tot);
+    }
+  }
+}
+
+
+// Fills the per-layer tile / bias workgroup offsets; returns the grid size.
+inline int wgrad_prepare(WgradParams& p) {
+  ROCFM_REQUIRE(p.Bp % 128 == 0, "mlp_wgrad: Bp must be a multiple of 128");
+  p.tile_start[0] = 0;
+  p.bias_start[0] = 0;
+  for (int l = 0; l < p.nl; ++l) {
+    ROCFM_REQUIRE(p.dims[l] % 32 == 0 && p.dims[l + 1] % 32 == 0, "mlp_wgrad: dims must be padded to 32");
+    p.tile_start[l + 1] = p.tile_start[l] + (p.dims[l] / 32) * (p.dims[l + 1] / 32);
+    p.bias_start[l + 1] = p.bias_start[l] + p.dims[l + 1] / 32;
+  }
+  for (int l = p.nl + 1; l <= kMaxHidden; ++l) {
+    p.tile_start[l] = p.tile_start[p.nl];
+    p.bias_start[l] = p.bias_start[p.nl];
+  }
+  return p.tile_start[p.nl] + p.bias_start[p.nl] + 1;
+}
+
+}  // namespace rocfm

@@ -27,6 +27,9 @@ void launch_dense_apply(DenseApplyParams p, hipStream_t stream);
 
 // emb_update.hip (declared in kernels/emb_update.h)
 
+// step_tail.hip: mlp_wgrad + emb_rows_update as workgroup roles of one launch
+void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream);
+
 // sort.hip
 size_t sort_pairs_temp_bytes(int n, int end_bit);
 void sort_pairs_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_out,

@@ -490,9 +490,10 @@ class FusedDeepFM:
         # the side chain is forked first: in the captured graph it then gets its own hardware
         # queue and starts at once (forked later it was serialised behind the embedding update)
         side = self._fork_next(p)
-        aux = self._enqueue_rows_then_fork_wgrad(p)
-        self._enqueue_emb_update(p)
-        self._join(aux)
+        s = self.stream_ptr
+        self.H.deepfm_rows(self.rows_params[p], s)
+        self._tail(self.wgrad_params[p], self.emb_params[p],
+                   self.emb_dense_params[p] if self.embedding_update == "exact" else None, s)
         self._join(side)
 
     def _enqueue_pipelined(self, S: int) -> None:
@@ -603,11 +604,19 @@ class FusedDeepFM:
         for k in range(S):
             rows, wp, _, ep, ed = self.m_params[q][k]
             H.deepfm_rows(rows, s)
+            self._tail(wp, ep, ed, s)
+        main.wait_stream(side)
+
+    def _tail(self, wp, ep, ed, s: int) -> None:
+        """MLP weight gradients + embedding update: one launch (step_tail.hip) when the rows fit."""
+        H = self.H
+        if self.Kp <= 32:
+            H.step_tail(wp, ep, s)
+        else:
             H.mlp_wgrad(wp, s)
             H.emb_rows_update(ep, s)
-            if ed is not None:
-                H.emb_dense_update(ed, s)
-        main.wait_stream(side)
+        if ed is not None:
+            H.emb_dense_update(ed, s)
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         if getattr(self, "mS", None) is None or self.mS != Smax or getattr(self, "_m_pool", None) is not self.pool_ids:
