@@ -66,6 +66,20 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// MFMA B-fragment swizzle of a row-major bf16 matrix [R][C] (R % 16 == 0, C % 32 == 0): the
+// 16-row × 32-column block (nt, u) is stored as 64 lanes × 8 contiguous elements in the order the
+// 16x16x32 B operand wants them (lane l: row 16·nt + (l & 15), columns 32·u + 8·(l >> 4) .. +7),
+// so one fragment load is a 1 KiB contiguous read (3.1× faster per workgroup than the strided
+// row-major pattern, tools/frag_probe.py).
+__host__ __device__ __forceinline__ size_t frag_swz(int r, int c, int C) {
+  const int nt = r >> 4, rl = r & 15, u = c >> 5, cc = c & 31;
+  return ((size_t)(nt * (C >> 5) + u) * 64 + rl + 16 * (cc >> 3)) * 8 + (cc & 7);
+}
+// Offset (elements) of fragment (nt, u) for this lane in a frag_swz matrix with C columns.
+__device__ __forceinline__ size_t frag_at(int nt, int u, int C, int lane) {
+  return ((size_t)(nt * (C >> 5) + u) * 64 + lane) * 8;
+}
 __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
 
 // Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)) and

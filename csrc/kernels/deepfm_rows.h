@@ -29,6 +29,8 @@ struct RowsParams {
   const float* b_out;  // [1]
   const uint16_t* WT[kMaxHidden];  // layer l: [dims[l+1]][dims[l]] bf16 (forward B operand)
   const uint16_t* Wb[kMaxHidden];  // layer l: [dims[l]][dims[l+1]] bf16 (backward B operand)
+  const uint16_t* WTs[kMaxHidden];  // frag_swz copies of WT / Wb (compile-time-shape kernels load these)
+  const uint16_t* Wbs[kMaxHidden];
   const float* bias[kMaxHidden];   // layer l: [dims[l+1]]
   float keep[kMaxHidden];
   int dims[kMaxHidden + 1];  // dims[0] = round_up(F*K, 32); dims[l>0] = hidden width padded to 32
@@ -48,6 +50,8 @@ struct RowsParams {
   RowsLds lds;
   unsigned long long* stamps;  // diagnostic (nullable)
   int force_generic;           // 1: never use a compile-time-shape instantiation (tests)
+  int ablate;                  // diagnostics only (results invalid): bit0 skip h0ᵀ stores, bit1 skip
+                               // the FM loop, bit2 skip the phase-B weight prefetch
 };
 
 struct WgradParams {
@@ -63,6 +67,8 @@ struct WgradParams {
   int offW[kMaxHidden], offb[kMaxHidden], off_wout, off_bout, off_fmb;
   uint16_t* WT[kMaxHidden];
   uint16_t* Wb[kMaxHidden];
+  uint16_t* WTs[kMaxHidden];  // frag_swz copies (nullable): WT as [Dout][Din], Wb as [Din][Dout]
+  uint16_t* Wbs[kMaxHidden];
   int tile_start[kMaxHidden + 1];  // prefix sums of 32×32 tiles per layer
   int bias_start[kMaxHidden + 1];  // prefix sums of 32-column bias blocks per layer
   int fuse_opt;
@@ -83,6 +89,8 @@ struct DenseApplyParams {
   int offW[kMaxHidden];
   uint16_t* WT[kMaxHidden];
   uint16_t* Wb[kMaxHidden];
+  uint16_t* WTs[kMaxHidden];  // frag_swz copies (nullable)
+  uint16_t* Wbs[kMaxHidden];
   int apply;
   OptParams opt;
   const int64_t* step;

@@ -115,9 +115,17 @@ struct CtShape {
 
 }  // namespace
 
+// Diagnostic phase stamps kept in LDS and written out once at the end, so that recording them
+// adds no global store (and no vmcnt wait) inside the measured phases.
+#define ROWS_STAMP(i)                                                                             \
+  do {                                                                                            \
+    if (p.stamps != nullptr && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime();   \
+  } while (0)
+
 template <int KP4, class SH>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ unsigned long long s_stamp[16];
   const SH sh(p);
   const RowsLds& L = p.lds;
   int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
@@ -138,17 +146,14 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const int Bp = p.Bp;
   const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  ROCFM_STAMP(p.stamps, 0);
+  ROWS_STAMP(0);
 
   // ---- static shapes: prefetch the forward layer-0 weight fragments at kernel entry --------------
   bf16x8 fw0[SH::KSF0];
   if constexpr (SH::kStatic) {
-    const bool own = wave < sh.dim(1) / 16;
-    const uint16_t* bp = p.WT[0] + (size_t)(min(wave, sh.dim(1) / 16 - 1) * 16 + (lane & 15)) * sh.dim(0) +
-                         8 * (lane >> 4);
+    const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-    for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(bp + 32 * u);
-    (void)own;
+    for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
   }
   const uint32_t step = p.step ? (uint32_t)(*p.step) : 0u;
 
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
   lds_barrier();
-  ROCFM_STAMP(p.stamps, 1);
+  ROWS_STAMP(1);
 
   // ---- phase A: gather rows, e = V·x (f32 scratch), h0 = bf16(e), w·x ---------------------------
   {
@@ -211,10 +216,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   }
   lds_barrier();
-  ROCFM_STAMP(p.stamps, 2);
+  ROWS_STAMP(2);
 
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
-  {
+  if (!(p.ablate & 2)) {
     const int r = t >> 5, q = t & 31;
     float cterm = 0.f, yw = 0.f;
     for (int k = q; k < K; k += 32) {
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
     if (q == 0) s_ylin[r] = s_prm[L.prm_fmb] + yw + 0.5f * cterm;
   }
-  if (p.train) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
+  if (p.train && !(p.ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
     for (int it = t; it < D0p * 2; it += kRowThreads) {
@@ -252,39 +257,34 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
   bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
   bf16x8 bw0[SH::NJB0][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
-  if constexpr (SH::kStatic) {
+  if constexpr (SH::kStatic) if (!(p.ablate & 4)) {
     if constexpr (SH::nl >= 2) {
-      const uint16_t* bp = p.WT[1] + (size_t)(min(wave, sh.dim(2) / 16 - 1) * 16 + (lane & 15)) * sh.dim(1) +
-                           8 * (lane >> 4);
+      const int nt = min(wave, sh.dim(2) / 16 - 1);
 #pragma unroll
-      for (int u = 0; u < SH::KSF1; ++u) fw1[u] = ld_frag(bp + 32 * u);
+      for (int u = 0; u < SH::KSF1; ++u) fw1[u] = ld_frag(p.WTs[1] + frag_at(nt, u, sh.dim(1), lane));
     }
     if constexpr (SH::nl >= 3) {
-      const uint16_t* bp = p.WT[2] + (size_t)(min(wave, sh.dim(3) / 16 - 1) * 16 + (lane & 15)) * sh.dim(2) +
-                           8 * (lane >> 4);
+      const int nt = min(wave, sh.dim(3) / 16 - 1);
 #pragma unroll
-      for (int u = 0; u < SH::KSF2; ++u) fw2[u] = ld_frag(bp + 32 * u);
+      for (int u = 0; u < SH::KSF2; ++u) fw2[u] = ld_frag(p.WTs[2] + frag_at(nt, u, sh.dim(2), lane));
     }
     if (p.train) {
       // backward of layer 0: dh0 tiles w + 8j of dims[0]/16, k = dims[1]
 #pragma unroll
       for (int j = 0; j < SH::NJB0; ++j) {
         const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
-        const uint16_t* bp = p.Wb[0] + (size_t)(nt * 16 + (lane & 15)) * sh.dim(1) + 8 * (lane >> 4);
 #pragma unroll
-        for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(bp + 32 * u);
+        for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
       }
       if constexpr (SH::nl >= 2) {
-        const uint16_t* bp = p.Wb[1] + (size_t)(min(wave, sh.dim(1) / 16 - 1) * 16 + (lane & 15)) * sh.dim(2) +
-                             8 * (lane >> 4);
+        const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-        for (int u = 0; u < SH::KSB1; ++u) bw1[u] = ld_frag(bp + 32 * u);
+        for (int u = 0; u < SH::KSB1; ++u) bw1[u] = ld_frag(p.Wbs[1] + frag_at(nt, u, sh.dim(2), lane));
       }
       if constexpr (SH::nl >= 3) {
-        const uint16_t* bp = p.Wb[2] + (size_t)(min(wave, sh.dim(2) / 16 - 1) * 16 + (lane & 15)) * sh.dim(3) +
-                             8 * (lane >> 4);
+        const int nt = min(wave, sh.dim(2) / 16 - 1);
 #pragma unroll
-        for (int u = 0; u < SH::KSB2; ++u) bw2[u] = ld_frag(bp + 32 * u);
+        for (int u = 0; u < SH::KSB2; ++u) bw2[u] = ld_frag(p.Wbs[2] + frag_at(nt, u, sh.dim(3), lane));
       }
     }
   }
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const bool drop = p.train && keep < 1.f;
     const float inv_keep = 1.f / keep;
     lds_barrier();  // previous layer's tile (and phase A/B) complete
-    ROCFM_STAMP(p.stamps, 3 + l);
+    ROWS_STAMP(3 + l);
     const int ntiles = Dout >> 4;
     for (int nt = wave; nt < ntiles; nt += kWaves) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   lds_barrier();
 
-  ROCFM_STAMP(p.stamps, 9);
+  ROWS_STAMP(9);
   // ---- phase D: output layer + loss head (wave 0) ----------------------------------------------
   if (wave == 0) {
     const int Dn = sh.dim(NL);
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
   for (int a = NL; a >= 1; --a) {
     lds_barrier();
-    if (a == NL) ROCFM_STAMP(p.stamps, 10);
+    if (a == NL) ROWS_STAMP(10);
     const int li = a - 1, Dout = sh.dim(a), Din = sh.dim(li);
     const int ntiles = Din >> 4;
     constexpr int NJ = SH::kStatic ? (SH::NJB0 > 1 ? SH::NJB0 : 1) : 4;
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     dz_nxt = tmp;
   }
   lds_barrier();
-  ROCFM_STAMP(p.stamps, 11);
+  ROWS_STAMP(11);
 
   // ---- phase F: FM backward → per-lookup gradient rows -----------------------------------------
   for (int base = 0; base < nitemsF; base += kRowThreads * 4) {
@@ -510,7 +510,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   }
   lds_barrier();
-  ROCFM_STAMP(p.stamps, 12);
+  ROWS_STAMP(12);
+  if (p.stamps != nullptr) {
+    lds_barrier();
+    if (t < 13) p.stamps[blockIdx.x * 16 + t] = s_stamp[t];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -565,11 +569,16 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
 template <int KP4, class SH>
 static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   static bool attr_set = false;
-  if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
+  static int max_dyn = 0;
+  if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
+    hipFuncAttributes fa{};
+    ROCFM_HIP_CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>)));
+    max_dyn = 160 * 1024 - (int)fa.sharedSizeBytes;
     ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn));
     attr_set = true;
   }
+  ROCFM_REQUIRE(p.lds.total <= max_dyn, "deepfm_rows: LDS layout exceeds the 160 KiB per workgroup");
   hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
                      p);
 }
@@ -582,6 +591,8 @@ static bool try_static(const RowsParams& p, hipStream_t stream) {
   if (p.F != F || p.K != K || p.nl != nl || p.dims[1] != D1 || (nl >= 2 && p.dims[2] != D2) ||
       (nl >= 3 && p.dims[3] != D3))
     return false;
+  for (int l = 0; l < nl; ++l)
+    if (!p.WTs[l] || !p.Wbs[l]) return false;  // the static kernels load the frag_swz weight copies
   constexpr int KP4 = (K + 1 + 3) / 4;
   launch_rows_t<KP4, CtShape<F, K, D1, D2, D3>>(p, stream);
   return true;

@@ -47,6 +47,10 @@ __global__ __launch_bounds__(256) void dense_apply_kernel(const DenseApplyParams
         const uint16_t h = f2bf(w);
         p.WT[l][(size_t)o * p.dims[l] + i] = h;
         p.Wb[l][(size_t)i * p.dims[l + 1] + o] = h;
+        if (p.WTs[l]) {
+          p.WTs[l][frag_swz(o, i, p.dims[l])] = h;
+          p.Wbs[l][frag_swz(i, o, p.dims[l + 1])] = h;
+        }
       }
     }
   }

@@ -102,7 +102,12 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
         if (p.s0) p.s0[idx[e]] = a[e];
         if (p.s1) p.s1[idx[e]] = b[e];
         const uint16_t hw = f2bf(w[e]);
-        p.Wb[li][(size_t)(ti * 32 + il[e]) * Dout + to * 32 + ol[e]] = hw;  // 64-B runs along o
+        const int ii = ti * 32 + il[e], oo = to * 32 + ol[e];
+        p.Wb[li][(size_t)ii * Dout + oo] = hw;  // 64-B runs along o
+        if (p.WTs[li]) {
+          p.WTs[li][frag_swz(oo, ii, Din)] = hw;
+          p.Wbs[li][frag_swz(ii, oo, Dout)] = hw;
+        }
         s_T[ol[e] * 34 + il[e]] = hw;
       }
       __syncthreads();

@@ -138,6 +138,9 @@ class FusedDeepFM:
         self.dense_slots = init_slots(hp, self.dense)
         self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
+        # MFMA-fragment-swizzled copies (common.h frag_swz): what the compile-time-shape row kernel loads
+        self.WTs = [torch.zeros_like(w) for w in self.WT]
+        self.Wbs = [torch.zeros_like(w) for w in self.Wb]
         self.steps = torch.zeros(2, dtype=torch.int64, device=dev)   # global_step, by parity
         self.cursor = torch.zeros(2, dtype=torch.int64, device=dev)  # pool batch index, by parity
         self.lrt = torch.zeros(2, dtype=torch.float32, device=dev)     # per-step lr_t, by parity
@@ -225,9 +228,10 @@ class FusedDeepFM:
         for l in range(L.nl):
             rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),
                          float(self.spec.keep_probs[l]))
+            rp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
         for a in range(L.nl + 1):
             rp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
-        if rp.lds_bytes() > 160 * 1024:
+        if rp.lds_bytes() > 160 * 1024 - 256:  # 256 B: the kernel's static LDS (diagnostic stamps)
             raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
         return rp
 
@@ -252,6 +256,7 @@ class FusedDeepFM:
             wp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
         for l in range(L.nl):
             wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+            wp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
         dp = H.DenseApplyParams()
         dp.params = self.dense.data_ptr()
         dp.grads = self.dense_grads_flat.data_ptr()
@@ -262,6 +267,7 @@ class FusedDeepFM:
         dp.set_dims(L.dims)
         for l in range(L.nl):
             dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
+            dp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
         ep = H.EmbUpdateParams()
         ep.skeys, ep.svals = skeys_ptr, svals_ptr
         ep.n = self.n_lookup

@@ -49,10 +49,14 @@ def main():
         eng.rows_params[p].stamps = s_rows.data_ptr()
         eng.wgrad_params[p].stamps = s_wg.data_ptr()
         eng.emb_params[p].stamps = s_emb.data_ptr()
+    abl = int(os.environ.get("ABLATE", "0"))
+    for p in range(2):
+        eng.rows_params[p].ablate = abl
     for _ in range(3):
         s_rows.zero_(); s_wg.zero_(); s_emb.zero_()
         eng.train_step()
         torch.cuda.synchronize()
+    print("ablate", abl)
     report("deepfm_rows", s_rows.view(-1, 16).cpu(), [0, 1, 2, 3, 4, 5, 9, 10, 11, 12],
            ["0 ids/vals stage", "A gather+e+h0", "B FM + h0T store", "C layer0 fwd", "C layer1 fwd",
             "C layer2 fwd", "D head + dz_L", "E backward (3 GEMMs)", "F FM bwd + contrib"])
