@@ -148,30 +148,64 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   ROWS_STAMP(0);
 
-  // ---- static shapes: prefetch the forward layer-0 weight fragments at kernel entry --------------
+  // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
+  // The ids are the head of the kernel's latency chain (ids → gathered rows): their loads are
+  // issued first; the layer-0 weight prefetch is issued behind them and lands during phase A.
   bf16x8 fw0[SH::KSF0];
   if constexpr (SH::kStatic) {
+    constexpr int kItems = (kRowTile * SH::F + kRowThreads - 1) / kRowThreads;
+    int32_t idr[kItems];
+    float vlr[kItems];
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      const int i = t + u * kRowThreads;
+      const bool valid = i < kRowTile * F && row0 + fdiv(i, magicF) < p.B;
+      idr[u] = valid ? p.ids[(size_t)row0 * F + i] : 0;
+      vlr[u] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
+    }
+    float br[SH::nl];
+#pragma unroll
+    for (int l = 0; l < SH::nl; ++l) br[l] = t < sh.dim(l + 1) ? p.bias[l][t] : 0.f;
+    const float wo = t < sh.dim(SH::nl) ? p.w_out[t] : 0.f;
+    const float lab = (t < kRowTile && row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
+    const float bo = t == 0 ? *p.b_out : 0.f, fb = t == 0 ? *p.fm_bias : 0.f;
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
     for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      const int i = t + u * kRowThreads;
+      if (i < kRowTile * F) {
+        s_ids[i] = idr[u];
+        s_vals[i] = vlr[u];
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < SH::nl; ++l)
+      if (t < sh.dim(l + 1)) s_prm[L.prm_bias[l] + t] = br[l];
+    if (t < sh.dim(SH::nl)) s_prm[L.prm_wout + t] = wo;
+    if (t == 0) {
+      s_prm[L.prm_bout] = bo;
+      s_prm[L.prm_fmb] = fb;
+    }
+    if (t < kRowTile) s_prm[L.prm_lab + t] = lab;
+  } else {
+    for (int i = t; i < kRowTile * F; i += kRowThreads) {
+      const bool valid = row0 + fdiv(i, magicF) < p.B;
+      s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
+      s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+      for (int c = t; c < sh.dim(l + 1); c += kRowThreads) s_prm[L.prm_bias[l] + c] = p.bias[l][c];
+    for (int c = t; c < sh.dim(NL); c += kRowThreads) s_prm[L.prm_wout + c] = p.w_out[c];
+    if (t == 0) {
+      s_prm[L.prm_bout] = *p.b_out;
+      s_prm[L.prm_fmb] = *p.fm_bias;
+    }
+    if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
   }
   const uint32_t step = p.step ? (uint32_t)(*p.step) : 0u;
-
-  // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
-  for (int i = t; i < kRowTile * F; i += kRowThreads) {
-    const bool valid = row0 + fdiv(i, magicF) < p.B;
-    s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
-    s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
-  }
-#pragma unroll
-  for (int l = 0; l < NL; ++l)
-    for (int c = t; c < sh.dim(l + 1); c += kRowThreads) s_prm[L.prm_bias[l] + c] = p.bias[l][c];
-  for (int c = t; c < sh.dim(NL); c += kRowThreads) s_prm[L.prm_wout + c] = p.w_out[c];
-  if (t == 0) {
-    s_prm[L.prm_bout] = *p.b_out;
-    s_prm[L.prm_fmb] = *p.fm_bias;
-  }
-  if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
   lds_barrier();
   ROWS_STAMP(1);
 
