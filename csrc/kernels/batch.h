@@ -57,4 +57,16 @@ struct FetchMultiParams {
 
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream);
 
+// After the multi-batch sort: each lookup's position in its batch's sorted order (the row kernel
+// writes its gradient row there, so the embedding update reads rows contiguously) and, per
+// batch and `chunk`-entry workgroup chunk, the end of the run holding the chunk's last entry.
+struct SortAuxParams {
+  const uint32_t* skeys;  // [S·n] sorted (batch << id_bits | id)
+  const uint32_t* svals;  // [S·n] global lookup index (batch · n + lookup)
+  int n, S, chunk;
+  int32_t* pos;           // [S·n] pos[batch · n + lookup] = sorted position within the batch
+  int32_t* chunk_end;     // [S][ceil(n / chunk)] (nullable)
+};
+void launch_sort_aux(const SortAuxParams& p, hipStream_t stream);
+
 }  // namespace rocfm

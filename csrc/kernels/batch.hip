@@ -81,6 +81,37 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
   }
 }
 
+__global__ __launch_bounds__(256) void sort_aux_kernel(const SortAuxParams p) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)p.S * p.n;
+  if (i < total) {
+    const int k = (int)(i / p.n);
+    p.pos[p.svals[i]] = (int32_t)(i - (long long)k * p.n);
+  }
+  if (p.chunk_end) {
+    const int nch = (p.n + p.chunk - 1) / p.chunk;
+    if (i < (long long)p.S * nch) {
+      const int k = (int)(i / nch), c = (int)(i - (long long)k * nch);
+      const uint32_t* kb = p.skeys + (size_t)k * p.n;
+      const int last = min((c + 1) * p.chunk, p.n) - 1;
+      const uint32_t key = kb[last];
+      int lo = last + 1, hi = p.n;  // first position after `last` whose key differs (sorted)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (kb[mid] == key) lo = mid + 1; else hi = mid;
+      }
+      p.chunk_end[i] = lo;
+    }
+  }
+}
+
+void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.n > 0 && p.S > 0 && p.chunk > 0, "sort_aux: bad sizes");
+  const long long total = std::max<long long>((long long)p.S * p.n, (long long)p.S * ((p.n + p.chunk - 1) / p.chunk));
+  hipLaunchKernelGGL(sort_aux_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.pool_batches > 0 && p.S > 0, "fetch_multi: empty pool / S");
   ROCFM_REQUIRE(p.cur_dst != p.cur_src && p.step_dst != p.step_src, "fetch_multi: counters must differ");

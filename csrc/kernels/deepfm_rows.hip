@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const RowsLds& L = p.lds;
   int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
   float* s_vals = reinterpret_cast<float*>(smem + L.vals);
+  int32_t* s_pos = reinterpret_cast<int32_t*>(smem + L.pos);
   float* s_wx = reinterpret_cast<float*>(smem + L.wx);
   float* s_S = reinterpret_cast<float*>(smem + L.S);
   float* s_ylin = reinterpret_cast<float*>(smem + L.ylin);
@@ -163,6 +164,13 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       idr[u] = valid ? p.ids[(size_t)row0 * F + i] : 0;
       vlr[u] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
     }
+    int32_t psr[kItems];
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      const int i = t + u * kRowThreads;
+      const bool valid = p.contrib_pos && i < kRowTile * F && row0 + fdiv(i, magicF) < p.B;
+      psr[u] = valid ? p.contrib_pos[(size_t)row0 * F + i] : (int32_t)((size_t)row0 * F + i);
+    }
     float br[SH::nl];
 #pragma unroll
     for (int l = 0; l < SH::nl; ++l) br[l] = t < sh.dim(l + 1) ? p.bias[l][t] : 0.f;
@@ -178,6 +186,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       if (i < kRowTile * F) {
         s_ids[i] = idr[u];
         s_vals[i] = vlr[u];
+        s_pos[i] = psr[u];
       }
     }
 #pragma unroll
@@ -194,6 +203,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       const bool valid = row0 + fdiv(i, magicF) < p.B;
       s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
       s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
+      s_pos[i] = (valid && p.contrib_pos) ? p.contrib_pos[(size_t)row0 * F + i] : (int32_t)((size_t)row0 * F + i);
     }
 #pragma unroll
     for (int l = 0; l < NL; ++l)
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const int k = c4 * 4 + c;
         o[c] = (k < K) ? x * (g * (S[k] - vv[c] * x) + dh[k]) : ((k == K) ? g * x : 0.f);
       }
-      reinterpret_cast<float4*>(p.contrib + ((size_t)(row0 + r) * F + f) * Kp)[c4] =
+      reinterpret_cast<float4*>(p.contrib + (size_t)s_pos[r * F + f] * Kp)[c4] =
           make_float4(o[0], o[1], o[2], o[3]);
     }
   }
@@ -565,6 +575,7 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
   L.ids = take(kRowTile * F * 4);
   L.vals = take(kRowTile * F * 4);
   L.wx = take(kRowTile * F * 4);
+  L.pos = take(kRowTile * F * 4);
   L.S = take(kRowTile * K * 4);
   L.ylin = take(kRowTile * 4);
   L.g = take(kRowTile * 4);

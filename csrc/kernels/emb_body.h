@@ -46,6 +46,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const int cend = min(c0 + kChunk, p.n);
   const int i = c0 + t;
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
   ROCFM_STAMP(p.stamps, 0);
 
   // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
@@ -56,7 +57,8 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     key = p.skeys[i];
     head = (i == 0) || (p.skeys[i - 1] != key);
     const bool skip = p.max_key && key >= p.max_key;
-    const float4* src = contrib_row4(p, p.svals[i] - p.val_base);
+    const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)i * p.Kp)
+                                         : contrib_row4(p, p.svals[i] - p.val_base);
 #pragma unroll
     for (int u = 0; u < KP4; ++u) v[u] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : src[u];
   } else {
@@ -106,6 +108,10 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     const bool sentinel = p.max_key && lk >= p.max_key;  // sentinel padding sorts last: runs to n
     int pos = sentinel ? p.n : cend;
     if (t == 0) s_last_end = p.n;
+    if (p.chunk_end != nullptr && !sentinel) {  // precomputed by the side chain (sort_aux)
+      pos = p.n;
+      if (t == 0) s_last_end = ce_pre;
+    }
     __syncthreads();
     while (pos < p.n) {
       const int j = pos + t;
@@ -142,7 +148,8 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       const int j = k0 + t;
       float4 w[KP4];
       if (j < last_end) {
-        const float4* src = contrib_row4(p, p.svals[j] - p.val_base);
+        const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)j * p.Kp)
+                                             : contrib_row4(p, p.svals[j] - p.val_base);
 #pragma unroll
         for (int u = 0; u < KP4; ++u) w[u] = src[u];
       } else {

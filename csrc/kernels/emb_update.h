@@ -32,6 +32,8 @@ struct EmbUpdateParams {
   int out_cap;         // mode 2: capacity of out_keys/out_rows (rows past it are dropped, count kept)
   unsigned long long* stamps;  // diagnostic (nullable)
   uint32_t val_base;   // subtracted from svals (a batch's segment of a multi-batch sort)
+  int sorted_contrib;  // 1: contrib rows are already in sorted order (row i ↔ sorted entry i; svals unused)
+  const int32_t* chunk_end;  // nullable: per workgroup chunk, end of the run holding its last entry
 };
 
 struct EmbDenseParams {

@@ -552,6 +552,12 @@ class FusedDeepFM:
         self.m_sv = torch.zeros(2, Smax * n, **i32)
         self.m_temp = torch.zeros(max(H.sort_pairs_temp_bytes(Smax * n, self.m_bits), 16), dtype=torch.uint8,
                                   device=dev)
+        # each lookup's position in its batch's sorted order (the row kernel writes its gradient row
+        # there) and the per-chunk run ends of the fused step tail (sort_aux, side chain)
+        self.m_pos = torch.zeros(2, Smax * n, **i32)
+        self.m_chunk = self.H.tail_chunk()
+        self.m_nch = (n + self.m_chunk - 1) // self.m_chunk
+        self.m_cend = torch.zeros(2, Smax * self.m_nch, **i32)
         self.m_steps = torch.zeros(2, Smax, dtype=torch.int64, device=dev)
         self.m_lrt = torch.zeros(2, Smax, dtype=torch.float32, device=dev)
         self.m_cur = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -561,6 +567,13 @@ class FusedDeepFM:
                                                self.m_sk[q, k * n:].data_ptr(), self.m_sv[q, k * n:].data_ptr(),
                                                val_base=k * n, id_offset=k << idbits)
                           for k in range(Smax)] for q in range(2)]
+        for q in range(2):
+            for k in range(Smax):
+                rows, _, _, ep, _ = self.m_params[q][k]
+                rows.contrib_pos = self.m_pos[q, k * n:].data_ptr()
+                ep.sorted_contrib = 1
+                if self.Kp <= 32:  # the fused tail's 512-entry chunks
+                    ep.chunk_end = self.m_cend[q, k * self.m_nch:].data_ptr()
         self._m_graphs = {}
         self._m_primed = False
         self._m_warm = 0
@@ -590,6 +603,11 @@ class FusedDeepFM:
         H.sort_pairs_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys.data_ptr(),
                           self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
                           self.m_bits, stream.cuda_stream)
+        a = H.SortAuxParams()
+        a.skeys, a.svals = self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr()
+        a.n, a.S, a.chunk = self.n_lookup, self.mS, self.m_chunk
+        a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
+        H.sort_aux(a, stream.cuda_stream)
 
     def _prime_multi(self) -> None:
         base = 0 if self._ring else getattr(self, "_start_batch", 0)
