@@ -219,7 +219,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         const int slot = s_out_base + r;
         if (slot < p.out_cap) {
           p.out_rows[(size_t)slot * Kp + col] = g[u];
-          if (col == 0) p.out_keys[slot] = kk[u];
+          if (col == 0) p.out_keys[slot] = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
         }
       } else if (p.mode == 1) {
         p.dense_grad[idx[u]] = g[u];

@@ -25,7 +25,6 @@ __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradPara
 
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= 32 && e.K1 <= e.Kp, "step_tail: Kp must be a multiple of 4 and <= 32");
-  ROCFM_REQUIRE(e.mode != 2, "step_tail: export mode needs a zeroed counter; use emb_rows_update");
   if (e.id_stride <= 0) e.id_stride = 1;
   const int n_wg = wgrad_prepare(w);
   const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;

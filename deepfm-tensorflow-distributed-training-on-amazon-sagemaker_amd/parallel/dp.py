@@ -322,6 +322,7 @@ class FusedDataParallel:
 
     def train_step(self) -> None:
         e = self.eng
+        e._m_primed = False
         if not e._primed:
             e.prime()
         p = e._i % 2
@@ -335,31 +336,111 @@ class FusedDataParallel:
         e._i += 1
         self._after_steps(e._i - 1, e._i)
 
-    def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
-        """``n`` steps from the attached pool; with capturable collectives (RCCL), full step pairs
-        are replayed from one multi-step graph (``steps_per_graph`` steps per launch)."""
+    # ---- multi-step graphs (pool mode, capturable collectives) -----------------------------------
+    # The single-GPU pipeline of FusedDeepFM (serial main stream per step, one batched fetch+sort
+    # side chain per graph, sorted-order gradient rows) with the step's exchange captured inline:
+    #   dp       rows → tail(wgrad grads ‖ export Σrows) → all_gather → dense_apply(Σ ranks) → merge
+    #   dense_dp rows → tail(wgrad grads ‖ Σrows → dense table grad) → all_reduce → dense_apply
+    #            → emb_dense_update
+    def _build_multi_dp(self, Smax: int) -> None:
+        e, H = self.eng, self.eng.H
+        e._build_multi(Smax)
+        e._m_pool = e.pool_ids
+        S_, n = e.mS, e.n_lookup
+        self.m_dp = []
+        for q in range(2):
+            row = []
+            for k in range(S_):
+                rows, wp, da, ep, ed = e.m_params[q][k]
+                wp.grads = e.dense_grads_flat.data_ptr()
+                da.apply, da.grad_scale = 1, 1.0 / self.world
+                if self.mode == "dense_dp":
+                    da.grads = e.dense_grads_flat.data_ptr()
+                    ed.grad_scale = 1.0 / self.world
+                    row.append((rows, wp, ep, da, ed, None))
+                    continue
+                da.grads, da.nseg, da.seg_stride = self.recv.data_ptr(), self.world, self.S
+                ex = H.EmbUpdateParams()  # export: compacted (id, Σ grad row) into the send buffer
+                ex.skeys, ex.svals, ex.n = ep.skeys, ep.svals, n
+                ex.val_base, ex.id_offset, ex.sorted_contrib, ex.chunk_end = ep.val_base, ep.id_offset, 1, ep.chunk_end
+                ex.contrib, ex.K1, ex.Kp = e.contrib.data_ptr(), e.K1, e.Kp
+                ex.opt, ex.step = ep.opt, ep.step
+                ex.mode, ex.grad_scale = 2, 1.0
+                ex.out_keys = self.send[self.off_keys:].data_ptr()
+                ex.out_rows = self.send[self.off_rows:].data_ptr()
+                ex.out_count = self.send[self.off_cnt:].data_ptr()
+                ex.out_cap = self.cap
+                mg = H.MergeParams()
+                src = self.merge_params[0]
+                for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
+                          "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
+                          "overflow"):
+                    setattr(mg, f, getattr(src, f))
+                mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
+                row.append((rows, wp, ex, da, None, mg))
+            self.m_dp.append(row)
+        self._m_dp_S = Smax
+
+    def _enqueue_multi_dp(self, q: int, S: int) -> None:
+        e, H = self.eng, self.eng.H
+        main = torch.cuda.current_stream(self.device)
+        side = e.sort_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            e._prepare_multi(q, S, side)
+        s = main.cuda_stream
+        for k in range(S):
+            rows, wp, ep, da, ed, mg = self.m_dp[q][k]
+            if self.mode == "dp":
+                self.send_count.zero_()
+            H.deepfm_rows(rows, s)
+            e._tail(wp, ep, None, s)
+            self._exchange()
+            H.dense_apply(da, s)
+            if self.mode == "dp":
+                H.merge_scatter(mg, s)
+                H.merge_apply(mg, s)
+            else:
+                H.emb_dense_update(ed, s)
+        main.wait_stream(side)
+
+    def _train_steps_multi(self, n: int, Smax: int) -> None:
         e = self.eng
-        S = max(2, steps_per_graph // 2 * 2)
+        if getattr(self, "_m_dp_S", None) != Smax or getattr(e, "_m_pool", None) is not e.pool_ids:
+            self._build_multi_dp(Smax)
+        if not e._m_primed:
+            e._prime_multi()
         while n > 0:
-            if (self.graph_collectives and self.use_graph and self._warm >= 4 and e._primed and n >= S
-                    and e._i % 2 == 0 and not e._ring):
-                key = ("multi", S)
+            S = min(n, e.mS)
+            q = e._mq
+            if e._m_warm < 1:
+                self._enqueue_multi_dp(q, S)  # first run eager (code objects load outside capture)
+            else:
+                key = ("mdp", q, S)
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
                     torch.cuda.synchronize(self.device)
                     with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                        for k in range(S):
-                            self._step_body(k % 2)
+                        self._enqueue_multi_dp(q, S)
                     self._graphs[key] = g
                 g.replay()
-                e._i += S
-                self._warm += S
-                n -= S
-                self._after_steps(e._i - S, e._i)
-            else:
-                self.train_step()
-                n -= 1
+            e._m_warm += 1
+            e._mq ^= 1
+            e._i += S
+            n -= S
+            self._after_steps(e._i - S, e._i)
+        e._primed = False
+
+    def train_steps(self, n: int, steps_per_graph: int = 16) -> None:
+        """``n`` steps from the attached pool.  With capturable collectives (RCCL) the steps are
+        replayed from multi-step graphs (``steps_per_graph`` steps each, exchange included)."""
+        e = self.eng
+        if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
+            self._train_steps_multi(n, steps_per_graph)
+            return
+        for _ in range(n):
+            self.train_step()
 
     def close(self) -> None:
         """Release the captured graphs (required before destroy_process_group when they hold

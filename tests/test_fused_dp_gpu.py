@@ -80,3 +80,31 @@ def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode):
     torch.cuda.synchronize()
     torch.testing.assert_close(dp["dense"], single.dense.cpu(), rtol=2e-3, atol=2e-5)
     torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=2e-5)
+
+
+@pytest.mark.parametrize("mode", ["dp", "dense_dp"])
+def test_dp_multistep_graphs_world1_equal_single(mode):
+    """Single-process DP (no process group: the exchange is a copy) through the multi-step graph
+    pipeline (export → exchange → merge / dense apply inside the graph) ≡ the single-GPU engine."""
+    from rocfm.models.deepfm import init_params
+    from rocfm.models.fused import FusedDeepFM
+    from rocfm.parallel.dp import FusedDataParallel
+
+    spec, hp = _cfg()
+    upd = "exact" if mode == "dense_dp" else "sparse"
+    batches = _batches(128, 5, 11)
+    pool = [torch.stack([b[i] for b in batches]).cuda() for i in range(3)]
+    dp = FusedDataParallel(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=upd,
+                           mode=mode, use_graph=True)
+    one = FusedDeepFM(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=upd,
+                      use_graph=True)
+    dp.attach_pool(*pool)
+    one.attach_pool(*pool)
+    dp.train_steps(21, 8)
+    one.train_steps(21, 8)
+    torch.cuda.synchronize()
+    assert dp.global_step() == one.global_step() == 21
+    # same math; only fma contraction differs between the merge and the single-GPU update
+    torch.testing.assert_close(dp.emb, one.emb, rtol=2e-3, atol=2e-5)
+    torch.testing.assert_close(dp.dense, one.dense, rtol=2e-3, atol=2e-5)
+    dp.check()
