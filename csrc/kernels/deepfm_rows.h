@@ -51,6 +51,7 @@ struct RowsParams {
   unsigned long long* stamps;  // diagnostic (nullable)
   const int32_t* contrib_pos;  // nullable [B][F]: row of contrib receiving each lookup's gradient
                                // (its position in the sorted lookup order), else row·F + field
+  int32_t* zero_word;          // nullable: set to 0 at kernel start (DP: the export's row counter)
   int force_generic;           // 1: never use a compile-time-shape instantiation (tests)
   int ablate;                  // diagnostics only (results invalid): bit0 skip h0ᵀ stores, bit1 skip
                                // the FM loop, bit2 skip the phase-B weight prefetch

@@ -44,5 +44,7 @@ struct MergeParams {
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);
 void launch_merge_apply(const MergeParams& p, hipStream_t stream);
 void launch_merge_init(const MergeParams& p, hipStream_t stream);  // pos = −1, rep = W
+struct DenseApplyParams;
+void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d, hipStream_t stream);
 
 }  // namespace rocfm

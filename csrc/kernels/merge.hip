@@ -1,5 +1,8 @@
 // Multi-source row-gradient merge by direct addressing — see merge.h.
 #include "merge.h"
+#include "wgrad_body.h"
+
+#include <algorithm>
 
 namespace rocfm {
 namespace {
@@ -21,8 +24,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_init_kernel(MergeParams p
   if (i < p.Vmap) p.rep[i] = p.W;
 }
 
-__global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParams p) {
-  const int i = blockIdx.x * kMergeThreads + threadIdx.x;
+__device__ __forceinline__ void merge_scatter_body(const MergeParams& p, const int bid) {
+  const int i = bid * kMergeThreads + threadIdx.x;
   if (i >= p.W * p.cap) return;
   const int r = i / p.cap, j = i - r * p.cap;
   if (j == 0 && p.overflow && p.counts && p.counts[(size_t)r * p.count_stride] > p.cap) *p.overflow = 1;
@@ -31,6 +34,10 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParam
   const uint32_t row = key / p.key_div;
   p.pos[(size_t)r * p.Vmap + row] = j;
   atomicMin(&p.rep[row], r);
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParams p) {
+  merge_scatter_body(p, blockIdx.x);
 }
 
 // One thread per source entry; only representatives (lowest rank holding the key) do work.
@@ -133,6 +140,17 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
   }
 }
 
+// merge_scatter with the DP MLP optimizer (dense_apply over the gathered rank segments) as extra
+// workgroups of the same launch: the two are independent, the merge_apply that follows needs both.
+__global__ __launch_bounds__(kMergeThreads) void merge_scatter_dense_kernel(MergeParams p, DenseApplyParams d,
+                                                                            int n_scatter, int n_dense) {
+  if ((int)blockIdx.x < n_scatter) {
+    merge_scatter_body(p, blockIdx.x);
+  } else {
+    dense_apply_body(d, blockIdx.x - n_scatter, n_dense);
+  }
+}
+
 template <int KP4>
 void launch_apply_t(const MergeParams& p, hipStream_t stream) {
   const dim3 grid(cdiv(p.W * p.cap, kMergeThreads)), block(kMergeThreads);
@@ -164,6 +182,15 @@ void launch_merge_scatter(const MergeParams& p, hipStream_t stream) {
   if (p.cap <= 0) return;
   hipLaunchKernelGGL(merge_scatter_kernel, dim3(cdiv(p.W * p.cap, kMergeThreads)), dim3(kMergeThreads), 0, stream,
                      p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d, hipStream_t stream) {
+  check(p);
+  const int n_scatter = p.cap > 0 ? cdiv(p.W * p.cap, kMergeThreads) : 0;
+  const int n_dense = std::max(1, std::min(cdiv(d.n, 256), 256));
+  hipLaunchKernelGGL(merge_scatter_dense_kernel, dim3(n_scatter + n_dense), dim3(kMergeThreads), 0, stream, p, d,
+                     n_scatter, n_dense);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

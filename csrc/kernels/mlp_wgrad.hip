@@ -27,33 +27,7 @@ void launch_mlp_wgrad(WgradParams p, hipStream_t stream) {
 // or (apply == 0) just refresh the bf16 weight copies from the f32 masters (init / restore).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dense_apply_kernel(const DenseApplyParams p) {
-  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
-  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < p.n; idx += gridDim.x * 256) {
-    float w = p.params[idx];
-    if (p.apply) {
-      float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
-      float g = p.grads[idx];
-      for (int r = 1; r < p.nseg; ++r) g += p.grads[(size_t)r * p.seg_stride + idx];  // rank order
-      opt_apply(p.opt, st, w, g * p.grad_scale, a, b);
-      p.params[idx] = w;
-      if (p.s0) p.s0[idx] = a;
-      if (p.s1) p.s1[idx] = b;
-    }
-    for (int l = 0; l < p.nl; ++l) {
-      const int sz = p.dims[l] * p.dims[l + 1];
-      if (idx >= p.offW[l] && idx < p.offW[l] + sz) {
-        const int k = idx - p.offW[l];
-        const int i = k / p.dims[l + 1], o = k % p.dims[l + 1];
-        const uint16_t h = f2bf(w);
-        p.WT[l][(size_t)o * p.dims[l] + i] = h;
-        p.Wb[l][(size_t)i * p.dims[l + 1] + o] = h;
-        if (p.WTs[l]) {
-          p.WTs[l][frag_swz(o, i, p.dims[l])] = h;
-          p.Wbs[l][frag_swz(i, o, p.dims[l + 1])] = h;
-        }
-      }
-    }
-  }
+  dense_apply_body(p, blockIdx.x, gridDim.x);
 }
 
 void launch_dense_apply(DenseApplyParams p, hipStream_t stream) {

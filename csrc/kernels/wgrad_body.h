@@ -179,6 +179,39 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
 }
 
 
+// Elementwise optimizer over the flat dense buffer (+ bf16 / swizzled weight refresh), block `bid`
+// of `nblocks` 256-thread blocks (grid-strided).
+__device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, const int bid, const int nblocks) {
+  const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  for (int idx = bid * 256 + (int)threadIdx.x; idx < p.n; idx += nblocks * 256) {
+    float w = p.params[idx];
+    if (p.apply) {
+      float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
+      float g = p.grads[idx];
+      for (int r = 1; r < p.nseg; ++r) g += p.grads[(size_t)r * p.seg_stride + idx];  // rank order
+      opt_apply(p.opt, st, w, g * p.grad_scale, a, b);
+      p.params[idx] = w;
+      if (p.s0) p.s0[idx] = a;
+      if (p.s1) p.s1[idx] = b;
+    }
+    for (int l = 0; l < p.nl; ++l) {
+      const int sz = p.dims[l] * p.dims[l + 1];
+      if (idx >= p.offW[l] && idx < p.offW[l] + sz) {
+        const int k = idx - p.offW[l];
+        const int i = k / p.dims[l + 1], o = k % p.dims[l + 1];
+        const uint16_t h = f2bf(w);
+        p.WT[l][(size_t)o * p.dims[l] + i] = h;
+        p.Wb[l][(size_t)i * p.dims[l + 1] + o] = h;
+        if (p.WTs[l]) {
+          p.WTs[l][frag_swz(o, i, p.dims[l])] = h;
+          p.Wbs[l][frag_swz(i, o, p.dims[l + 1])] = h;
+        }
+      }
+    }
+  }
+}
+
+
 // Fills the per-layer tile / bias workgroup offsets; returns the grid size.
 inline int wgrad_prepare(WgradParams& p) {
   ROCFM_REQUIRE(p.Bp % 128 == 0, "mlp_wgrad: Bp must be a multiple of 128");

@@ -284,16 +284,10 @@ class FusedDataParallel:
             e.H.dense_apply(e.dense_apply_params[p], s)
             e.H.emb_dense_update(e.emb_dense_params[p], s)
             return
-        # MLP: Σ over the gathered rank segments (rank order) + optimizer, on the aux stream,
-        # concurrently with the embedding merge on the main stream
-        main = torch.cuda.current_stream(self.device)
-        aux = e.aux_stream
-        aux.wait_stream(main)
-        with torch.cuda.stream(aux):
-            e.H.dense_apply(e.dense_apply_params[p], aux.cuda_stream)
-        e.H.merge_scatter(self.merge_params[p], s)
+        # MLP: Σ over the gathered rank segments (rank order) + optimizer as extra workgroups of
+        # the row-scatter launch, then the row merge + optimizer
+        e.H.merge_scatter_dense(self.merge_params[p], e.dense_apply_params[p], s)
         e.H.merge_apply(self.merge_params[p], s)
-        e._join(aux)
 
     def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:
@@ -377,6 +371,7 @@ class FusedDataParallel:
                           "overflow"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
+                rows.zero_word = self.send[self.off_cnt:].data_ptr()
                 row.append((rows, wp, ex, da, None, mg))
             self.m_dp.append(row)
         self._m_dp_S = Smax
@@ -391,16 +386,14 @@ class FusedDataParallel:
         s = main.cuda_stream
         for k in range(S):
             rows, wp, ep, da, ed, mg = self.m_dp[q][k]
-            if self.mode == "dp":
-                self.send_count.zero_()
-            H.deepfm_rows(rows, s)
+            H.deepfm_rows(rows, s)  # (dp: also zeroes the export counter)
             e._tail(wp, ep, None, s)
             self._exchange()
-            H.dense_apply(da, s)
             if self.mode == "dp":
-                H.merge_scatter(mg, s)
+                H.merge_scatter_dense(mg, da, s)  # row scatter ‖ MLP optimizer, one launch
                 H.merge_apply(mg, s)
             else:
+                H.dense_apply(da, s)
                 H.emb_dense_update(ed, s)
         main.wait_stream(side)
 
