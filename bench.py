@@ -100,8 +100,9 @@ def main():
     keeps = [float(x) for x in a.dropout.split(",")]
     spec = ModelSpec(a.feature_size, a.field_size, a.embedding_size, layers, keeps, l2_reg=a.l2_reg)
     hp = OptHParams(name=a.optimizer, lr=a.learning_rate)
-    if a.parallelism == "rowshard":
-        params = None  # each rank initialises only its own shard (100M-1B rows never materialise on one host)
+    if a.parallelism == "rowshard" or (a.engine == "fused" and a.feature_size > 20_000_000):
+        params = None  # tables drawn on the device (each rank's own shard in rowshard mode): a
+        #                100M-1B-row table never materialises on the host
     else:
         params = init_params(spec, a.seed)  # identical on every rank (= rank-0 broadcast, HVD:418)
 

@@ -24,6 +24,7 @@ State layout (device):
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 from collections import OrderedDict
 from typing import Dict, List, Optional
@@ -128,12 +129,16 @@ class FusedDeepFM:
         L = self.layout
 
         # ---- parameters + optimizer state ----------------------------------------------------
-        P = params if params is not None else init_params(spec, seed)
         self.emb = torch.zeros(self.V, self.Kp, dtype=torch.float32, device=dev)
-        self.emb[:, : self.K].copy_(P["fm_v"])
-        self.emb[:, self.K].copy_(P["fm_w"])
+        if params is not None:
+            P = params
+            self.emb[:, : self.K].copy_(P["fm_v"])
+            self.emb[:, self.K].copy_(P["fm_w"])
+        else:  # tables drawn on the device in row chunks (no host copy of a 100M-1B-row table)
+            P = init_params(dataclasses.replace(spec, feature_size=1), seed)
+            self._init_table_device(seed)
         self.dense = torch.zeros(L.total, dtype=torch.float32, device=dev)
-        L.pack({k: v.to(dev) for k, v in P.items()}, self.dense)
+        L.pack({k: v.to(dev) for k, v in P.items() if k not in ("fm_w", "fm_v")}, self.dense)
         self.emb_slots = init_slots(hp, self.emb)
         self.dense_slots = init_slots(hp, self.dense)
         self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
@@ -188,6 +193,26 @@ class FusedDeepFM:
         self._warm = 0
         self._build_params()
         self.refresh_bf16()
+
+    def _init_table_device(self, seed: int, chunk_rows: int = 1 << 24) -> None:
+        """fm_v / fm_w with the reference initialisers (TF glorot_normal over the full table's fans,
+        truncated at ±2σ) drawn on the GPU chunk by chunk."""
+        from ..models.deepfm import TRUNC_NORMAL_STD
+
+        V, K = self.V, self.K
+        gen = torch.Generator(device=self.device).manual_seed(int(seed) * 1000003 + 1)
+        sv = math.sqrt(2.0 / (V + K)) / TRUNC_NORMAL_STD
+        sw = math.sqrt(2.0 / (V + V)) / TRUNC_NORMAL_STD
+        for r0 in range(0, V, chunk_rows):
+            blk = self.emb[r0:min(V, r0 + chunk_rows)]
+            x = torch.randn(blk.shape[0], K + 1, generator=gen, device=self.device)
+            bad = x.abs() > 2.0
+            while bool(bad.any()):
+                x = torch.where(bad, torch.randn(x.shape, generator=gen, device=self.device), x)
+                bad = x.abs() > 2.0
+            blk[:, :K].copy_(x[:, :K] * sv)
+            blk[:, K].copy_(x[:, K] * sw)
+            del x, bad
 
     # ------------------------------------------------------------------------------------------
     def _opt(self, p: int = 0, lrt_ptr: Optional[int] = None):

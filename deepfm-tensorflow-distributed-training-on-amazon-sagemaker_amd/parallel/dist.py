@@ -102,6 +102,9 @@ def broadcast_tensors(tensors, src: int = 0) -> None:
         return
     by_dtype = {}
     for t in tensors:
+        if t.numel() * t.element_size() >= (64 << 20) and t.is_contiguous():
+            dist.broadcast(t, src)  # large tables: in place, no concatenated copy
+            continue
         by_dtype.setdefault(t.dtype, []).append(t)
     for _, ts in by_dtype.items():
         flat = torch.cat([t.reshape(-1) for t in ts])
