@@ -49,6 +49,8 @@ struct FetchMultiParams {
   float* labels;    // [S][Bp]
   uint32_t* keys;   // [S][B*F] composite sort keys (nullable)
   int id_bits;
+  int shard_W;      // > 0: keys are owner-major row-shard keys (id % W)·Vs + id / W (shard.hip)
+  uint32_t shard_Vs;
   int64_t* steps;   // [S] global_step of each prepared step
   float* lrt;       // [S] lr_t of each prepared step
   float lr, beta1, beta2;

@@ -66,7 +66,10 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
     const int32_t id = si[i];
     di[i] = id;
     dv[i] = sv[i];
-    if (dk) dk[i] = kb | (uint32_t)id;
+    if (dk) {
+      const uint32_t u = (uint32_t)id;
+      dk[i] = kb | (p.shard_W > 0 ? (u % (uint32_t)p.shard_W) * p.shard_Vs + u / (uint32_t)p.shard_W : u);
+    }
   }
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.B; i += (long long)gridDim.x * 256)
     p.labels[(long long)k * p.Bp + i] = p.labels_pool[b * p.B + i];

@@ -31,6 +31,8 @@ struct ShardRouteParams {
   int32_t* counts;        // [W] unique ids per owner this batch (> cap means overflow)
   int32_t* overflow;      // sticky flag: set to 1 when any owner needs more than cap rows
   int32_t* scratch;       // [route_scratch_ints(n)] per-tile run-head counts
+  uint32_t key_base;      // subtracted from skeys (a batch's segment of a multi-batch sort)
+  uint32_t val_base;      // subtracted from svals (ditto)
 };
 
 // Owner side: serve the requested rows and emit the local row keys of the requests.

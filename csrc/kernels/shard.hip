@@ -65,8 +65,8 @@ __global__ __launch_bounds__(256) void shard_keys_kernel(ShardKeysParams p) {
 //            heads publish their global id to the owner's request list; pads the lists.
 __device__ __forceinline__ void load_tile(const ShardRouteParams& p, int i0, uint32_t (&k)[kRI], uint32_t& prev) {
 #pragma unroll
-  for (int u = 0; u < kRI; ++u) k[u] = (i0 + u < p.n) ? p.skeys[i0 + u] : kPad;
-  prev = (i0 > 0 && i0 <= p.n) ? p.skeys[i0 - 1] : kPad;
+  for (int u = 0; u < kRI; ++u) k[u] = (i0 + u < p.n) ? p.skeys[i0 + u] - p.key_base : kPad;
+  prev = (i0 > 0 && i0 <= p.n) ? p.skeys[i0 - 1] - p.key_base : kPad;
 }
 
 __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams p) {
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kRT) void shard_route_assign_kernel(ShardRouteParam
   uint32_t k[kRI], v[kRI], prev;
   load_tile(p, i0, k, prev);
 #pragma unroll
-  for (int u = 0; u < kRI; ++u) v[u] = (i0 + u < p.n) ? p.svals[i0 + u] : 0u;
+  for (int u = 0; u < kRI; ++u) v[u] = (i0 + u < p.n) ? p.svals[i0 + u] - p.val_base : 0u;
   int heads = 0;
   {
     uint32_t pv = prev;

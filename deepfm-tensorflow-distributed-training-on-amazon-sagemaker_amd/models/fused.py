@@ -432,7 +432,7 @@ class FusedDeepFM:
         self._graphs = [None, None]
         self._primed = False
         if getattr(self, "mS", None) is not None:
-            self._build_multi(self.mS)  # rebuild the multi-step parameter blocks with the new lr
+            self._build_multi(self.mS, getattr(self, "_m_shard", None))  # rebuild with the new lr
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -561,10 +561,13 @@ class FusedDeepFM:
     # 47 vs 55 µs/step); ONE side chain per graph prepares the NEXT graph's S batches (one copy
     # kernel) and sorts all S·B·F lookups at once (composite key batch << id_bits | id), joined
     # at the graph's end.
-    def _build_multi(self, Smax: int) -> None:
+    def _build_multi(self, Smax: int, shard: Optional[tuple] = None) -> None:
+        """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
-        idbits = max(1, math.ceil(math.log2(max(self.V, 2))))
+        self._m_shard = shard
+        key_range = self.V if shard is None else shard[0] * shard[1]
+        idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
         Smax = max(1, min(int(Smax), 1 << max(0, 32 - idbits)))
         sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
         self.mS, self.m_idbits, self.m_bits = Smax, idbits, idbits + sbits
@@ -617,6 +620,8 @@ class FusedDeepFM:
         f.ids, f.vals, f.labels = (self.m_ids[1 - q].data_ptr(), self.m_vals[1 - q].data_ptr(),
                                    self.m_labels[1 - q].data_ptr())
         f.keys, f.id_bits = self.m_keys.data_ptr(), self.m_idbits
+        if getattr(self, "_m_shard", None) is not None:
+            f.shard_W, f.shard_Vs = self._m_shard
         f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
         f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
         f.opt_type = OPT_ID[self.hp.name]
@@ -633,6 +638,8 @@ class FusedDeepFM:
         a.n, a.S, a.chunk = self.n_lookup, self.mS, self.m_chunk
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
         H.sort_aux(a, stream.cuda_stream)
+        if getattr(self, "_m_post", None) is not None:  # e.g. row-shard routing of the sorted batches
+            self._m_post(1 - q, stream)
 
     def _prime_multi(self) -> None:
         base = 0 if self._ring else getattr(self, "_start_batch", 0)

@@ -620,6 +620,7 @@ class FusedRowShard:
 
     def train_step(self) -> None:
         e = self.eng
+        e._m_primed = False
         if not e._primed:
             self.prime()
         p = e._i % 2
@@ -642,8 +643,11 @@ class FusedRowShard:
         if self.check_every and i1 // self.check_every != i0 // self.check_every:
             self.check()
 
-    def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
+    def train_steps(self, n: int, steps_per_graph: int = 16) -> None:
         e = self.eng
+        if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
+            self._train_steps_multi(n, steps_per_graph)
+            return
         S = max(2, steps_per_graph // 2 * 2)
         while n > 0:
             if (self.graph_collectives and self.use_graph and self._warm >= 4 and e._primed and n >= S
@@ -671,6 +675,116 @@ class FusedRowShard:
         RCCL collectives)."""
         torch.cuda.synchronize(self.device)
         self._graphs = {}
+
+    # ---- multi-step graphs (pool mode, capturable collectives) -----------------------------------
+    # FusedDeepFM's multi-step pipeline with row-shard routing: the side chain of a graph fetches
+    # the next graph's S batches with owner-major sort keys, sorts them at once and routes every
+    # batch (S route launches); each step then runs X1 → serve → X2 → rows → tail → X3 → X4 →
+    # owner merge ‖ MLP optimizer → merge apply, collectives captured inline.
+    def _build_multi_rs(self, Smax: int) -> None:
+        e, H = self.eng, self.H
+        W, cap, n, F = self.W, self.cap, self.n, e.F
+        e._build_multi(Smax, shard=(W, self.Vs))
+        e._m_pool = e.pool_ids
+        S_ = e.mS
+        dev = self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.ms_send = torch.full((2, S_, W * cap), PAD, **i32)
+        self.ms_local = torch.zeros(2, S_, e.Bp, F, **i32)
+        self.ms_skl = torch.zeros(2, S_, n, **i32)
+        self.ms_counts = torch.zeros(2, S_, W, **i32)
+        self.ms_scratch = torch.zeros(H.route_scratch_ints(n), **i32)
+        self.ms_route = []
+        self.ms_steps = []
+        for q in range(2):
+            routes, steps = [], []
+            for k in range(S_):
+                rp = H.ShardRouteParams()
+                rp.skeys, rp.svals, rp.n = e.m_sk[q, k * n:].data_ptr(), e.m_sv[q, k * n:].data_ptr(), n
+                rp.W, rp.Vs, rp.cap = W, self.Vs, cap
+                rp.key_base, rp.val_base = k << e.m_idbits, k * n
+                rp.send_ids, rp.local_idx = self.ms_send[q, k].data_ptr(), self.ms_local[q, k].data_ptr()
+                rp.skeys_local, rp.counts = self.ms_skl[q, k].data_ptr(), self.ms_counts[q, k].data_ptr()
+                rp.overflow, rp.scratch = self.overflow.data_ptr(), self.ms_scratch.data_ptr()
+                routes.append(rp)
+                rows, wp, da, ep, ed = e.m_params[q][k]
+                rows.ids, rows.emb = self.ms_local[q, k].data_ptr(), self.rows_in.data_ptr()
+                wp.grads = e.dense_grads_flat.data_ptr()
+                ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
+                ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
+                ep.grad_scale = 1.0
+                da.apply, da.grads, da.grad_scale = 1, e.dense_grads_flat.data_ptr(), 1.0 / W
+                mg = H.MergeParams()
+                src = self.owner_params[0]
+                for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
+                          "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
+                          "dense_grad"):
+                    setattr(mg, f, getattr(src, f))
+                mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
+                if ed is not None:
+                    ed.grad_scale = 1.0
+                steps.append((rows, wp, ep, da, ed, mg))
+            self.ms_route.append(routes)
+            self.ms_steps.append(steps)
+
+        def route_all(q, stream):
+            for rp in self.ms_route[q]:
+                H.shard_route(rp, stream.cuda_stream)
+
+        e._m_post = route_all
+        self._ms_S = Smax
+
+    def _enqueue_multi_rs(self, q: int, S: int) -> None:
+        e, H = self.eng, self.H
+        main = torch.cuda.current_stream(self.device)
+        side = e.sort_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            e._prepare_multi(q, S, side)
+        s = main.cuda_stream
+        for k in range(S):
+            rows, wp, ep, da, ed, mg = self.ms_steps[q][k]
+            self._exchange(self.recv_ids, self.ms_send[q, k])                   # X1 requests
+            H.shard_serve(self.serve, s)
+            self._exchange(self.rows_in, self.rows_out)                         # X2 rows
+            H.deepfm_rows(rows, s)
+            e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
+            self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
+            if self.W > 1:
+                all_reduce_(e.dense_grads_flat)                                 # X4 MLP grads
+            H.merge_scatter_dense(mg, da, s)                                    # owner scatter ‖ MLP opt
+            H.merge_apply(mg, s)
+            if ed is not None:
+                H.emb_dense_update(ed, s)
+        main.wait_stream(side)
+
+    def _train_steps_multi(self, n: int, Smax: int) -> None:
+        e = self.eng
+        if getattr(self, "_ms_S", None) != Smax or getattr(e, "_m_pool", None) is not e.pool_ids:
+            self._build_multi_rs(Smax)
+        if not e._m_primed:
+            e._prime_multi()
+        while n > 0:
+            S = min(n, e.mS)
+            q = e._mq
+            if e._m_warm < 1:
+                self._enqueue_multi_rs(q, S)
+            else:
+                key = ("mrs", q, S)
+                g = self._graphs.get(key)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize(self.device)
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        self._enqueue_multi_rs(q, S)
+                    self._graphs[key] = g
+                g.replay()
+            e._m_warm += 1
+            e._mq ^= 1
+            e._i += S
+            n -= S
+            self._after_steps(e._i - S, e._i)
+        e._primed = False
 
     def train_on(self, batches):
         it = iter(batches)

@@ -178,3 +178,26 @@ def test_fused_rowshard_2ranks_equals_single_gpu_union_batch(tmp_path, update):
     ids, vals, _ = _batches(100, 1, 5)[0]
     pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
     torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_rowshard_multistep_world1_equals_single(update):
+    """Row-shard through the multi-step graph pipeline (batched owner-major sort, per-batch routing
+    in the side chain, exchanges inline) ≡ the single-GPU engine."""
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg()
+    n = 11
+    eng = FusedRowShard(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=update,
+                        use_graph=True)
+    batches = _batches(128, n, 11)
+    eng.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
+                    torch.stack([b[2] for b in batches]).cuda())
+    eng.train_steps(n, 4)  # 4 eager + 4 graph + 3 tail graph
+    torch.cuda.synchronize()
+    eng.check()
+    ref = _single(update, n)
+    got, exp = eng.parameters_tf(), ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got[k], exp[k], rtol=2e-3, atol=2e-5)
