@@ -12,6 +12,7 @@ import re
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     n = re.sub(r"\(.*", "", name)
     n = re.sub(r"<.*", "", n) if "rocprim" not in n else "rocprim::" + re.findall(r"detail::(\w+)", name)[0] \
         if re.findall(r"detail::(\w+)", name) else n
