@@ -39,6 +39,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   __shared__ float4 s_rows[kChunk * KP4];
   __shared__ float4 s_cont[kWaves * KP4];
   __shared__ int s_head[kChunk + 1];
+  __shared__ uint32_t s_hkey[kChunk + 1];
   __shared__ int s_wcnt[kWaves];
   __shared__ int s_nh, s_last_end, s_out_base;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -89,7 +90,10 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   {
     int base = 0;
     for (int w = 0; w < wave; ++w) base += s_wcnt[w];
-    if (head) s_head[base + before] = i;
+    if (head) {
+      s_head[base + before] = i;
+      s_hkey[base + before] = key;
+    }
   }
   if (t == 0) {
     int tot = 0;
@@ -103,8 +107,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   if (nh == 0) return;
   // 4. end of the last run (all 256 threads probe 256 entries per round); mode 2 reserves slots
   {
-    const int last = s_head[nh - 1];
-    const uint32_t lk = p.skeys[last];
+    const uint32_t lk = s_hkey[nh - 1];
     const bool sentinel = p.max_key && lk >= p.max_key;  // sentinel padding sorts last: runs to n
     int pos = sentinel ? p.n : cend;
     if (t == 0) s_last_end = p.n;
@@ -139,7 +142,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   if (t == 0) s_head[nh] = min(s_last_end, cend);
   // 5. continuation of the last run past the chunk: full reductions over following chunks
   const int last_end = s_last_end;
-  const bool cont = last_end > cend && !(p.max_key && p.skeys[s_head[nh - 1]] >= p.max_key);
+  const bool cont = last_end > cend && !(p.max_key && s_hkey[nh - 1] >= p.max_key);
   if (cont) {
     float4 tot[KP4];
 #pragma unroll
@@ -170,65 +173,68 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   }
   __syncthreads();
   ROCFM_STAMP(p.stamps, 3);
-  // 6. (run, column) items over all threads: add the run's wave pieces (+ continuation), then the
-  //    optimizer; every thread issues its table/slot loads for up to 4 items before using any.
-  constexpr int Kp = KP4 * 4;
-  const int nitems = nh * Kp;
+  // 6. (run, float4 column group) items over all threads: add the run's wave pieces (+ the
+  //    continuation), then the optimizer on a float4 of the table row; every thread issues its
+  //    table/slot loads for up to 4 items before using any.
+  const int nitems = nh * KP4;
   for (int base = 0; base < nitems; base += kChunk * 4) {
-    float w[4], a[4], b[4], g[4];
+    float4 w[4], a[4], b[4], g[4];
     uint32_t kk[4];
-    size_t idx[4];
+    size_t idx4[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int it = min(base + u * kChunk + t, nitems - 1);
-      const int r = it / Kp, col = it - r * Kp;
+      const int r = it / KP4, u4 = it - r * KP4;
       const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
-      kk[u] = p.skeys[s];
+      kk[u] = s_hkey[r];
       const bool skip = p.max_key && kk[u] >= p.max_key;
-      const int u4 = col >> 2, comp = col & 3;
-      float acc = 0.f;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
       for (int ww = w0; ww <= w1; ++ww) {
         const int lastw = min(e, c0 + 64 * (ww + 1)) - 1 - c0;
-        const float4 x = s_rows[lastw * KP4 + u4];
-        acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
+        acc = f4add(acc, s_rows[lastw * KP4 + u4]);
       }
       if (cont && r == nh - 1) {
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) {
-          const float4 x = s_cont[ww * KP4 + u4];
-          acc += comp == 0 ? x.x : comp == 1 ? x.y : comp == 2 ? x.z : x.w;
-        }
+        for (int ww = 0; ww < kWaves; ++ww) acc = f4add(acc, s_cont[ww * KP4 + u4]);
       }
-      g[u] = acc * p.grad_scale;
+      g[u] = make_float4(acc.x * p.grad_scale, acc.y * p.grad_scale, acc.z * p.grad_scale, acc.w * p.grad_scale);
       const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
-      idx[u] = row * Kp + col;
+      idx4[u] = row * KP4 + u4;
       if (p.mode == 0) {  // issue the row's parameter + slot loads now
-        w[u] = p.emb[idx[u]];
-        a[u] = p.s0 ? p.s0[idx[u]] : 0.f;
-        b[u] = p.s1 ? p.s1[idx[u]] : 0.f;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        w[u] = reinterpret_cast<const float4*>(p.emb)[idx4[u]];
+        a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;
+        b[u] = p.s1 ? reinterpret_cast<const float4*>(p.s1)[idx4[u]] : z;
       }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int it = base + u * kChunk + t;
       if (it >= nitems) continue;
-      const int r = it / Kp, col = it - r * Kp;
-      if ((p.max_key && kk[u] >= p.max_key) || col >= p.K1) continue;
+      const int r = it / KP4, u4 = it - r * KP4;
+      if (p.max_key && kk[u] >= p.max_key) continue;
       if (p.mode == 2) {
         const int slot = s_out_base + r;
         if (slot < p.out_cap) {
-          p.out_rows[(size_t)slot * Kp + col] = g[u];
-          if (col == 0) p.out_keys[slot] = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
+          reinterpret_cast<float4*>(p.out_rows)[(size_t)slot * KP4 + u4] = g[u];  // pad columns are 0
+          if (u4 == 0) p.out_keys[slot] = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
         }
       } else if (p.mode == 1) {
-        p.dense_grad[idx[u]] = g[u];
+        reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];
       } else {
-        float ww = w[u], aa = a[u], bb = b[u];
-        opt_apply(p.opt, st, ww, g[u] + p.l2 * ww, aa, bb);
-        p.emb[idx[u]] = ww;
-        if (p.s0) p.s0[idx[u]] = aa;
-        if (p.s1) p.s1[idx[u]] = bb;
+        float* wc = &w[u].x;
+        float* ac = &a[u].x;
+        float* bc = &b[u].x;
+        const float* gc = &g[u].x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (u4 * 4 + c >= p.K1) continue;  // padding columns keep their (zero) values
+          opt_apply(p.opt, st, wc[c], gc[c] + p.l2 * wc[c], ac[c], bc[c]);
+        }
+        reinterpret_cast<float4*>(p.emb)[idx4[u]] = w[u];
+        if (p.s0) reinterpret_cast<float4*>(p.s0)[idx4[u]] = a[u];
+        if (p.s1) reinterpret_cast<float4*>(p.s1)[idx4[u]] = b[u];
       }
     }
   }
