@@ -267,16 +267,42 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if (!(p.ablate & 2)) {
     const int r = t >> 5, q = t & 31;
     float cterm = 0.f, yw = 0.f;
-    for (int k = q; k < K; k += 32) {
+    // G = ⌊32/K⌋ lanes per embedding column split the F fields (field f → group f mod G); the
+    // group partials are combined in group order through shuffles (deterministic)
+    const int G = K <= 32 ? 32 / K : 1;
+    if (G > 1) {
+      const int k = q % K, gq = q / K;
       float S = 0.f, Q = 0.f;
+      if (gq < G) {
 #pragma unroll 4
-      for (int f = 0; f < F; ++f) {
-        const float e = s_f32[r * D0p + f * K + k];
-        S += e;
-        Q += e * e;
+        for (int f = gq; f < F; f += G) {
+          const float e = s_f32[r * D0p + f * K + k];
+          S += e;
+          Q += e * e;
+        }
       }
-      s_S[r * K + k] = S;
-      cterm += S * S - Q;
+      float St = 0.f, Qt = 0.f;
+      for (int j = 0; j < G; ++j) {  // uniform loop: every lane takes part in each shuffle
+        const int src = (lane & 32) + k + j * K;
+        St += __shfl(S, src, 64);
+        Qt += __shfl(Q, src, 64);
+      }
+      if (gq == 0) {
+        s_S[r * K + k] = St;
+        cterm = St * St - Qt;
+      }
+    } else {
+      for (int k = q; k < K; k += 32) {
+        float S = 0.f, Q = 0.f;
+#pragma unroll 4
+        for (int f = 0; f < F; ++f) {
+          const float e = s_f32[r * D0p + f * K + k];
+          S += e;
+          Q += e * e;
+        }
+        s_S[r * K + k] = S;
+        cterm += S * S - Q;
+      }
     }
     for (int f = q; f < F; f += 32) yw += s_wx[r * F + f];
 #pragma unroll
