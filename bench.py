@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--learning_rate", type=float, default=0.0005)
     ap.add_argument("--l2_reg", type=float, default=0.0001)
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"])
+    ap.add_argument("--compute_dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: the MLP input layer's forward GEMM on fp8-e4m3 MFMA (dynamic scales)")
     ap.add_argument("--embedding_update", default="sparse", choices=["sparse", "exact"])
     ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
@@ -131,17 +133,18 @@ def main():
             from rocfm.parallel.emb_shard import FusedRowShard
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
-                                use_graph=not a.no_graph, capacity=cap)
+                                use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype)
         elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
-                                    mode=parallelism, seed=a.seed, use_graph=not a.no_graph, capacity=cap)
+                                    mode=parallelism, seed=a.seed, use_graph=not a.no_graph, capacity=cap,
+                                    compute_dtype=a.compute_dtype)
         else:
             from rocfm.models.fused import FusedDeepFM
 
             eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
-                              use_graph=not a.no_graph)
+                              use_graph=not a.no_graph, compute_dtype=a.compute_dtype)
 
         eng.attach_pool(pool_ids, pool_vals, pool_labels)
 
@@ -204,7 +207,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(value / (base * world), 3) if base else None),
-        "dtype": "bf16",
+        "dtype": a.compute_dtype if a.engine == "fused" else "fp32",
         "data": "synthetic Criteo-shape (39 fields, Zipf ids, HBM-resident batch pool), random-init weights",
         "config": {
             "model": f"DeepFM Criteo-shape ({a.field_size} fields, {_human(a.feature_size)}-hash vocab, k={a.embedding_size}, "

@@ -10,7 +10,7 @@ constexpr int kRowTile = 16;   // rows per workgroup = one 16-row MFMA M tile
 constexpr int kRowThreads = 512;  // 8 waves
 
 struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
-  int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32, pos;
+  int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32, pos, amax;
   int lda[kMaxHidden + 1];  // bf16 row stride of each activation tile
   int ldz;                  // bf16 row stride of the dz ping-pong tiles
   int prm;                  // f32 block of small parameters staged at kernel start:
@@ -52,6 +52,8 @@ struct RowsParams {
   const int32_t* contrib_pos;  // nullable [B][F]: row of contrib receiving each lookup's gradient
                                // (its position in the sorted lookup order), else row·F + field
   int32_t* zero_word;          // nullable: set to 0 at kernel start (DP: the export's row counter)
+  int fp8;                     // 1: the input layer's forward GEMM on fp8-e4m3 MFMA (per-row activation
+                               // and per-column weight scales; compile-time-shape kernels only)
   int force_generic;           // 1: never use a compile-time-shape instantiation (tests)
   int ablate;                  // diagnostics only (results invalid): bit0 skip h0ᵀ stores, bit1 skip
                                // the FM loop, bit2 skip the phase-B weight prefetch

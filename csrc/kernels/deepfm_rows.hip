@@ -33,6 +33,23 @@ namespace {
 
 __device__ __forceinline__ bf16x8 ld_frag(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// fp8 (OCP e4m3fn, gfx950) quantisation of 8 bf16 values scaled by s into one MFMA operand
+// (byte j = element j; round-to-nearest-even conversion).
+__device__ __forceinline__ long quant_fp8x8(bf16x8 v, float s) {
+  int lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((uint16_t)v[0]) * s, bf2f((uint16_t)v[1]) * s, lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((uint16_t)v[2]) * s, bf2f((uint16_t)v[3]) * s, lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((uint16_t)v[4]) * s, bf2f((uint16_t)v[5]) * s, hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((uint16_t)v[6]) * s, bf2f((uint16_t)v[7]) * s, hi, true);
+  return (long)(uint32_t)lo | ((long)(uint32_t)hi << 32);
+}
+__device__ __forceinline__ float absmax_bf16x8(bf16x8 v, float m) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f((uint16_t)v[j])));
+  return m;
+}
+constexpr float kFp8Max = 448.f;  // largest finite e4m3fn
+
 __device__ __forceinline__ uint32_t pick4(const Philox4& b, int i) {
   return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
 }
@@ -135,6 +152,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   float* s_S = reinterpret_cast<float*>(smem + L.S);
   float* s_ylin = reinterpret_cast<float*>(smem + L.ylin);
   float* s_g = reinterpret_cast<float*>(smem + L.g);
+  float* s_amax = reinterpret_cast<float*>(smem + L.amax);  // fp8: per-row max |h0|
   float* s_f32 = reinterpret_cast<float*>(smem + L.f32);  // e (forward) / dh0 (backward), stride dims[0]
   float* s_prm = reinterpret_cast<float*>(smem + L.prm);
 
@@ -266,7 +284,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
   if (!(p.ablate & 2)) {
     const int r = t >> 5, q = t & 31;
-    float cterm = 0.f, yw = 0.f;
+    float cterm = 0.f, yw = 0.f, amx = 0.f;
     // G = ⌊32/K⌋ lanes per embedding column split the F fields (field f → group f mod G); the
     // group partials are combined in group order through shuffles (deterministic)
     const int G = K <= 32 ? 32 / K : 1;
@@ -279,6 +297,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           const float e = s_f32[r * D0p + f * K + k];
           S += e;
           Q += e * e;
+          amx = fmaxf(amx, fabsf(e));
         }
       }
       float St = 0.f, Qt = 0.f;
@@ -299,10 +318,16 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           const float e = s_f32[r * D0p + f * K + k];
           S += e;
           Q += e * e;
+          amx = fmaxf(amx, fabsf(e));
         }
         s_S[r * K + k] = S;
         cterm += S * S - Q;
       }
+    }
+    if (p.fp8) {  // row max |bf16(e)| = bf16(max |e|) (rounding is monotonic)
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o, 64));
+      if (q == 0) s_amax[r] = bf2f(f2bf(amx));
     }
     for (int f = q; f < F; f += 32) yw += s_wx[r * F + f];
 #pragma unroll
@@ -377,7 +402,25 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SH::kStatic) {
         const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
-        if (l == 0) {
+        if (l == 0 && p.fp8) {
+          // fp8-e4m3 MFMA: weights quantised per output column (this wave owns whole columns, all
+          // of K in registers), activations per row; the product is de-scaled in the epilogue
+          float wm = 0.f;
+#pragma unroll
+          for (int u = 0; u < SH::KSF0; ++u) wm = absmax_bf16x8(fw0[u], wm);
+          wm = fmaxf(wm, __shfl_xor(wm, 16, 64));
+          wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
+          const float sb = kFp8Max / fmaxf(wm, 1e-30f);
+          const float sa = kFp8Max / fmaxf(s_amax[lane & 15], 1e-30f);
+#pragma unroll
+          for (int u = 0; u < SH::KSF0; ++u)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(quant_fp8x8(ld_frag(ap + 32 * u), sa),
+                                                            quant_fp8x8(fw0[u], sb), acc, 0, 0, 0);
+          const int rbq = (lane >> 4) * 4;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i] *= (fmaxf(s_amax[rbq + i], 1e-30f) / kFp8Max) * (1.f / sb);
+        } else if (l == 0) {
 #pragma unroll
           for (int u = 0; u < SH::KSF0; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
         } else if (l == 1) {
@@ -605,6 +648,7 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
   L.pos = take(kRowTile * F * 4);
   L.S = take(kRowTile * K * 4);
   L.ylin = take(kRowTile * 4);
+  L.amax = take(kRowTile * 4);
   L.g = take(kRowTile * 4);
   int maxh = 0;
   for (int a = 0; a <= nl; ++a) {
@@ -689,6 +733,8 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
       return;
     }
   }
+  ROCFM_REQUIRE(!p.fp8, "deepfm_rows: compute_dtype=fp8 needs a compile-time-shape instantiation (39 fields, "
+                        "k in {8,10,12}, MLP 128-64-32 or 64-32) or compute_dtype=bf16");
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N)                          \
   case N:                                     \

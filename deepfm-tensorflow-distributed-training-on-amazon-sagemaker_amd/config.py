@@ -102,7 +102,8 @@ class Config:
     embedding_update: str = "sparse"  # sparse (lazy L2 + row optimizer) | exact (dense, faithful Q1)
     parallelism: str = "auto"  # auto | dp (replicated table) | rowshard (PS-equivalent) | dense_dp
     lr_scaling: str = "linear"  # linear (lr × world, HVD:171) | none
-    compute_dtype: str = "bf16"  # bf16 | fp32 (MLP MFMA operand dtype in the fused engine)
+    compute_dtype: str = "bf16"  # bf16 | fp8: MLP MFMA operands in the fused engine (fp8: the input
+    #                              layer's forward GEMM on e4m3 with dynamic per-row/per-column scales)
     seed: int = 1234
     save_checkpoints_steps: int = 0  # 0 → only at end (plus save_checkpoints_secs)
     save_checkpoints_secs: int = 600  # Estimator default cadence
@@ -153,6 +154,8 @@ class Config:
             raise ValueError(f"unknown task_type {self.task_type!r}")
         if self.embedding_update not in ("sparse", "exact"):
             raise ValueError(f"unknown embedding_update {self.embedding_update!r}")
+        if self.compute_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"compute_dtype must be bf16 or fp8, got {self.compute_dtype!r}")
         if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard"):
             raise ValueError(f"unknown parallelism {self.parallelism!r}")
         if self.engine not in ("auto", "fused", "torch"):

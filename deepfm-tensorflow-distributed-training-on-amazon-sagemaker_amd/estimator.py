@@ -96,7 +96,7 @@ class Estimator:
             if self.engine_name == "fused":
                 return FusedRowShard(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                      embedding_update=cfg.embedding_update, seed=cfg.seed,
-                                     use_graph=cfg.use_hip_graph, capacity=cap)
+                                     use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype)
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
                                  seed=cfg.seed)
         if self.engine_name == "fused":
@@ -106,11 +106,11 @@ class Estimator:
                 mode = "dense_dp" if (cfg.embedding_update == "exact" or cfg.parallelism == "dense_dp") else "dp"
                 return FusedDataParallel(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                          embedding_update=cfg.embedding_update, mode=mode, seed=cfg.seed,
-                                         use_graph=cfg.use_hip_graph, capacity=cap)
+                                         use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype)
             from .models.fused import FusedDeepFM
 
             return FusedDeepFM(self.spec, self.hp, cfg.batch_size, self.device, embedding_update=cfg.embedding_update,
-                               seed=cfg.seed, params=P, use_graph=cfg.use_hip_graph)
+                               seed=cfg.seed, params=P, use_graph=cfg.use_hip_graph, compute_dtype=cfg.compute_dtype)
         from .models.torch_engine import TorchDeepFM
 
         eng = TorchDeepFM(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,

@@ -100,7 +100,7 @@ class FusedDeepFM:
                  embedding_update: str = "sparse", seed: int = 1234,
                  params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
                  use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None,
-                 force_generic_kernels: bool = False):
+                 force_generic_kernels: bool = False, compute_dtype: str = "bf16"):
         if spec.batch_norm:
             raise ValueError("the fused engine does not implement batch_norm; use engine=torch")
         if len(spec.layers) > 6:
@@ -125,6 +125,9 @@ class FusedDeepFM:
         self.loss_code = 0 if spec.loss_type == "log_loss" else 1
         self.lr_scale = 1.0
         self.force_generic = bool(force_generic_kernels)
+        if compute_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"compute_dtype must be bf16 or fp8, got {compute_dtype!r}")
+        self.compute_dtype = compute_dtype
         dev = self.device
         L = self.layout
 
@@ -249,6 +252,7 @@ class FusedDeepFM:
         rp.loss_type = self.loss_code
         rp.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         rp.force_generic = 1 if self.force_generic else 0
+        rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
         rp.set_dims(L.dims)
         for l in range(L.nl):
             rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),

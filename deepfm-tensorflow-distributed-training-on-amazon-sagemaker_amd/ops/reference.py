@@ -57,7 +57,7 @@ def bf16(x: torch.Tensor) -> torch.Tensor:
 def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]], w_out: torch.Tensor,
                          b_out: float, fm_bias: float, ids: torch.Tensor, vals: torch.Tensor,
                          labels: torch.Tensor, K: int, keeps: List[float], masks: Optional[List[torch.Tensor]],
-                         inv_scale: float, train: bool = True, loss_type: int = 0):
+                         inv_scale: float, train: bool = True, loss_type: int = 0, fp8: bool = False):
     """Forward + backward with the fused kernels' numerics, on unpadded shapes.
 
     ``emb`` [V, Kp] (cols 0..K-1 fm_v, col K fm_w); ``layers[l]`` = {W [in,out] f32, b [out]}.
@@ -73,7 +73,10 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
     y_lin = fm_bias + (w * x).sum(1) + 0.5 * (S * S - (e * e).sum(1)).sum(1)
     h = [bf16(e.reshape(B, F * K))]
     for li, L in enumerate(layers):
-        z = h[-1] @ bf16(L["W"]) + L["b"]
+        if fp8 and li == 0:
+            z = fp8_rowcol_matmul(h[-1], bf16(L["W"])) + L["b"]
+        else:
+            z = h[-1] @ bf16(L["W"]) + L["b"]
         a = torch.relu(z)
         if train and keeps[li] < 1.0:
             a = torch.where(masks[li], a / keeps[li], torch.zeros_like(a))
@@ -109,6 +112,19 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
     out["h"] = h
     out["dz"] = dz
     return out
+
+
+FP8_MAX = 448.0  # largest finite float8 e4m3fn
+
+
+def fp8_rowcol_matmul(A: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """A·W with A quantised to fp8-e4m3 per row and W per column (scale = 448 / max|·|), f32
+    accumulate, de-scaled — the fused kernel's compute_dtype=fp8 input-layer GEMM."""
+    sa = FP8_MAX / A.abs().amax(1, keepdim=True).clamp_min(1e-30)
+    sb = FP8_MAX / W.abs().amax(0, keepdim=True).clamp_min(1e-30)
+    Aq = (A * sa).to(torch.float8_e4m3fn).float()
+    Wq = (W * sb).to(torch.float8_e4m3fn).float()
+    return (Aq @ Wq) * ((1.0 / sa) * (1.0 / sb))
 
 
 def emb_grad_reference(ids: torch.Tensor, contrib: torch.Tensor):

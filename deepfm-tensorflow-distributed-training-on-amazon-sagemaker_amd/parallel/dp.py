@@ -138,7 +138,7 @@ class FusedDataParallel:
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", mode: str = "dp", seed: int = 1234, use_graph: bool = True,
-                 capacity: Optional[int] = None, check_every: int = 256):
+                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16"):
         from ..models.fused import FusedDeepFM
 
         self.world = _world()
@@ -152,7 +152,7 @@ class FusedDataParallel:
         self.mode = mode
         self.eng = FusedDeepFM(spec, hp, batch_size, device, embedding_update=embedding_update, seed=seed,
                                params=params, use_graph=False, fuse_dense_opt=False,
-                               dropout_seed=seed + 7919 * self.rank)
+                               dropout_seed=seed + 7919 * self.rank, compute_dtype=compute_dtype)
         e = self.eng
         self.use_graph = use_graph
         self.graph_collectives = use_graph and collectives_capturable()

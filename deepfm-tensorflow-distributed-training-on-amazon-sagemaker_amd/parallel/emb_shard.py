@@ -384,7 +384,7 @@ class FusedRowShard:
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
-                 capacity: Optional[int] = None, check_every: int = 256):
+                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16"):
         from ..models.fused import FusedDeepFM
 
         W, r = _world_rank()
@@ -398,7 +398,7 @@ class FusedRowShard:
         spec_loc = dataclasses.replace(spec, feature_size=Vs)
         self.eng = e = FusedDeepFM(spec_loc, hp, batch_size, dev, embedding_update=embedding_update, seed=seed,
                                    params=P, use_graph=False, fuse_dense_opt=False,
-                                   dropout_seed=seed + 7919 * r)
+                                   dropout_seed=seed + 7919 * r, compute_dtype=compute_dtype)
         del P
         self.H, self.device, self.embedding_update = e.H, e.device, embedding_update
         self.use_graph, self.check_every = use_graph, int(check_every)
