@@ -2,6 +2,10 @@
 // CPU-only machines (tests) and feeds pinned buffers on the GPU box.
 #include <pybind11/numpy.h>
 #include <cstring>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -139,19 +143,34 @@ PYBIND11_MODULE(_rocfm_io, m) {
   m.def(
       "count_records",
       [](const std::string& path) {
-        // framing walk only (u64 length, u32 crc, payload, u32 crc): no payload read, no CRC check
-        FILE* f = fopen(path.c_str(), "rb");
-        if (!f) throw std::runtime_error("cannot open " + path);
-        int64_t n = 0;
-        uint8_t hdr[12];
+        // framing walk only (u64 length, u32 crc, payload, u32 crc) over a read-only mapping: no
+        // payload read, no CRC check (a stdio seek per record costs a syscall each)
         py::gil_scoped_release nogil;
-        while (fread(hdr, 1, 12, f) == 12) {
-          uint64_t len;
-          std::memcpy(&len, hdr, 8);
-          if (fseeko(f, (off_t)len + 4, SEEK_CUR) != 0) break;
-          ++n;
+        int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw std::runtime_error("cannot open " + path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) {
+          ::close(fd);
+          throw std::runtime_error("cannot stat " + path);
         }
-        fclose(f);
+        const size_t size = (size_t)st.st_size;
+        int64_t n = 0;
+        if (size >= 12) {
+          void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+          if (m == MAP_FAILED) {
+            ::close(fd);
+            throw std::runtime_error("mmap failed for " + path);
+          }
+          const uint8_t* b = static_cast<const uint8_t*>(m);
+          for (size_t off = 0; off + 12 <= size; ++n) {
+            uint64_t len;
+            std::memcpy(&len, b + off, 8);
+            if (len > size - off - 12) break;
+            off += 12 + len + 4;
+          }
+          munmap(m, size);
+        }
+        ::close(fd);
         return n;
       },
       py::arg("path"));
@@ -169,7 +188,7 @@ PYBIND11_MODULE(_rocfm_io, m) {
       .def(py::init([](std::vector<std::string> files, int field_size, int64_t max_id, int batch_size,
                        bool drop_remainder, int num_epochs, int shard_count, int shard_index, int num_threads,
                        int num_slots, bool verify_crc, bool skip_bad, int shuffle_buffer, uint64_t seed,
-                       bool stream_mode) {
+                       bool stream_mode, int64_t skip_batches) {
              LoaderOptions o;
              o.files = std::move(files);
              o.schema.field_size = field_size;
@@ -186,13 +205,14 @@ PYBIND11_MODULE(_rocfm_io, m) {
              o.shuffle_buffer = shuffle_buffer;
              o.seed = seed;
              o.stream_mode = stream_mode;
+             o.skip_batches = skip_batches;
              return new BatchLoader(o);
            }),
            py::arg("files"), py::arg("field_size"), py::arg("max_id") = 0, py::arg("batch_size") = 1024,
            py::arg("drop_remainder") = true, py::arg("num_epochs") = 1, py::arg("shard_count") = 1,
            py::arg("shard_index") = 0, py::arg("num_threads") = 4, py::arg("num_slots") = 4,
            py::arg("verify_crc") = true, py::arg("skip_bad") = false, py::arg("shuffle_buffer") = 0,
-           py::arg("seed") = 0, py::arg("stream_mode") = false)
+           py::arg("seed") = 0, py::arg("stream_mode") = false, py::arg("skip_batches") = 0)
       .def("set_slot",
            [](BatchLoader& L, int i, uintptr_t ids, uintptr_t vals, uintptr_t labels) {
              L.set_slot(i, reinterpret_cast<int32_t*>(ids), reinterpret_cast<float*>(vals),
@@ -209,7 +229,18 @@ PYBIND11_MODULE(_rocfm_io, m) {
              return py::make_tuple(slot, rows, epoch);
            })
       .def("release", &BatchLoader::release)
+      .def("next_group",
+           [](BatchLoader& L, int max_n) {
+             int n = 0, rows = 0, epoch = 0, first;
+             {
+               py::gil_scoped_release nogil;
+               first = L.next_group(max_n, &n, &rows, &epoch);
+             }
+             return py::make_tuple(first, n, rows, epoch);
+           })
+      .def("release_group", &BatchLoader::release_group)
       .def("stop", &BatchLoader::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bad_records", &BatchLoader::bad_records)
-      .def_property_readonly("records_seen", &BatchLoader::records_seen);
+      .def_property_readonly("records_seen", &BatchLoader::records_seen)
+      .def_property_readonly("index_fallbacks", &BatchLoader::index_fallbacks);
 }

@@ -42,6 +42,7 @@ struct LoaderOptions {
   int shuffle_buffer = 0;  // records; 0 = no record shuffle (reference default, Q6)
   uint64_t seed = 0;
   bool stream_mode = false;  // pipe mode: files are FIFOs / "-" for stdin, read sequentially
+  int64_t skip_batches = 0;  // drop the first N batches undecoded (resume after a restart)
 };
 
 struct Slot {
@@ -60,9 +61,15 @@ class BatchLoader {
   // at end of data.  Throws on decode/framing errors.
   int next(int* nrows, int* epoch);
   void release(int slot);
+  // Up to max_n consecutive batches in consecutive slots (a group never wraps the slot ring):
+  // blocks until all of them are decoded.  Returns the first slot and fills n (0 at end of data),
+  // the row count of the group's last batch and its epoch.
+  int next_group(int max_n, int* n, int* last_rows, int* epoch);
+  void release_group(int first, int n);
   void stop();
   size_t bad_records() const { return bad_.load(); }
   size_t records_seen() const { return seen_.load(); }
+  size_t index_fallbacks() const { return fallbacks_.load(); }  // files indexed by the sequential walk
 
   struct Chunk;  // owns the bytes (mmap or arena)
 
@@ -92,7 +99,7 @@ class BatchLoader {
   std::string error_;
   std::thread reader_;
   std::vector<std::thread> workers_;
-  std::atomic<size_t> bad_{0}, seen_{0};
+  std::atomic<size_t> bad_{0}, seen_{0}, fallbacks_{0};
   bool started_ = false;
 };
 

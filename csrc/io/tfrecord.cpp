@@ -111,14 +111,30 @@ inline int parse_int64_list(const uint8_t* p, const uint8_t* end, int32_t* dst, 
       uint64_t len;
       if (!read_varint(p, end, &len) || (uint64_t)(end - p) < len) return -1;
       const uint8_t* e2 = p + len;
+      // ids < 2^21 (any realistic vocabulary) are 1-3 byte varints: decoded without the loop;
+      // negative int64 ids read as huge unsigned values and fail the single range compare
+      const uint64_t lim = (max_id > 0 && max_id < 0x80000000LL) ? (uint64_t)max_id : 0x80000000ull;
+      bool bad = false;
       while (p < e2) {
         uint64_t v;
-        if (!read_varint(p, e2, &v)) return -1;
-        int64_t sv = (int64_t)v;
-        if (sv < 0 || (max_id > 0 && sv >= max_id) || sv > 0x7fffffffLL) *oob = true;
-        if (cnt < cap) dst[cnt] = (int32_t)sv;
+        const uint32_t b0 = p[0];
+        if (b0 < 0x80) {
+          v = b0;
+          p += 1;
+        } else if (e2 - p >= 2 && p[1] < 0x80) {
+          v = (b0 & 0x7f) | ((uint64_t)p[1] << 7);
+          p += 2;
+        } else if (e2 - p >= 3 && p[1] >= 0x80 && p[2] < 0x80) {
+          v = (b0 & 0x7f) | ((uint64_t)(p[1] & 0x7f) << 7) | ((uint64_t)p[2] << 14);
+          p += 3;
+        } else if (!read_varint(p, e2, &v)) {
+          return -1;
+        }
+        bad |= v >= lim;
+        if (cnt < cap) dst[cnt] = (int32_t)v;
         ++cnt;
       }
+      if (bad) *oob = true;
     } else if (fno == 1 && wire == 0) {
       uint64_t v;
       if (!read_varint(p, end, &v)) return -1;

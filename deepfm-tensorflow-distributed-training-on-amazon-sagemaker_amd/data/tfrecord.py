@@ -151,16 +151,21 @@ class TFRecordDataset:
 
     Each yielded batch is a tuple of CPU tensors living in one of ``num_slots`` pinned buffers; the
     slot is recycled when the NEXT batch is requested, so consumers must copy (e.g. an async H2D
-    copy followed by using the device tensor) before advancing the iterator twice.
+    copy followed by using the device tensor) before advancing the iterator twice.  ``hold=h``
+    delays the recycling: a batch's slot is released when batch t+h is requested (consumers that
+    keep ``h`` asynchronous copies in flight; the pool grows to keep 4 slots for the decoders).
     """
 
     def __init__(self, files: Sequence[str], field_size: int, batch_size: int, feature_size: int = 0,
                  num_epochs: int = 1, shard_count: int = 1, shard_index: int = 0, drop_remainder: bool = True,
                  num_threads: int = 4, num_slots: int = 6, verify_crc: bool = True, skip_bad: bool = False,
-                 shuffle_buffer: int = 0, seed: int = 0, stream_mode: bool = False, pin_memory: Optional[bool] = None):
+                 shuffle_buffer: int = 0, seed: int = 0, stream_mode: bool = False, pin_memory: Optional[bool] = None,
+                 hold: int = 1):
         self.files = list(files)
         self.F = int(field_size)
         self.B = int(batch_size)
+        self.hold = max(1, int(hold))
+        num_slots = max(int(num_slots), self.hold + 4)
         self.kw = dict(field_size=self.F, max_id=int(feature_size), batch_size=self.B, drop_remainder=drop_remainder,
                        num_epochs=int(num_epochs), shard_count=int(shard_count), shard_index=int(shard_index),
                        num_threads=int(num_threads), num_slots=int(num_slots), verify_crc=verify_crc,
@@ -185,17 +190,59 @@ class TFRecordDataset:
             self.loader.set_slot(i, ids.data_ptr(), vals.data_ptr(), labels.data_ptr())
             bufs.append((ids, vals, labels))
         self.loader.start()
-        prev = None
+        held = []
         try:
             while True:
                 slot, rows, epoch = self.loader.next()
-                if prev is not None:
-                    self.loader.release(prev)
+                while len(held) >= self.hold or (slot < 0 and held):
+                    self.loader.release(held.pop(0))
                 if slot < 0:
                     break
-                prev = slot
+                held.append(slot)
                 ids, vals, labels = bufs[slot]
                 yield ids[:rows], vals[:rows], labels[:rows]
+        finally:
+            self.loader.stop()
+
+    def groups(self, size: int, hold: int = 2, skip: int = 0, limit: Optional[int] = None):
+        """Iterate over groups of ``size`` consecutive batches (fewer at the end of the data) as
+        stacked views ``ids [n,B,F]``, ``vals [n,B,F]``, ``labels [n,B]`` of ONE pinned slot ring,
+        so a consumer moves a whole group with one host→device copy per tensor.  The ring holds
+        ``(hold + 2) · size`` batches; a group's slots are recycled when the group ``hold`` places
+        later is requested.  ``skip`` batches are dropped undecoded by the C++ reader (resume);
+        ``limit`` caps the number of batches yielded.  A trailing partial batch (drop_remainder
+        False) is yielded on its own as a 2-D batch."""
+        io = _io_mod()
+        if io is None:
+            raise RuntimeError("rocfm native IO module missing; run `python build.py`")
+        size, hold = max(1, int(size)), max(1, int(hold))
+        ns = (hold + 2) * size
+        kw = dict(self.kw, num_slots=ns, skip_batches=int(skip))
+        self.loader = io.BatchLoader(self.files, **kw)
+        B, F = self.B, self.F
+        ids = torch.zeros(ns, B, F, dtype=torch.int32, pin_memory=self.pin)
+        vals = torch.zeros(ns, B, F, dtype=torch.float32, pin_memory=self.pin)
+        labels = torch.zeros(ns, B, dtype=torch.float32, pin_memory=self.pin)
+        for i in range(ns):
+            self.loader.set_slot(i, ids[i].data_ptr(), vals[i].data_ptr(), labels[i].data_ptr())
+        self.loader.start()
+        held = []
+        left = -1 if limit is None else int(limit)
+        try:
+            while left != 0:
+                first, n, rows, epoch = self.loader.next_group(size if left < 0 else min(size, left))
+                while len(held) >= hold or (n == 0 and held):
+                    self.loader.release_group(*held.pop(0))
+                if n == 0:
+                    break
+                held.append((first, n))
+                left -= n if left > 0 else 0
+                full = n if rows == B else n - 1
+                if full:
+                    yield ids[first:first + full], vals[first:first + full], labels[first:first + full]
+                if full < n:
+                    last = first + n - 1
+                    yield ids[last, :rows], vals[last, :rows], labels[last, :rows]
         finally:
             self.loader.stop()
 

@@ -137,6 +137,13 @@ class Estimator:
                                shuffle_buffer=(cfg.batch_size * 8 if (training and cfg.perform_shuffle) else 0),
                                seed=cfg.seed + self.info.rank, stream_mode=bool(cfg.pipe_mode))
 
+    def _host_batches(self, ds: Iterable):
+        chk = ids_check_enabled()
+        for b in ds:
+            if chk:
+                check_ids(b[0], self.cfg.feature_size)
+            yield b
+
     def _device_batches(self, ds: Iterable):
         """Host (pinned) batches → device tensors; waits for each H2D copy before the loader may
         recycle its pinned slot (the iterator releases the previous slot on advance)."""
@@ -167,17 +174,25 @@ class Estimator:
         fast-forwards the input stream (resume after a restart without re-training consumed data;
         the reference re-reads from the start, an Estimator limitation rocfm does not copy)."""
         cfg = self.cfg
+        # single GPU + graphs: groups of S batches decoded into one pinned ring, moved by the engine
+        # with one copy per group (copy stream → HBM ring) and trained S steps per graph launch
+        stream = self.engine_name == "fused" and not hasattr(self.eng, "eng") and cfg.use_hip_graph \
+            and self.device.type == "cuda"
+        S = 16
         ds = self._dataset(files, num_epochs, training=True)
-        batches = self._device_batches(_skip(ds, skip_batches))
         limit = self._agreed_steps(ds)
         if limit is not None:
             limit = max(0, limit - skip_batches)
         if max_steps:
             limit = max_steps if limit is None else min(limit, max_steps)
-        if limit is not None:
-            batches = _take(batches, limit)
-        elif self.world > 1:
-            batches = self._lockstep(batches)
+        if stream:
+            batches = self._host_batches(ds.groups(S, hold=2, skip=skip_batches, limit=limit))
+        else:
+            batches = self._device_batches(_skip(ds, skip_batches))
+            if limit is not None:
+                batches = _take(batches, limit)
+            elif self.world > 1:
+                batches = self._lockstep(batches)
         t0 = time.time()
         last_t, last_step = t0, self.global_step
         n0 = self.global_step
@@ -189,9 +204,9 @@ class Estimator:
         wd = Watchdog(cfg.watchdog_s).start() if cfg.watchdog_s > 0 else None
         batches = _timed(batches, timer)
 
-        def after_step():
+        def after_step(step=None):
             nonlocal last_t, last_step, loss
-            step = self.global_step
+            step = self.global_step if step is None else step
             if wd is not None:
                 wd.beat()
             if prof is not None:
@@ -220,7 +235,14 @@ class Estimator:
 
         try:
             with trace_range("train"):
-                if self.engine_name == "fused":
+                if stream:
+                    # single GPU: batches staged into an HBM ring, S steps per graph launch
+                    def after_graph(first, n):
+                        for st in range(first + 1, first + n + 1):
+                            after_step(st)
+
+                    self.eng.train_stream(batches, S, after_steps=after_graph, hold=2)
+                elif self.engine_name == "fused":
                     it = self.eng.train_on(batches) if not hasattr(self.eng, "eng") else self._dp_train_on(batches)
                     for _ in it:
                         after_step()

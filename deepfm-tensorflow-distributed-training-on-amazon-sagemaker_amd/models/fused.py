@@ -686,23 +686,131 @@ class FusedDeepFM:
             self._prime_multi()
         while n > 0:
             S = min(n, self.mS)
-            q = self._mq
-            if self._m_warm < 1:
-                self._enqueue_multi(q, S)  # first run eager (code objects load outside capture)
-            else:
-                g = self._m_graphs.get((q, S))
-                if g is None:
-                    g = torch.cuda.CUDAGraph()
-                    torch.cuda.synchronize(self.device)
-                    with torch.cuda.graph(g):
-                        self._enqueue_multi(q, S)
-                    self._m_graphs[(q, S)] = g
-                g.replay()
-            self._m_warm += 1
-            self._mq ^= 1
-            self._i += S
+            self._run_multi_graph(S)
             n -= S
         self._primed = False  # the per-step path re-primes from the global step if used next
+
+    def _run_multi_graph(self, S: int) -> None:
+        """One multi-step graph of S steps (eager the first time: code objects load outside capture)."""
+        q = self._mq
+        if self._m_warm < 1:
+            self._enqueue_multi(q, S)
+        else:
+            g = self._m_graphs.get((q, S))
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(self.device)
+                with torch.cuda.graph(g):
+                    self._enqueue_multi(q, S)
+                self._m_graphs[(q, S)] = g
+            g.replay()
+        self._m_warm += 1
+        self._mq ^= 1
+        self._i += S
+
+    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1) -> int:
+        """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
+
+        Batches are copied host → HBM on a copy stream into a device ring of 4·S batch slots, two
+        graphs ahead of the graph that consumes them (a graph's side chain reads the NEXT graph's
+        batches).  A graph waits only for the copies of the batches its side chain reads, and a
+        copy only for the graph that last read its slots (three graphs back), so the host, which
+        stages copies and launches one graph per S steps, runs up to two graphs ahead of the GPU.
+        Items are single batches ``(ids [B,F], vals [B,F], labels [B])`` or groups of n ≤ S
+        consecutive batches stacked ``[n,B,F]`` (``TFRecordDataset.groups``: one copy per group).
+        The source may recycle an item's host memory once it has been advanced ``hold`` more
+        times; the copy of every such item is waited for first.  Returns the number of steps
+        trained; ``after_steps(first_step, n_steps)`` runs after each graph launch.
+        """
+        S = int(steps_per_graph)
+        R = 4 * S
+        hold = max(1, int(hold))
+        dev = self.device
+        ring = getattr(self, "_stream_ring", None)
+        if ring is None or ring[0].shape[0] != R:
+            ring = (torch.zeros(R, self.B, self.F, dtype=torch.int32, device=dev),
+                    torch.zeros(R, self.B, self.F, dtype=torch.float32, device=dev),
+                    torch.zeros(R, self.B, dtype=torch.float32, device=dev))
+            self._stream_ring = ring
+        i0 = self._i
+        # pool batch index of global step i = (start + i) % R  with start ≡ −i0 (mod R) → slot i − i0
+        self.attach_pool(*ring, start=(R - i0 % R) % R)
+        self._ring_mode_stream = True
+        copy = getattr(self, "_copy_stream", None) or torch.cuda.Stream(device=dev)
+        self._copy_stream = copy
+        it = iter(batches)
+        staged = 0  # batches copied into the ring so far
+
+        def mark(stream):
+            e = torch.cuda.Event()
+            e.record(stream)
+            return e
+
+        pending = []  # (event, host batch) kept alive until its copy has completed
+
+        def stage(k):  # copy up to k more batches; returns how many were available
+            nonlocal staged
+            got = 0
+            while got < k:
+                while len(pending) > hold - 1:  # the item `hold` back is recycled by this next()
+                    pending.pop(0)[0].synchronize()
+                b = next(it, None)
+                if b is None:
+                    break
+                ids, vals, labels = b
+                if ids.dim() == 2:
+                    ids, vals, labels = ids.unsqueeze(0), vals.unsqueeze(0), labels.unsqueeze(0)
+                n = ids.shape[0]
+                if ids.shape[1] != self.B:
+                    raise ValueError(f"batch has {ids.shape[1]} rows, engine built for {self.B}")
+                if got + n > k:
+                    raise ValueError(f"a group of {n} batches does not fit the {k - got} left of this graph (S={S})")
+                with torch.cuda.stream(copy):
+                    o = 0
+                    while o < n:  # contiguous ring slots (split at the ring's end)
+                        slot = (staged + o) % R
+                        m = min(n - o, R - slot)
+                        ring[0][slot:slot + m].copy_(ids[o:o + m], non_blocking=True)
+                        ring[1][slot:slot + m].copy_(vals[o:o + m], non_blocking=True)
+                        ring[2][slot:slot + m].copy_(labels[o:o + m], non_blocking=True)
+                        o += m
+                pending.append((mark(copy), b))
+                staged += n
+                got += n
+            return got
+
+        main = torch.cuda.current_stream(dev)
+        avail = stage(2 * S)
+        if avail == 0:
+            return 0
+        cevs = [mark(copy)]  # cevs[j]: copies read by graph j's side chain (graph j+1's batches)
+        main.wait_event(cevs[0])
+        if getattr(self, "mS", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
+            self._build_multi(S)
+            self._m_pool = self.pool_ids
+        self._prime_multi()  # prepares steps i0 .. i0+S-1 from the ring
+        evs = [mark(main)]  # evs[j + 1]: end of graph j; evs[0]: the prime
+        done, j = 0, 0
+        while done < staged:
+            n = min(S, staged - done)
+            # stage graph j+2's batches; their ring slots held graph j-2's batches, last read by
+            # graph j-3's side chain (or by the prime)
+            copy.wait_event(evs[max(0, j - 2)])
+            more = stage(S)
+            cevs.append(mark(copy))
+            main.wait_event(cevs[j])
+            self._run_multi_graph(n)
+            evs.append(mark(main))
+            if after_steps is not None:
+                after_steps(i0 + done, n)
+            done += n
+            j += 1
+            if n < S and more == 0:
+                break
+        for e0, _ in pending:
+            e0.synchronize()
+        self._primed = False
+        return done
 
     def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
         """``n`` optimisation steps from the attached pool; full step-pairs are replayed from one

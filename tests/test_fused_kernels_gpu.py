@@ -182,6 +182,31 @@ def test_multi_step_graph_equals_per_step(update):
     assert torch.equal(a.emb, b.emb)
 
 
+def test_train_stream_equals_per_step():
+    """Host batches streamed through the HBM ring + multi-step graphs (two calls, the second
+    starting mid-ring with a partial tail graph) train bit-identically to per-step training."""
+    spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[0.7, 0.8],
+                     l2_reg=1e-3)
+    hp = OptHParams(name="Adam", lr=2e-3)
+    g = torch.Generator().manual_seed(11)
+    NB, B = 45, 128
+    host = [tuple(t.pin_memory() for t in _batch(B, 39, 3000, g)) for _ in range(NB)]
+    a = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=True)
+    b = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=False)
+    seen = []
+    assert a.train_stream(iter(host[:21]), 4, after_steps=lambda s, n: seen.append((s, n))) == 21
+    assert seen[0] == (0, 4) and seen[-1] == (20, 1)
+    assert a.train_stream(iter(host[21:]), 4) == 24
+    b.attach_pool(torch.stack([h[0] for h in host]).cuda(), torch.stack([h[1] for h in host]).cuda(),
+                  torch.stack([h[2] for h in host]).cuda())
+    for _ in range(NB):
+        b.train_step()
+    torch.cuda.synchronize()
+    assert a.global_step() == b.global_step() == NB
+    assert torch.equal(a.emb, b.emb) and torch.equal(a.dense, b.dense)
+    assert torch.equal(a.emb_slots[1], b.emb_slots[1])
+
+
 def test_fp8_input_layer_matches_fp8_oracle():
     """compute_dtype=fp8: the input layer's forward GEMM runs on fp8-e4m3 MFMA with per-row /
     per-column scales; the step matches an oracle with the same quantisation (and differs from

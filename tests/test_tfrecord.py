@@ -162,3 +162,62 @@ def test_discover_files(tmp_path):
     tr = T.discover_files(str(tmp_path), "tr")
     assert [os.path.basename(x) for x in tr] == ["tr2.tfrecords", "tr1.tfrecords"] or len(tr) == 2
     assert len(T.discover_files(str(tmp_path), "va")) == 1 and len(T.discover_files(str(tmp_path), "te")) == 1
+
+
+def _big(tmp_path, n=30000, seed=5, name="big.tfrecords"):
+    """≈9.5 MB of 39-field records: the loader indexes it with ≥2 parallel framing walks."""
+    p = str(tmp_path / name)
+    labels, ids, vals = _write(p, n, F=39, seed=seed, V=1_000_000)
+    assert os.path.getsize(p) >= 8 << 20
+    return p, labels, ids, vals
+
+
+def test_parallel_index_matches_sequential_scan(tmp_path):
+    p, labels, ids, vals = _big(tmp_path)
+    for threads in (1, 3, 8):
+        ds = T.TFRecordDataset([p], 39, 1000, num_threads=threads, pin_memory=False)
+        got = _collect(ds)
+        assert len(got) == 30
+        assert np.array_equal(torch.cat([g[0] for g in got]).numpy(), ids)
+        assert np.array_equal(torch.cat([g[2] for g in got]).numpy(), labels)
+        assert ds.loader.index_fallbacks == 0
+    assert io().count_records(p) == 30000
+
+
+def test_parallel_index_corruption_falls_back_to_sequential_semantics(tmp_path):
+    p, labels, ids, vals = _big(tmp_path)
+    data = bytearray(open(p, "rb").read())
+    # corrupt a payload byte of a record in the second half (a parallel walk's range)
+    off, k = 0, 0
+    while off < len(data) * 3 // 4:
+        (n,) = struct.unpack("<Q", data[off:off + 8])
+        off += 12 + n + 4
+        k += 1
+    data[off + 12 + 3] ^= 0xFF
+    open(p, "wb").write(bytes(data))
+    with pytest.raises(RuntimeError):
+        _collect(T.TFRecordDataset([p], 39, 1000, num_threads=4, pin_memory=False))
+    ds = T.TFRecordDataset([p], 39, 1000, num_threads=4, skip_bad=True, drop_remainder=False, pin_memory=False)
+    got = _collect(ds)
+    assert ds.loader.index_fallbacks == 0 and ds.bad_records == 1  # a bad data CRC is skipped in parallel
+    keep = np.delete(ids, k, axis=0)
+    assert np.array_equal(torch.cat([g[0] for g in got]).numpy(), keep)
+
+
+def test_groups_match_batches_skip_limit_tail(tmp_path):
+    p = str(tmp_path / "g.tfrecords")
+    _, ids, _ = _write(p, 1000, seed=6)
+    ref = torch.tensor(ids[: 1000 // 16 * 16], dtype=torch.int32).view(-1, 16, 5)  # 62 batches
+    ds = T.TFRecordDataset([p], 5, 16, num_threads=3, pin_memory=False)
+    got = [(g[0].clone(), g[2].clone()) for g in ds.groups(8, hold=2)]
+    assert [g[0].shape[0] for g in got] == [8] * 7 + [6]
+    assert torch.equal(torch.cat([g[0] for g in got]), ref)
+    # skip 5 batches (dropped undecoded by the reader), then at most 20
+    got = [g[0].clone() for g in ds.groups(8, skip=5, limit=20)]
+    assert [g.shape[0] for g in got] == [8, 8, 4]
+    assert torch.equal(torch.cat(got), ref[5:25])
+    # drop_remainder=False: the partial tail batch comes alone, 2-D
+    ds = T.TFRecordDataset([p], 5, 16, drop_remainder=False, pin_memory=False)
+    got = list(ds.groups(8))
+    assert got[-1][0].shape == (1000 - 62 * 16, 5)
+    assert sum(g[0].shape[0] for g in got[:-1]) == 62
