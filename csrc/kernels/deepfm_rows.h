@@ -11,6 +11,9 @@ constexpr int kRowThreads = 512;  // 8 waves
 
 struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
   int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32, pos, amax;
+  int bnr[kMaxHidden];  // batch_norm: f32 [16][dims[l+1]] post-ReLU values r of layer l (kept for backward)
+  int bnst[kMaxHidden]; // batch_norm: f32 [2][dims[l+1]] batch mean, 1/sqrt(var + eps) of layer l
+  int bndy, bntot;      // batch_norm backward scratch: f32 [16][max dim] dy, [2][max dim] column totals
   int lda[kMaxHidden + 1];  // bf16 row stride of each activation tile
   int ldz;                  // bf16 row stride of the dz ping-pong tiles
   int prm;                  // f32 block of small parameters staged at kernel start:
@@ -57,6 +60,19 @@ struct RowsParams {
   int force_generic;           // 1: never use a compile-time-shape instantiation (tests)
   int ablate;                  // diagnostics only (results invalid): bit0 skip h0ᵀ stores, bit1 skip
                                // the FM loop, bit2 skip the phase-B weight prefetch
+  // batch_norm=True (PS:241-244, 316-338): y = γ·(r − μ_B)/√(σ²_B + ε) + β after each hidden ReLU,
+  // batch moments over ALL B rows (grid-wide reductions inside the launch; runtime-shape kernel).
+  int bn;
+  const float* bn_gamma[kMaxHidden];  // [dims[l+1]] (inside the flat dense buffer)
+  const float* bn_beta[kMaxHidden];
+  float* bn_mean[kMaxHidden];         // moving averages: updated by training, read by inference
+  float* bn_var[kMaxHidden];
+  float bn_decay, bn_eps;
+  int bn_dmax;                        // max hidden dim (stride of the scratch below)
+  float* bn_part;                     // [2·nl][gridDim][bn_dmax][2] per-workgroup partial moments
+  float* bn_grad;                     // [nl][2][bn_dmax]: Σ dy·x̂ (d γ), Σ dy (d β) of the batch
+  unsigned* bn_sync;                  // [2] grid-barrier arrival / exit counters (0 between launches)
+  int* bn_error;                      // set if a grid barrier timed out (the host check raises)
 };
 
 struct WgradParams {
@@ -81,6 +97,10 @@ struct WgradParams {
   const int64_t* step;
   float grad_scale;
   unsigned long long* stamps;  // diagnostic (nullable)
+  int bn;                      // batch_norm: emit d γ / d β of every layer from bn_grad
+  const float* bn_grad;        // [nl][2][bn_dmax] (written by deepfm_rows)
+  int bn_dmax;
+  int off_gamma[kMaxHidden], off_beta[kMaxHidden];
 };
 
 struct DenseApplyParams {

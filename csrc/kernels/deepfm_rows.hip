@@ -98,6 +98,55 @@ __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const u
   }
 }
 
+// ---- batch normalisation (batch_norm=True) -----------------------------------------------------
+// Batch moments couple every row of the batch, so the BN layers split the launch with grid-wide
+// barriers (2 per hidden layer: forward moments, backward column sums).  The launcher checks that
+// the whole grid is resident; every spin is bounded (1 s) and flags bn_error instead of hanging.
+constexpr uint64_t kBnSpinTicks = 100000000ull;  // s_memrealtime runs at 100 MHz
+typedef __attribute__((address_space(1))) unsigned bn_gu32;
+
+// Grid barrier k (0-based, in execution order) of this launch on one monotonic arrival counter:
+// every wave drains its stores, one lane per workgroup releases at agent scope (writes back this
+// XCD's L2), arrives, polls relaxed with s_sleep, then acquires (drops this CU's stale L1 lines),
+// so the partial moments other workgroups stored before the barrier are read fresh after it.
+__device__ __forceinline__ void bn_grid_sync(const RowsParams& p, unsigned k) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bn_gu32* c = (bn_gu32*)(p.bn_sync);
+    const unsigned target = (k + 1u) * gridDim.x;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kBnSpinTicks) {
+        atomicOr(p.bn_error, 1);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// After the last barrier: the last workgroup out zeroes both counters for the next launch.
+__device__ __forceinline__ void bn_grid_exit(const RowsParams& p) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bn_gu32* c = (bn_gu32*)(p.bn_sync);
+    if (__hip_atomic_fetch_add(c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Rows of workgroup w that are real batch rows (the padded tail contributes nothing).
+__device__ __forceinline__ int bn_rows(int B, int w) { return max(0, min(kRowTile, B - w * kRowTile)); }
+
 // ---- shapes ----------------------------------------------------------------------------------
 // Runtime shape: any F/K/MLP the host validated.
 struct RtShape {
@@ -437,6 +486,23 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
       const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
       const float bc = s_prm[L.prm_bias[l] + c];
+      if constexpr (!SH::kStatic) {
+        if (p.bn) {  // training: keep r = relu(z) for the batch moments; inference: moving moments
+          float* R = reinterpret_cast<float*>(smem + L.bnr[l]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float a = fmaxf(acc[i] + bc, 0.f);
+            if (!p.train)
+              a = (a - p.bn_mean[l][c]) * rsqrtf(p.bn_var[l][c] + p.bn_eps) * p.bn_gamma[l][c] + p.bn_beta[l][c];
+            if (row0 + rb + i >= p.B) a = 0.f;
+            if (p.train)
+              R[(rb + i) * Dout + c] = a;
+            else
+              O[(rb + i) * ldo + c] = f2bf(a);
+          }
+          continue;
+        }
+      }
       Philox4 bits{0u, 0u, 0u, 0u};
       if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
       float hv[4];
@@ -451,6 +517,65 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       if (p.train)
         *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+    }
+    if constexpr (!SH::kStatic) {
+      if (p.bn && p.train) {
+        // batch moments of r over all B rows: this workgroup's (mean, M2) per column → grid
+        // barrier → Chan's combination in workgroup order (deterministic) → normalise, dropout
+        lds_barrier();
+        const float* R = reinterpret_cast<const float*>(smem + L.bnr[l]);
+        float* ST = reinterpret_cast<float*>(smem + L.bnst[l]);
+        const int nv = bn_rows(p.B, blockIdx.x);
+        float2* part = reinterpret_cast<float2*>(p.bn_part) + (size_t)l * gridDim.x * p.bn_dmax;
+        for (int c = t; c < Dout; c += kRowThreads) {
+          float sm = 0.f;
+          for (int r = 0; r < nv; ++r) sm += R[r * Dout + c];
+          const float m = nv ? sm / (float)nv : 0.f;
+          float q = 0.f;
+          for (int r = 0; r < nv; ++r) {
+            const float d = R[r * Dout + c] - m;
+            q += d * d;
+          }
+          part[(size_t)blockIdx.x * p.bn_dmax + c] = make_float2(m, q);
+        }
+        bn_grid_sync(p, (unsigned)l);
+        for (int c = t; c < Dout; c += kRowThreads) {
+          float sm = 0.f;
+          for (int w = 0; w < (int)gridDim.x; ++w) sm += (float)bn_rows(p.B, w) * part[(size_t)w * p.bn_dmax + c].x;
+          const float mean = sm / (float)p.B;
+          float m2 = 0.f;
+          for (int w = 0; w < (int)gridDim.x; ++w) {
+            const float2 v = part[(size_t)w * p.bn_dmax + c];
+            const float d = v.x - mean;
+            m2 += v.y + (float)bn_rows(p.B, w) * d * d;
+          }
+          ST[c] = mean;
+          ST[Dout + c] = rsqrtf(m2 / (float)p.B + p.bn_eps);
+          if (blockIdx.x == 0) {  // moving averages; the variance one is unbiased (TF fused BN)
+            p.bn_mean[l][c] = p.bn_mean[l][c] * p.bn_decay + mean * (1.f - p.bn_decay);
+            p.bn_var[l][c] = p.bn_var[l][c] * p.bn_decay + (m2 / (float)max(p.B - 1, 1)) * (1.f - p.bn_decay);
+          }
+        }
+        lds_barrier();
+        for (int it = t; it < (kRowTile / 4) * Dout; it += kRowThreads) {
+          const int rg = it / Dout, c = it - rg * Dout;
+          Philox4 bits{0u, 0u, 0u, 0u};
+          if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + 4 * rg) >> 2, (uint32_t)c);
+          const float mean = ST[c], rstd = ST[Dout + c], ga = p.bn_gamma[l][c], be = p.bn_beta[l][c];
+          float hv[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * rg + i;
+            float a = (R[r * Dout + c] - mean) * rstd * ga + be;
+            if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
+            if (row0 + r >= p.B) a = 0.f;
+            hv[i] = a;
+            O[r * ldo + c] = f2bf(a);
+          }
+          *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + 4 * rg) =
+              make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+        }
+      }
     }
   }
   lds_barrier();
@@ -507,7 +632,85 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   uint16_t* dz_cur = reinterpret_cast<uint16_t*>(smem + L.dzA);
   uint16_t* dz_nxt = reinterpret_cast<uint16_t*>(smem + L.dzB);
   const int ldz = L.ldz;
-  {
+  // batch-norm backward of hidden layer l from dy (LDS, gradient w.r.t. the BN output before
+  // dropout): column sums Σdy, Σdy·x̂ over the batch (grid barrier), then
+  // dz = 1[r > 0]·γ·rstd·(dy − mean(dy) − x̂·mean(dy·x̂)) → bf16 tile `dst` + dzT[l+1]
+  auto bn_backward = [&](int l, uint16_t* dst) {
+    lds_barrier();
+    const int D = sh.dim(l + 1);
+    const float* R = reinterpret_cast<const float*>(smem + L.bnr[l]);
+    const float* ST = reinterpret_cast<const float*>(smem + L.bnst[l]);
+    const float* DY = reinterpret_cast<const float*>(smem + L.bndy);
+    float* TOT = reinterpret_cast<float*>(smem + L.bntot);
+    const int nv = bn_rows(p.B, blockIdx.x);
+    const int kb = NL + (NL - 1 - l);
+    float2* part = reinterpret_cast<float2*>(p.bn_part) + (size_t)kb * gridDim.x * p.bn_dmax;
+    for (int c = t; c < D; c += kRowThreads) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < nv; ++r) {
+        const float dy = DY[r * D + c];
+        s1 += dy;
+        s2 += dy * (R[r * D + c] - ST[c]) * ST[D + c];
+      }
+      part[(size_t)blockIdx.x * p.bn_dmax + c] = make_float2(s1, s2);
+    }
+    bn_grid_sync(p, (unsigned)kb);
+    for (int c = t; c < D; c += kRowThreads) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int w = 0; w < (int)gridDim.x; ++w) {
+        const float2 v = part[(size_t)w * p.bn_dmax + c];
+        s1 += v.x;
+        s2 += v.y;
+      }
+      TOT[c] = s1 / (float)p.B;
+      TOT[D + c] = s2 / (float)p.B;
+      if (blockIdx.x == 0) {
+        p.bn_grad[(size_t)(2 * l) * p.bn_dmax + c] = s2;      // d γ
+        p.bn_grad[(size_t)(2 * l + 1) * p.bn_dmax + c] = s1;  // d β
+      }
+    }
+    lds_barrier();
+    for (int it = t; it < (kRowTile / 4) * D; it += kRowThreads) {
+      const int rg = it / D, c = it - rg * D;
+      const float mean = ST[c], rstd = ST[D + c], gs = p.bn_gamma[l][c] * rstd;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * rg + i;
+        const float rv = R[r * D + c];
+        const float xh = (rv - mean) * rstd;
+        const float dz = gs * (DY[r * D + c] - TOT[c] - xh * TOT[D + c]);
+        v[i] = (rv > 0.f && row0 + r < p.B) ? dz : 0.f;
+        dst[r * ldz + c] = f2bf(v[i]);
+      }
+      *reinterpret_cast<uint2*>(p.dzT[l + 1] + (size_t)c * Bp + row0 + 4 * rg) =
+          make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    }
+  };
+  bool bn_head = false;
+  if constexpr (!SH::kStatic) {
+    if (p.bn) {  // dy of the last hidden layer's BN output: g·w_out through its dropout mask
+      const int l = NL - 1, Dn = sh.dim(NL);
+      float* DY = reinterpret_cast<float*>(smem + L.bndy);
+      const float keep = p.keep[l], inv_keep = 1.f / keep;
+      const bool drop = keep < 1.f;
+      for (int it = t; it < (kRowTile / 4) * Dn; it += kRowThreads) {
+        const int rg = it / Dn, c = it - rg * Dn;
+        Philox4 bits{0u, 0u, 0u, 0u};
+        if (drop) bits = dropout_bits(p.seed, (uint32_t)l, step, (uint32_t)(row0 + 4 * rg) >> 2, (uint32_t)c);
+        const float wc = s_prm[L.prm_wout + c];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rg + i;
+          const bool kept = !drop || keep_from_bits(pick4(bits, i), keep);
+          DY[r * Dn + c] = kept ? s_g[r] * wc * inv_keep : 0.f;
+        }
+      }
+      bn_backward(l, dz_cur);
+      bn_head = true;
+    }
+  }
+  if (!bn_head) {
     const int a = NL, Dn = sh.dim(a);
     const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[a]);
     const int ldh = L.lda[a];
@@ -567,6 +770,19 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const f32x4 acc = accs[j];
         const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
         if (li >= 1) {
+          if constexpr (!SH::kStatic) {
+            if (p.bn) {  // gradient w.r.t. layer li-1's BN output, through its dropout mask
+              float* DY = reinterpret_cast<float*>(smem + L.bndy);
+              const float keep = p.keep[li - 1], inv_keep = 1.f / keep;
+              const bool drop = keep < 1.f;
+              Philox4 bits{0u, 0u, 0u, 0u};
+              if (drop) bits = dropout_bits(p.seed, (uint32_t)(li - 1), step, (uint32_t)(row0 + rb) >> 2, (uint32_t)c);
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                DY[(rb + i) * Din + c] = (!drop || keep_from_bits(pick4(bits, i), keep)) ? acc[i] * inv_keep : 0.f;
+              continue;
+            }
+          }
           const uint16_t* H = reinterpret_cast<const uint16_t*>(smem + L.act[li]);
           const int ldh = L.lda[li];
           const float inv_keep = 1.f / p.keep[li - 1];
@@ -584,6 +800,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           for (int i = 0; i < 4; ++i) s_f32[(rb + i) * D0p + c] = acc[i];
         }
       }
+    }
+    if constexpr (!SH::kStatic) {
+      if (p.bn && li >= 1) bn_backward(li - 1, dz_nxt);
     }
     uint16_t* tmp = dz_cur;
     dz_cur = dz_nxt;
@@ -625,6 +844,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   lds_barrier();
   ROWS_STAMP(12);
+  if constexpr (!SH::kStatic) {
+    if (p.bn) bn_grid_exit(p);
+  }
   if (p.stamps != nullptr) {
     lds_barrier();
     if (t < 13) p.stamps[blockIdx.x * 16 + t] = s_stamp[t];
@@ -634,7 +856,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 // ------------------------------------------------------------------------------------------------
 static int align16(int x) { return (x + 15) & ~15; }
 
-RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
   RowsLds L{};
   int off = 0;
   auto take = [&](int bytes) {
@@ -665,6 +887,14 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K) {
     L.dzB = take(kRowTile * L.ldz * 2);
   }
   L.f32 = take(kRowTile * dims[0] * 4);
+  if (bn) {
+    for (int l = 0; l < nl; ++l) {
+      L.bnr[l] = take(kRowTile * dims[l + 1] * 4);
+      L.bnst[l] = take(2 * dims[l + 1] * 4);
+    }
+    L.bndy = take(kRowTile * maxh * 4);
+    L.bntot = take(2 * maxh * 4);
+  }
   int n = 0;
   for (int l = 0; l < nl; ++l) {
     L.prm_bias[l] = n;
@@ -695,6 +925,17 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
     attr_set = true;
   }
   ROCFM_REQUIRE(p.lds.total <= max_dyn, "deepfm_rows: LDS layout exceeds the 160 KiB per workgroup");
+  if (p.bn && p.train) {  // grid barriers: every workgroup must be resident at once
+    int per_cu = 0, dev = 0, cus = 0;
+    ROCFM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>), kRowThreads, p.lds.total));
+    ROCFM_HIP_CHECK(hipGetDevice(&dev));
+    ROCFM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    // the occupancy query can over-report by one block per CU: trust one fewer when it says > 1
+    const int limit = cus * (per_cu > 1 ? per_cu - 1 : per_cu);
+    ROCFM_REQUIRE(p.Bp / kRowTile <= limit, "deepfm_rows: batch_norm needs every workgroup of the batch resident "
+                                            "at once (batch too large for one launch; use engine=torch)");
+  }
   hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
                      p);
 }
@@ -723,10 +964,14 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Bp % kRowTile == 0 && p.Bp >= p.B, "deepfm_rows: Bp must be a multiple of 16 and >= B");
   ROCFM_REQUIRE((p.Bp % 64) == 0 || !p.train, "deepfm_rows: training needs Bp % 64 == 0");
   p.magicF = (uint32_t)((1ull << 32) / (uint64_t)p.F + 1ull);
-  p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K);
+  p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
   if (p.Bp / kRowTile == 0) return;
-  if (!p.force_generic) {
+  if (p.bn && p.train) {
+    ROCFM_REQUIRE(p.bn_part && p.bn_grad && p.bn_sync && p.bn_error, "deepfm_rows: batch_norm buffers missing");
+    for (int a = 1; a <= p.nl; ++a) ROCFM_REQUIRE(p.dims[a] <= p.bn_dmax, "deepfm_rows: bn_dmax < hidden dim");
+  }
+  if (!p.force_generic && !p.bn) {
     if (try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
         try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream)) {
       ROCFM_HIP_CHECK(hipGetLastError());

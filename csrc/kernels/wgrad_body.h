@@ -175,6 +175,13 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
       emit(p, st, p.off_bout, tot);
       emit(p, st, p.off_fmb, tot);
     }
+    if (p.bn) {  // batch_norm γ / β: column sums already reduced over the batch by deepfm_rows
+      for (int l = 0; l < p.nl; ++l)
+        for (int c = t; c < p.dims[l + 1]; c += kWgThreads) {
+          emit(p, st, p.off_gamma[l] + c, p.bn_grad[(size_t)(2 * l) * p.bn_dmax + c] * p.grad_scale);
+          emit(p, st, p.off_beta[l] + c, p.bn_grad[(size_t)(2 * l + 1) * p.bn_dmax + c] * p.grad_scale);
+        }
+    }
   }
 }
 

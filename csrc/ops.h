@@ -20,7 +20,7 @@ void launch_frag_probe(const uint16_t* W, int K, int swz, int nblocks, unsigned 
                        hipStream_t stream);
 
 // deepfm_rows.hip
-RowsLds rows_lds_layout(const int* dims, int nl, int F, int K);
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0);
 void launch_deepfm_rows(RowsParams p, hipStream_t stream);
 
 // mlp_wgrad.hip

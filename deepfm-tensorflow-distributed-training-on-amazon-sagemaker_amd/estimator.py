@@ -8,7 +8,7 @@
     est.train_and_evaluate(tr, va)        # per-epoch train + all-rank eval (fixes Q7/Q8/Q13)
 
 Engines: ``fused`` — the MI355X HIP path (rocfm.models.fused, one graph-replayed step per batch),
-``torch`` — eager PyTorch (CPU, batch_norm, or the GPU baseline); ``auto`` picks fused on a GPU
+``torch`` — eager PyTorch (CPU, batch_norm beyond 4096 rows per GPU, or the GPU baseline); ``auto`` picks fused on a GPU
 when the config allows it.  Multi-process runs (torchrun, one process per GPU) use data
 parallelism (rocfm.parallel.dp); only rank 0 writes checkpoints/exports (HVD:402-415, 490).
 """
@@ -80,8 +80,11 @@ class Estimator:
     def _pick_engine(self) -> str:
         e = self.cfg.engine
         if e == "auto":
-            ok = (self.device.type == "cuda" and has_hip() and not self.cfg.batch_norm and len(self.spec.layers) <= 6
-                  and self.spec.embedding_size <= 63 and self.spec.field_size <= 64)
+            # batch_norm runs fused while the batch's row-kernel grid fits on the chip at once (its
+            # moments are reduced with grid barriers): ≤ 4096 rows per GPU
+            ok = (self.device.type == "cuda" and has_hip() and len(self.spec.layers) <= 6
+                  and self.spec.embedding_size <= 63 and self.spec.field_size <= 64
+                  and not (self.cfg.batch_norm and self.cfg.batch_size > 4096))
             return "fused" if ok else "torch"
         if e == "fused" and self.device.type != "cuda":
             raise ValueError("engine=fused needs a GPU")
@@ -204,26 +207,29 @@ class Estimator:
         wd = Watchdog(cfg.watchdog_s).start() if cfg.watchdog_s > 0 else None
         batches = _timed(batches, timer)
 
-        def after_step(step=None):
+        def log_line(step, value):
             nonlocal last_t, last_step, loss
+            loss = value
+            if faults.corrupt_loss(step):
+                loss = float("nan")
+            if numerics_check_enabled():
+                check_finite(loss, step)
+            now = time.time()
+            eps = (step - last_step) * cfg.batch_size * self.world / max(now - last_t, 1e-9)
+            _, stall = timer.lap()
+            last_t, last_step = now, step
+            self._log({"event": "train", "global_step": step, "loss": loss, "examples_per_sec": eps,
+                       "examples_per_sec_per_gpu": eps / self.world, "lr": self.hp.lr * self._lr_scale,
+                       "input_stall": round(stall, 4)})
+
+        def after_step(step=None, log=True):
             step = self.global_step if step is None else step
             if wd is not None:
                 wd.beat()
             if prof is not None:
                 prof.step(step)
-            if cfg.log_steps and step % cfg.log_steps == 0:
-                loss = self.batch_loss()
-                if faults.corrupt_loss(step):
-                    loss = float("nan")
-                if numerics_check_enabled():
-                    check_finite(loss, step)
-                now = time.time()
-                eps = (step - last_step) * cfg.batch_size * self.world / max(now - last_t, 1e-9)
-                _, stall = timer.lap()
-                last_t, last_step = now, step
-                self._log({"event": "train", "global_step": step, "loss": loss, "examples_per_sec": eps,
-                           "examples_per_sec_per_gpu": eps / self.world, "lr": self.hp.lr * self._lr_scale,
-                           "input_stall": round(stall, 4)})
+            if log and cfg.log_steps and step % cfg.log_steps == 0:
+                log_line(step, self.batch_loss())
             if cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0:
                 self.save()
             elif cfg.save_checkpoints_secs and time.time() - self._last_save_t > cfg.save_checkpoints_secs:
@@ -236,12 +242,27 @@ class Estimator:
         try:
             with trace_range("train"):
                 if stream:
-                    # single GPU: batches staged into an HBM ring, S steps per graph launch
+                    # single GPU: batches staged into an HBM ring, S steps per graph launch.  Loss
+                    # logging must not drain the queue of launched graphs: the loss after the graph
+                    # that crosses a log_steps boundary is fetched asynchronously and logged (with
+                    # that graph's last step) once ready.
+                    pend = []
+
+                    def flush(block):
+                        while pend and (block or pend[0][1].query()):
+                            st, ev, host = pend.pop(0)
+                            ev.synchronize()
+                            log_line(st, float(host[0]))
+
                     def after_graph(first, n):
                         for st in range(first + 1, first + n + 1):
-                            after_step(st)
+                            after_step(st, log=False)
+                        if cfg.log_steps and (first + n) // cfg.log_steps > first // cfg.log_steps:
+                            pend.append((first + n, *self.eng.loss_async()))
+                        flush(False)
 
                     self.eng.train_stream(batches, S, after_steps=after_graph, hold=2)
+                    flush(True)
                 elif self.engine_name == "fused":
                     it = self.eng.train_on(batches) if not hasattr(self.eng, "eng") else self._dp_train_on(batches)
                     for _ in it:
@@ -252,6 +273,8 @@ class Estimator:
                         after_step()
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
+                if hasattr(self.eng, "check"):  # sticky device error flags (exchange overflow, BN barrier)
+                    self.eng.check()
         finally:
             if wd is not None:
                 wd.stop()

@@ -62,6 +62,14 @@ class DenseLayout:
         off += 1
         self.off_fmb = off
         off += 1
+        # batch_norm: trainable γ / β per hidden layer (padded columns: γ 1, β 0 — they stay 0)
+        self.off_gamma, self.off_beta = [], []
+        if spec.batch_norm:
+            for l in range(self.nl):
+                self.off_gamma.append(off)
+                off += self.dims[l + 1]
+                self.off_beta.append(off)
+                off += self.dims[l + 1]
         self.total = (off + 3) // 4 * 4
 
     def views(self, flat: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
@@ -72,6 +80,9 @@ class DenseLayout:
             W = flat[self.offW[l]:self.offW[l] + self.dims[l] * self.dims[l + 1]].view(self.dims[l], self.dims[l + 1])
             v[wn] = W[: self.real[l], : self.real[l + 1]]
             v[bn] = flat[self.offb[l]:self.offb[l] + self.real[l + 1]]
+            if self.spec.batch_norm:
+                v[f"Deep-part/bn_{l}/beta"] = flat[self.off_beta[l]:self.off_beta[l] + self.real[l + 1]]
+                v[f"Deep-part/bn_{l}/gamma"] = flat[self.off_gamma[l]:self.off_gamma[l] + self.real[l + 1]]
         wn, bn = mlp_names(self.spec)[-1]
         v[wn] = flat[self.off_wout:self.off_wout + self.real[self.nl]].view(-1, 1)
         v[bn] = flat[self.off_bout:self.off_bout + 1]
@@ -101,8 +112,6 @@ class FusedDeepFM:
                  params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
                  use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None,
                  force_generic_kernels: bool = False, compute_dtype: str = "bf16"):
-        if spec.batch_norm:
-            raise ValueError("the fused engine does not implement batch_norm; use engine=torch")
         if len(spec.layers) > 6:
             raise ValueError("the fused engine supports at most 6 hidden layers")
         self.H = require_hip()
@@ -144,6 +153,22 @@ class FusedDeepFM:
         L.pack({k: v.to(dev) for k, v in P.items() if k not in ("fm_w", "fm_v")}, self.dense)
         self.emb_slots = init_slots(hp, self.emb)
         self.dense_slots = init_slots(hp, self.dense)
+        # batch_norm: moving moments [layer][mean|var][column] (pads: mean 0, var 1) + the row
+        # kernel's grid-reduction scratch (per-barrier partials, γ/β gradient sums, counters)
+        self.bn = bool(spec.batch_norm)
+        self.bn_dmax = max(L.dims[1:])
+        if self.bn:
+            self.bn_stats = torch.zeros(L.nl, 2, self.bn_dmax, dtype=torch.float32, device=dev)
+            self.bn_stats[:, 1] = 1.0
+            for l in range(L.nl):
+                n = L.real[l + 1]
+                self.bn_stats[l, 0, :n].copy_(P[f"Deep-part/bn_{l}/moving_mean"].reshape(-1))
+                self.bn_stats[l, 1, :n].copy_(P[f"Deep-part/bn_{l}/moving_variance"].reshape(-1))
+            nwg = (self.B + 127) // 128 * 128 // 16
+            self.bn_part = torch.zeros(2 * L.nl, nwg, self.bn_dmax, 2, dtype=torch.float32, device=dev)
+            self.bn_grad = torch.zeros(L.nl, 2, self.bn_dmax, dtype=torch.float32, device=dev)
+            self.bn_sync = torch.zeros(4, dtype=torch.int32, device=dev)
+            self.bn_error = torch.zeros(4, dtype=torch.int32, device=dev)
         self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         # MFMA-fragment-swizzled copies (common.h frag_swz): what the compile-time-shape row kernel loads
@@ -260,6 +285,13 @@ class FusedDeepFM:
             rp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
         for a in range(L.nl + 1):
             rp.set_act(a, self.actT[a].data_ptr(), self.dzT[a].data_ptr() if self.dzT[a] is not None else 0)
+        if self.bn:
+            rp.bn, rp.bn_decay, rp.bn_eps, rp.bn_dmax = 1, float(self.spec.batch_norm_decay), 1e-3, self.bn_dmax
+            rp.bn_part, rp.bn_grad = self.bn_part.data_ptr(), self.bn_grad.data_ptr()
+            rp.bn_sync, rp.bn_error = self.bn_sync.data_ptr(), self.bn_error.data_ptr()
+            for l in range(L.nl):
+                rp.set_bn(l, self.dense[L.off_gamma[l]:].data_ptr(), self.dense[L.off_beta[l]:].data_ptr(),
+                          self.bn_stats[l, 0].data_ptr(), self.bn_stats[l, 1].data_ptr())
         if rp.lds_bytes() > 160 * 1024 - 256:  # 256 B: the kernel's static LDS (diagnostic stamps)
             raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
         return rp
@@ -286,6 +318,10 @@ class FusedDeepFM:
         for l in range(L.nl):
             wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
             wp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
+        if self.bn:
+            wp.bn, wp.bn_grad, wp.bn_dmax = 1, self.bn_grad.data_ptr(), self.bn_dmax
+            for l in range(L.nl):
+                wp.set_bn(l, L.off_gamma[l], L.off_beta[l])
         dp = H.DenseApplyParams()
         dp.params = self.dense.data_ptr()
         dp.grads = self.dense_grads_flat.data_ptr()
@@ -891,6 +927,23 @@ class FusedDeepFM:
         loss = float(self.loss_rows[: self.B].double().mean().item())
         return loss + (self.l2_value() if include_l2 else 0.0)
 
+    def loss_async(self, include_l2: bool = True):
+        """``batch_loss()`` without draining the stream: the reduction and a copy into pinned host
+        memory are enqueued on the training stream.  Returns ``(event, host)``; ``host[0]`` holds
+        the loss once the event has completed (``event.query()`` / ``synchronize()``)."""
+        v = self.loss_rows[: self.B].double().mean()
+        if include_l2:
+            nb = 1024
+            part = torch.zeros(nb, dtype=torch.float32, device=self.device)
+            self.H.emb_sumsq(self.emb.data_ptr(), self.V * self.Kp // 4, self.Kp, self.K1, part.data_ptr(), nb,
+                             self.stream_ptr)
+            v = v + self.spec.l2_reg * 0.5 * part.double().sum()
+        host = torch.empty(1, dtype=torch.float64, pin_memory=True)
+        host.copy_(v.view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, host
+
     def last_probs(self) -> torch.Tensor:
         return self.prob[: self.B]
 
@@ -900,8 +953,10 @@ class FusedDeepFM:
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         """TF-named variables + optimizer slots + global_step (CPU tensors)."""
         torch.cuda.synchronize(self.device)
+        self.check()
         sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         tf = self._tf_views(self.emb, self.dense)
+        tf.update(self._bn_views())
         for k, v in tf.items():
             sd[k] = v.detach().cpu().clone()
         names = slot_names(self.hp.name)
@@ -919,6 +974,11 @@ class FusedDeepFM:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         with torch.no_grad():
             self._load_views(sd, "", self.emb, self.dense, strict)
+            for k, view in self._bn_views().items():
+                if k in sd:
+                    view.copy_(sd[k].to(view.device).reshape(view.shape))
+                elif strict:
+                    raise KeyError(f"checkpoint is missing {k}")
             for si, sn in enumerate(slot_names(self.hp.name)):
                 self._load_views(sd, "/" + sn, self.emb_slots[si], self.dense_slots[si], strict)
             if "global_step" in sd:
@@ -947,5 +1007,23 @@ class FusedDeepFM:
                 continue
             view.copy_(sd[key].to(view.device).reshape(view.shape))
 
+    def _bn_views(self) -> "OrderedDict[str, torch.Tensor]":
+        """batch_norm moving moments (non-trainable: no optimizer slots), TF names."""
+        v: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        if self.bn:
+            for l in range(self.layout.nl):
+                n = self.layout.real[l + 1]
+                v[f"Deep-part/bn_{l}/moving_mean"] = self.bn_stats[l, 0, :n]
+                v[f"Deep-part/bn_{l}/moving_variance"] = self.bn_stats[l, 1, :n]
+        return v
+
+    def check(self) -> None:
+        """Raise if a batch-norm grid barrier of the row kernel timed out (the step's moments are
+        then invalid; a sticky device flag, read with one small copy)."""
+        if self.bn and int(self.bn_error[0].item()) != 0:
+            raise RuntimeError("deepfm_rows: a batch_norm grid barrier timed out (not every workgroup was resident)")
+
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
-        return OrderedDict((k, v.detach().cpu().clone()) for k, v in self._tf_views(self.emb, self.dense).items())
+        tf = self._tf_views(self.emb, self.dense)
+        tf.update(self._bn_views())
+        return OrderedDict((k, v.detach().cpu().clone()) for k, v in tf.items())

@@ -57,11 +57,15 @@ def bf16(x: torch.Tensor) -> torch.Tensor:
 def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]], w_out: torch.Tensor,
                          b_out: float, fm_bias: float, ids: torch.Tensor, vals: torch.Tensor,
                          labels: torch.Tensor, K: int, keeps: List[float], masks: Optional[List[torch.Tensor]],
-                         inv_scale: float, train: bool = True, loss_type: int = 0, fp8: bool = False):
+                         inv_scale: float, train: bool = True, loss_type: int = 0, fp8: bool = False,
+                         bn: Optional[List[Dict[str, torch.Tensor]]] = None, bn_eps: float = 1e-3):
     """Forward + backward with the fused kernels' numerics, on unpadded shapes.
 
     ``emb`` [V, Kp] (cols 0..K-1 fm_v, col K fm_w); ``layers[l]`` = {W [in,out] f32, b [out]}.
-    Returns dict with prob, loss_rows, g, contrib [B*F, K+1], dW/db per layer, dw_out, d_bout.
+    ``bn[l]`` = {gamma, beta, mean, var} enables batch norm after each ReLU (batch moments when
+    training, the given moving moments otherwise); its outputs include the batch moments and the
+    γ / β gradients.  Returns dict with prob, loss_rows, g, contrib [B*F, K+1], dW/db per layer,
+    dw_out, d_bout.
     """
     B, F = ids.shape
     rows = emb[ids.long()]  # [B,F,Kp]
@@ -72,12 +76,22 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
     S = e.sum(1)
     y_lin = fm_bias + (w * x).sum(1) + 0.5 * (S * S - (e * e).sum(1)).sum(1)
     h = [bf16(e.reshape(B, F * K))]
+    bn_state = []
     for li, L in enumerate(layers):
         if fp8 and li == 0:
             z = fp8_rowcol_matmul(h[-1], bf16(L["W"])) + L["b"]
         else:
             z = h[-1] @ bf16(L["W"]) + L["b"]
         a = torch.relu(z)
+        if bn is not None:
+            if train:
+                mean, var = a.mean(0), a.var(0, unbiased=False)
+            else:
+                mean, var = bn[li]["mean"], bn[li]["var"]
+            rstd = torch.rsqrt(var + bn_eps)
+            xh = (a - mean) * rstd
+            bn_state.append((a, xh, rstd, mean, var))
+            a = xh * bn[li]["gamma"] + bn[li]["beta"]
         if train and keeps[li] < 1.0:
             a = torch.where(masks[li], a / keeps[li], torch.zeros_like(a))
         h.append(bf16(a))
@@ -94,12 +108,31 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
         return out
     nl = len(layers)
     dz = [None] * (nl + 1)
-    dz[nl] = bf16(torch.where(h[nl] > 0, g[:, None] * w_out[None, :] / keeps[nl - 1], torch.zeros_like(h[nl])))
+    dgamma, dbeta = [None] * nl, [None] * nl
+
+    def undrop(l, d):  # gradient through layer l's dropout
+        if keeps[l] < 1.0:
+            return torch.where(masks[l], d / keeps[l], torch.zeros_like(d))
+        return d
+
+    def bn_back(l, dy):  # dy: gradient w.r.t. layer l's BN output → bf16 dz of its pre-activation
+        r, xh, rstd, _, _ = bn_state[l]
+        dgamma[l], dbeta[l] = (dy * xh).sum(0), dy.sum(0)
+        dr = bn[l]["gamma"] * rstd * (dy - dy.mean(0) - xh * (dy * xh).mean(0))
+        return bf16(torch.where(r > 0, dr, torch.zeros_like(dr)))
+
+    if bn is not None:
+        dz[nl] = bn_back(nl - 1, undrop(nl - 1, g[:, None] * w_out[None, :]))
+    else:
+        dz[nl] = bf16(torch.where(h[nl] > 0, g[:, None] * w_out[None, :] / keeps[nl - 1], torch.zeros_like(h[nl])))
     dh0 = None
     for a in range(nl, 0, -1):
         dh = dz[a] @ bf16(layers[a - 1]["W"]).t()
         if a - 1 >= 1:
-            dz[a - 1] = bf16(torch.where(h[a - 1] > 0, dh / keeps[a - 2], torch.zeros_like(dh)))
+            if bn is not None:
+                dz[a - 1] = bn_back(a - 2, undrop(a - 2, dh))
+            else:
+                dz[a - 1] = bf16(torch.where(h[a - 1] > 0, dh / keeps[a - 2], torch.zeros_like(dh)))
         else:
             dh0 = dh
     de = g[:, None, None] * (S[:, None, :] - e) + dh0.reshape(B, F, K)
@@ -111,6 +144,10 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
     out["d_bout"] = g.sum()
     out["h"] = h
     out["dz"] = dz
+    if bn is not None:
+        out["dgamma"], out["dbeta"] = dgamma, dbeta
+        out["bn_mean"] = [st[3] for st in bn_state]
+        out["bn_var"] = [st[4] for st in bn_state]
     return out
 
 

@@ -444,6 +444,7 @@ class FusedDataParallel:
     def check(self) -> None:
         """Raise if a rank exported more unique rows than the exchange capacity (rows past the
         capacity would have been dropped from that step's update)."""
+        self.eng.check()
         if self.overflowed():
             raise RuntimeError(f"DP exchange overflow: a rank exported more unique rows than capacity {self.cap}; "
                                "rebuild with a larger capacity (default batch_size*field_size never overflows)")

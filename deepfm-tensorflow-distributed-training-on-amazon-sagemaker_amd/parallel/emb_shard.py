@@ -805,6 +805,7 @@ class FusedRowShard:
     def check(self) -> None:
         """Raise if any owner's request list overflowed the exchange capacity (or a request was
         routed to the wrong owner) since construction."""
+        self.eng.check()
         ov, bad = int(self.overflow.item()), int(self.bad.item())
         if ov:
             c = torch.stack(self.counts).max().item()

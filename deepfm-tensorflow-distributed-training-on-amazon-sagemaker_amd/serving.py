@@ -32,7 +32,7 @@ class Predictor:
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.params = {k: v.to(self.device) for k, v in params.items()}
         self.fused = None
-        if engine in ("auto", "fused") and self.device.type == "cuda" and not self.spec.batch_norm:
+        if engine in ("auto", "fused") and self.device.type == "cuda":
             from .ops import has_hip
 
             if has_hip():

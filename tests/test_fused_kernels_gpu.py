@@ -235,3 +235,97 @@ def test_fp8_input_layer_matches_fp8_oracle():
     for l in range(3):
         dW = before[f"Deep-part/mlp{l}/weights"] - after[f"Deep-part/mlp{l}/weights"]
         torch.testing.assert_close(dW, ref8["dW"][l], rtol=3e-2, atol=3e-5)
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def _bn_spec(layers, keep):
+    return ModelSpec(feature_size=5000, field_size=39, embedding_size=10, layers=layers,
+                     keep_probs=[keep] * len(layers), l2_reg=1e-3, batch_norm=True, batch_norm_decay=0.9)
+
+
+def _bn_params(spec, seed):
+    P = init_params(spec, seed)
+    g = torch.Generator().manual_seed(seed)
+    for i in range(len(spec.layers)):  # non-trivial γ / β / moving moments
+        n = spec.layers[i]
+        P[f"Deep-part/bn_{i}/gamma"] = 0.5 + torch.rand(n, generator=g)
+        P[f"Deep-part/bn_{i}/beta"] = 0.2 * torch.rand(n, generator=g) - 0.1
+        P[f"Deep-part/bn_{i}/moving_mean"] = 0.1 * torch.rand(n, generator=g)
+        P[f"Deep-part/bn_{i}/moving_variance"] = 0.5 + torch.rand(n, generator=g)
+    return P
+
+
+@pytest.mark.parametrize("layers,keep", [([128, 64, 32], 0.5), ([64, 32], 1.0)])
+def test_fused_batch_norm_matches_oracle(layers, keep):
+    """batch_norm=True on the fused row kernel (batch moments via in-launch grid reductions):
+    forward, MLP / γ / β / embedding gradients and the moving-moment updates match the fp32
+    oracle with the same bf16 rounding points and dropout masks; inference uses the moving
+    moments.  B=192 leaves 4 all-padding workgroups in the grid."""
+    dev = torch.device("cuda")
+    spec = _bn_spec(layers, keep)
+    B, K = 192, 10
+    P = _bn_params(spec, 7)
+    eng = FusedDeepFM(spec, OptHParams(name="GD", lr=1.0), B, dev, params=P, use_graph=False)
+    gen = torch.Generator().manual_seed(2)
+    ids, vals, labels = _batch(B, 39, 5000, gen)
+    emb, lays, w_out, b_out, fmb, masks = _ref_inputs(eng, spec, 0, spec.keep_probs)
+    bn = [{"gamma": P[f"Deep-part/bn_{i}/gamma"], "beta": P[f"Deep-part/bn_{i}/beta"]} for i in range(len(layers))]
+    before = eng.parameters_tf()
+    eng.load_batch(ids.to(dev), vals.to(dev), labels.to(dev))
+    eng.train_step()
+    torch.cuda.synchronize()
+    eng.check()
+    ref = R.fused_step_reference(emb, lays, w_out, b_out, fmb, ids, vals, labels, K, spec.keep_probs, masks,
+                                 1.0 / B, train=True, bn=bn)
+    # BN rescales each column to unit variance, so a 1-ulp bf16 flip of an activation (f32
+    # accumulation order differs between MFMA and the oracle) moves outputs more than without BN:
+    # compare by relative norm, which a wrong moment / gradient formula would miss by far
+    errs = {"prob": _rel(eng.prob[:B].cpu(), ref["prob"])}
+    after = eng.parameters_tf()
+    for l in range(len(layers)):
+        for name, key in ((f"mlp{l}/weights", "dW"), (f"mlp{l}/biases", "db"), (f"bn_{l}/gamma", "dgamma"),
+                          (f"bn_{l}/beta", "dbeta")):
+            d = before[f"Deep-part/{name}"] - after[f"Deep-part/{name}"]
+            errs[name] = _rel(d, ref[key][l])
+        mm = 0.9 * before[f"Deep-part/bn_{l}/moving_mean"] + 0.1 * ref["bn_mean"][l]
+        mv = 0.9 * before[f"Deep-part/bn_{l}/moving_variance"] + 0.1 * ref["bn_var"][l] * B / (B - 1)
+        torch.testing.assert_close(after[f"Deep-part/bn_{l}/moving_mean"], mm, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(after[f"Deep-part/bn_{l}/moving_variance"], mv, rtol=1e-4, atol=1e-5)
+    uniq, acc = R.emb_grad_reference(ids, ref["contrib"])
+    delta = emb[:, : K + 1] - eng.emb.detach().cpu()[:, : K + 1]
+    errs["emb"] = _rel(delta[uniq], acc + spec.l2_reg * emb[uniq, : K + 1])
+    bad = {k: v for k, v in errs.items() if not v < 2e-2}
+    assert not bad, f"relative errors vs the oracle: {errs}"
+    # inference: the moving moments, no dropout
+    emb2, lays2, w2, b2, f2, _ = _ref_inputs(eng, spec, 0, [1.0] * len(layers))
+    bn2 = [{"gamma": after[f"Deep-part/bn_{i}/gamma"], "beta": after[f"Deep-part/bn_{i}/beta"],
+            "mean": after[f"Deep-part/bn_{i}/moving_mean"], "var": after[f"Deep-part/bn_{i}/moving_variance"]}
+           for i in range(len(layers))]
+    prob, _ = eng.predict_batch(ids[:100].to(dev), vals[:100].to(dev))
+    ref2 = R.fused_step_reference(emb2, lays2, w2, b2, f2, ids[:100], vals[:100], labels[:100], K,
+                                  [1.0] * len(layers), None, 1.0 / 100, train=False, bn=bn2)
+    assert _rel(prob.cpu(), ref2["prob"]) < 2e-3
+
+
+def test_fused_batch_norm_multistep_graph_equals_per_step():
+    """Grid-barrier counters reset between launches: multi-step graph replays of the batch-norm
+    row kernel train bit-identically to per-step eager launches."""
+    spec = _bn_spec([64, 32], 0.7)
+    g = torch.Generator().manual_seed(4)
+    pool = [_batch(128, 39, 5000, g) for _ in range(5)]
+    ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
+    hp = OptHParams(name="Adam", lr=2e-3)
+    a = FusedDeepFM(spec, hp, 128, "cuda", params=_bn_params(spec, 3), use_graph=True)
+    b = FusedDeepFM(spec, hp, 128, "cuda", params=_bn_params(spec, 3), use_graph=False)
+    a.attach_pool(ids, vals, labels)
+    b.attach_pool(ids, vals, labels)
+    a.train_steps(21, 8)
+    for _ in range(21):
+        b.train_step()
+    torch.cuda.synchronize()
+    a.check()
+    b.check()
+    assert torch.equal(a.dense, b.dense) and torch.equal(a.emb, b.emb) and torch.equal(a.bn_stats, b.bn_stats)

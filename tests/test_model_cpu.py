@@ -157,3 +157,39 @@ def test_fused_reference_gradients_vs_autograd():
     torch.nn.functional.binary_cross_entropy_with_logits(y, labels).backward()
     torch.testing.assert_close(ref["dW"][0], Q["Deep-part/mlp0/weights"].grad, rtol=0.05, atol=2e-3)
     torch.testing.assert_close(ref["dw_out"], Q["Deep-part/deep_out/weights"].grad.reshape(-1), rtol=0.05, atol=2e-3)
+
+
+def test_fused_reference_batch_norm_vs_autograd():
+    """The kernel oracle's batch-norm forward/backward (batch moments, γ/β gradients, dz through
+    the normalisation) equals autograd of the f32 DeepFM with batch_norm=True."""
+    spec = _spec(feature_size=40, layers=[16, 8])
+    spec.batch_norm = True
+    P = init_params(spec, 5)
+    with torch.no_grad():  # non-trivial γ / β
+        for i in range(2):
+            P[f"Deep-part/bn_{i}/gamma"].uniform_(0.5, 1.5)
+            P[f"Deep-part/bn_{i}/beta"].uniform_(-0.2, 0.2)
+    ids, vals, labels = _batch(spec, 24)
+    K = spec.embedding_size
+    emb = torch.zeros(40, 8)
+    emb[:, :K] = P["fm_v"]
+    emb[:, K] = P["fm_w"]
+    layers = [{"W": P[f"Deep-part/mlp{i}/weights"], "b": P[f"Deep-part/mlp{i}/biases"]} for i in range(2)]
+    bn = [{"gamma": P[f"Deep-part/bn_{i}/gamma"], "beta": P[f"Deep-part/bn_{i}/beta"]} for i in range(2)]
+    w_out = P["Deep-part/deep_out/weights"].reshape(-1)
+    ref = R.fused_step_reference(emb, layers, w_out, 0.0, 0.0, ids, vals, labels, K, [1.0, 1.0], None, 1.0 / 24,
+                                 bn=bn)
+    names = ["Deep-part/mlp0/weights", "Deep-part/mlp1/biases", "Deep-part/bn_0/gamma", "Deep-part/bn_1/beta",
+             "Deep-part/bn_0/beta", "Deep-part/bn_1/gamma"]
+    Q = {k: v.clone().requires_grad_(k in names) for k, v in P.items()}
+    y = forward(Q, ids, vals, spec, train=True)
+    torch.nn.functional.binary_cross_entropy_with_logits(y, labels).backward()
+    tol = dict(rtol=0.06, atol=3e-3)
+    torch.testing.assert_close(ref["dW"][0], Q[names[0]].grad, **tol)
+    torch.testing.assert_close(ref["db"][1], Q[names[1]].grad, **tol)
+    torch.testing.assert_close(ref["dgamma"][0], Q[names[2]].grad, **tol)
+    torch.testing.assert_close(ref["dbeta"][1], Q[names[3]].grad, **tol)
+    torch.testing.assert_close(ref["dbeta"][0], Q[names[4]].grad, **tol)
+    torch.testing.assert_close(ref["dgamma"][1], Q[names[5]].grad, **tol)
+    # the oracle's probabilities match the model's training-mode forward
+    torch.testing.assert_close(ref["prob"], torch.sigmoid(y.detach()), rtol=2e-2, atol=2e-3)
