@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--steps_per_graph", type=int, default=16, help="fused engine: steps captured per HIP graph")
+    ap.add_argument("--steps_per_graph", type=int, default=64, help="fused engine: steps captured per HIP graph")
     ap.add_argument("--capacity", default="auto",
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
                          "over the batch pool, 'safe' = batch_size*field_size (never overflows), or a number")
@@ -178,6 +178,8 @@ def main():
         eng.set_lr_scale(float(world))  # Horovod linear LR scaling (HVD:171)
 
     run(a.warmup)
+    if hasattr(eng, "precapture"):
+        eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

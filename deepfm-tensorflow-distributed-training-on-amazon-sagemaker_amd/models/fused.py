@@ -601,14 +601,20 @@ class FusedDeepFM:
     # 47 vs 55 µs/step); ONE side chain per graph prepares the NEXT graph's S batches (one copy
     # kernel) and sorts all S·B·F lookups at once (composite key batch << id_bits | id), joined
     # at the graph's end.
+    def _multi_S(self, Smax: int, shard: Optional[tuple] = None):
+        """(id bits, steps per graph): the composite sort key batch << id_bits | id is 32-bit,
+        so S is clamped to 2^(32 - id_bits)."""
+        key_range = self.V if shard is None else shard[0] * shard[1]
+        idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
+        return idbits, max(1, min(int(Smax), 1 << max(0, 32 - idbits)))
+
     def _build_multi(self, Smax: int, shard: Optional[tuple] = None) -> None:
         """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
         self._m_shard = shard
-        key_range = self.V if shard is None else shard[0] * shard[1]
-        idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
-        Smax = max(1, min(int(Smax), 1 << max(0, 32 - idbits)))
+        self.m_req = int(Smax)  # requested S (mS may be clamped below it by the key width)
+        idbits, Smax = self._multi_S(Smax, shard)
         sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
         self.mS, self.m_idbits, self.m_bits = Smax, idbits, idbits + sbits
         i32 = dict(dtype=torch.int32, device=dev)
@@ -686,22 +692,83 @@ class FusedDeepFM:
         self.m_cur[1] = base + self._i
         self.m_step[1] = self._i
         self._prepare_multi(1, 0, torch.cuda.current_stream(self.device))  # → parity-0 buffers
+        self._m_side_ev = None  # the prime ran on the main stream
         self._mq = 0
         self._m_primed = True
 
-    def _enqueue_multi(self, q: int, S: int) -> None:
-        H = self.H
-        main = torch.cuda.current_stream(self.device)
-        side = self.sort_stream
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._prepare_multi(q, S, side)
-        s = main.cuda_stream
+    def _multi_body(self, q: int, S: int) -> None:
+        """The main chain of one S-step graph: rows → tail per step, strictly serial."""
+        H, s = self.H, torch.cuda.current_stream(self.device).cuda_stream
         for k in range(S):
             rows, wp, _, ep, ed = self.m_params[q][k]
             H.deepfm_rows(rows, s)
             self._tail(wp, ep, ed, s)
-        main.wait_stream(side)
+
+    def _launch_multi(self, graphs: dict, key: tuple, S: int, body, capture_error_mode: str = "global",
+                      capture_only: bool = False) -> None:
+        """Launch one S-step multi-step graph of parity q = ``self._mq`` as TWO graphs on two streams:
+
+        * the side graph (fetch + sort of the NEXT graph's S batches into the parity 1-q buffers)
+          on the sort stream, after the previous main graph (the last reader of those buffers);
+        * the main graph ``body(q, S)`` on the current stream, after the previous side graph (the
+          producer of this graph's parity-q buffers).
+
+        Side graph N therefore runs concurrently with main graph N on its own hardware queue.  (A
+        single graph with the side chain as a forked branch was measured to run the branch AFTER
+        the main chain on ROCm 7 — ≈200 µs of sort per 16 steps exposed at every graph boundary.)
+        The first launch is eager (code objects load outside capture).  ``capture_only``: capture
+        the pair if missing and return without launching (used to keep captures out of timed
+        regions)."""
+        q = self._mq
+        main = torch.cuda.current_stream(self.device)
+        side = self.sort_stream
+        eager = self._m_warm < 1
+        gs = gm = None
+        if not eager:
+            gs, gm = graphs.get(key + (q, S, "side")), graphs.get(key + (q, S, "main"))
+            if gm is None:
+                torch.cuda.synchronize(self.device)
+                gs, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gs, capture_error_mode=capture_error_mode):
+                    self._prepare_multi(q, S, torch.cuda.current_stream(self.device))
+                with torch.cuda.graph(gm, capture_error_mode=capture_error_mode):
+                    body(q, S)
+                graphs[key + (q, S, "side")], graphs[key + (q, S, "main")] = gs, gm
+        if capture_only:
+            return
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            if eager:
+                self._prepare_multi(q, S, side)
+            else:
+                gs.replay()
+        ev = torch.cuda.Event()
+        ev.record(side)
+        if self._m_side_ev is not None:
+            main.wait_event(self._m_side_ev)
+        if eager:
+            body(q, S)
+        else:
+            gm.replay()
+        self._m_side_ev = ev
+        self._m_warm += 1
+        self._mq ^= 1
+        self._i += S
+
+    def _precapture_multi(self, graphs: dict, key: tuple, n: int, body, capture_error_mode: str = "global") -> None:
+        """Capture every (parity, S) graph pair that ``n`` more steps will launch, so that no
+        capture lands inside a timed region (e.g. the S < Smax remainder graph)."""
+        if self._m_warm < 1:
+            return
+        q0 = self._mq
+        try:
+            while n > 0:
+                S = min(n, self.mS)
+                self._launch_multi(graphs, key, S, body, capture_error_mode, capture_only=True)
+                self._mq ^= 1
+                n -= S
+        finally:
+            self._mq = q0
 
     def _tail(self, wp, ep, ed, s: int) -> None:
         """MLP weight gradients + embedding update: one launch (step_tail.hip) when the rows fit."""
@@ -715,7 +782,7 @@ class FusedDeepFM:
             H.emb_dense_update(ed, s)
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
-        if getattr(self, "mS", None) is None or self.mS != Smax or getattr(self, "_m_pool", None) is not self.pool_ids:
+        if getattr(self, "m_req", None) != Smax or getattr(self, "_m_pool", None) is not self.pool_ids:
             self._build_multi(Smax)
             self._m_pool = self.pool_ids
         if not self._m_primed:
@@ -724,25 +791,18 @@ class FusedDeepFM:
             S = min(n, self.mS)
             self._run_multi_graph(S)
             n -= S
+        torch.cuda.current_stream(self.device).wait_stream(self.sort_stream)
         self._primed = False  # the per-step path re-primes from the global step if used next
 
     def _run_multi_graph(self, S: int) -> None:
         """One multi-step graph of S steps (eager the first time: code objects load outside capture)."""
-        q = self._mq
-        if self._m_warm < 1:
-            self._enqueue_multi(q, S)
-        else:
-            g = self._m_graphs.get((q, S))
-            if g is None:
-                g = torch.cuda.CUDAGraph()
-                torch.cuda.synchronize(self.device)
-                with torch.cuda.graph(g):
-                    self._enqueue_multi(q, S)
-                self._m_graphs[(q, S)] = g
-            g.replay()
-        self._m_warm += 1
-        self._mq ^= 1
-        self._i += S
+        self._launch_multi(self._m_graphs, ("m",), S, self._multi_body)
+
+    def precapture(self, n: int, steps_per_graph: int = 16) -> None:
+        """Capture the graphs ``train_steps(n, steps_per_graph)`` will replay (no launch)."""
+        if self.use_graph and not self._ring and self.fuse_dense_opt and steps_per_graph > 1 \
+                and getattr(self, "m_req", None) == steps_per_graph and self._m_primed:
+            self._precapture_multi(self._m_graphs, ("m",), n, self._multi_body)
 
     def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1) -> int:
         """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
@@ -758,7 +818,7 @@ class FusedDeepFM:
         times; the copy of every such item is waited for first.  Returns the number of steps
         trained; ``after_steps(first_step, n_steps)`` runs after each graph launch.
         """
-        S = int(steps_per_graph)
+        S = self._multi_S(int(steps_per_graph))[1]
         R = 4 * S
         hold = max(1, int(hold))
         dev = self.device
@@ -821,28 +881,30 @@ class FusedDeepFM:
             return 0
         cevs = [mark(copy)]  # cevs[j]: copies read by graph j's side chain (graph j+1's batches)
         main.wait_event(cevs[0])
-        if getattr(self, "mS", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
+        if getattr(self, "m_req", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
             self._build_multi(S)
             self._m_pool = self.pool_ids
         self._prime_multi()  # prepares steps i0 .. i0+S-1 from the ring
-        evs = [mark(main)]  # evs[j + 1]: end of graph j; evs[0]: the prime
+        prime_ev = mark(main)
+        sevs = []  # sevs[j]: end of graph j's side chain (side graph, sort stream)
         done, j = 0, 0
         while done < staged:
             n = min(S, staged - done)
             # stage graph j+2's batches; their ring slots held graph j-2's batches, last read by
             # graph j-3's side chain (or by the prime)
-            copy.wait_event(evs[max(0, j - 2)])
+            copy.wait_event(sevs[j - 3] if j >= 3 else prime_ev)
             more = stage(S)
             cevs.append(mark(copy))
-            main.wait_event(cevs[j])
+            self.sort_stream.wait_event(cevs[j])
             self._run_multi_graph(n)
-            evs.append(mark(main))
+            sevs.append(self._m_side_ev)
             if after_steps is not None:
                 after_steps(i0 + done, n)
             done += n
             j += 1
             if n < S and more == 0:
                 break
+        main.wait_stream(self.sort_stream)
         for e0, _ in pending:
             e0.synchronize()
         self._primed = False

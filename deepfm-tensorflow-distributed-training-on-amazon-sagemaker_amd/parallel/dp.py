@@ -377,13 +377,9 @@ class FusedDataParallel:
         self._m_dp_S = Smax
 
     def _enqueue_multi_dp(self, q: int, S: int) -> None:
+        """Main chain of one S-step DP graph (the side graph is launched by FusedDeepFM._launch_multi)."""
         e, H = self.eng, self.eng.H
-        main = torch.cuda.current_stream(self.device)
-        side = e.sort_stream
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            e._prepare_multi(q, S, side)
-        s = main.cuda_stream
+        s = torch.cuda.current_stream(self.device).cuda_stream
         for k in range(S):
             rows, wp, ep, da, ed, mg = self.m_dp[q][k]
             H.deepfm_rows(rows, s)  # (dp: also zeroes the export counter)
@@ -395,7 +391,6 @@ class FusedDataParallel:
             else:
                 H.dense_apply(da, s)
                 H.emb_dense_update(ed, s)
-        main.wait_stream(side)
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         e = self.eng
@@ -405,25 +400,18 @@ class FusedDataParallel:
             e._prime_multi()
         while n > 0:
             S = min(n, e.mS)
-            q = e._mq
-            if e._m_warm < 1:
-                self._enqueue_multi_dp(q, S)  # first run eager (code objects load outside capture)
-            else:
-                key = ("mdp", q, S)
-                g = self._graphs.get(key)
-                if g is None:
-                    g = torch.cuda.CUDAGraph()
-                    torch.cuda.synchronize(self.device)
-                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                        self._enqueue_multi_dp(q, S)
-                    self._graphs[key] = g
-                g.replay()
-            e._m_warm += 1
-            e._mq ^= 1
-            e._i += S
+            e._launch_multi(self._graphs, ("mdp",), S, self._enqueue_multi_dp, capture_error_mode="thread_local")
             n -= S
             self._after_steps(e._i - S, e._i)
+        torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
         e._primed = False
+
+    def precapture(self, n: int, steps_per_graph: int = 16) -> None:
+        """Capture the graphs ``train_steps(n, steps_per_graph)`` will replay (no launch)."""
+        e = self.eng
+        if getattr(self, "_m_dp_S", None) == steps_per_graph and e._m_primed and self.graph_collectives \
+                and self.use_graph and not e._ring and steps_per_graph > 1:
+            e._precapture_multi(self._graphs, ("mdp",), n, self._enqueue_multi_dp, "thread_local")
 
     def train_steps(self, n: int, steps_per_graph: int = 16) -> None:
         """``n`` steps from the attached pool.  With capturable collectives (RCCL) the steps are

@@ -643,6 +643,13 @@ class FusedRowShard:
         if self.check_every and i1 // self.check_every != i0 // self.check_every:
             self.check()
 
+    def precapture(self, n: int, steps_per_graph: int = 16) -> None:
+        """Capture the graphs ``train_steps(n, steps_per_graph)`` will replay (no launch)."""
+        e = self.eng
+        if getattr(self, "_ms_S", None) == steps_per_graph and e._m_primed and self.graph_collectives \
+                and self.use_graph and not e._ring and steps_per_graph > 1:
+            e._precapture_multi(self._graphs, ("mrs",), n, self._enqueue_multi_rs, "thread_local")
+
     def train_steps(self, n: int, steps_per_graph: int = 16) -> None:
         e = self.eng
         if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
@@ -735,13 +742,10 @@ class FusedRowShard:
         self._ms_S = Smax
 
     def _enqueue_multi_rs(self, q: int, S: int) -> None:
+        """Main chain of one S-step row-shard graph (the side graph is launched by
+        FusedDeepFM._launch_multi)."""
         e, H = self.eng, self.H
-        main = torch.cuda.current_stream(self.device)
-        side = e.sort_stream
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            e._prepare_multi(q, S, side)
-        s = main.cuda_stream
+        s = torch.cuda.current_stream(self.device).cuda_stream
         for k in range(S):
             rows, wp, ep, da, ed, mg = self.ms_steps[q][k]
             self._exchange(self.recv_ids, self.ms_send[q, k])                   # X1 requests
@@ -756,7 +760,6 @@ class FusedRowShard:
             H.merge_apply(mg, s)
             if ed is not None:
                 H.emb_dense_update(ed, s)
-        main.wait_stream(side)
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         e = self.eng
@@ -766,24 +769,10 @@ class FusedRowShard:
             e._prime_multi()
         while n > 0:
             S = min(n, e.mS)
-            q = e._mq
-            if e._m_warm < 1:
-                self._enqueue_multi_rs(q, S)
-            else:
-                key = ("mrs", q, S)
-                g = self._graphs.get(key)
-                if g is None:
-                    g = torch.cuda.CUDAGraph()
-                    torch.cuda.synchronize(self.device)
-                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                        self._enqueue_multi_rs(q, S)
-                    self._graphs[key] = g
-                g.replay()
-            e._m_warm += 1
-            e._mq ^= 1
-            e._i += S
+            e._launch_multi(self._graphs, ("mrs",), S, self._enqueue_multi_rs, capture_error_mode="thread_local")
             n -= S
             self._after_steps(e._i - S, e._i)
+        torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
         e._primed = False
 
     def train_on(self, batches):
