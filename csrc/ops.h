@@ -11,6 +11,7 @@
 #include "kernels/shard.h"
 #include "kernels/merge.h"
 #include "kernels/metrics.h"
+#include "kernels/p2p.h"
 
 namespace rocfm {
 

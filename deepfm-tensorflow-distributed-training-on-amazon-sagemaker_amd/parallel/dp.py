@@ -138,7 +138,8 @@ class FusedDataParallel:
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", mode: str = "dp", seed: int = 1234, use_graph: bool = True,
-                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16"):
+                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
+                 exchange: Optional[str] = None):
         from ..models.fused import FusedDeepFM
 
         self.world = _world()
@@ -158,6 +159,8 @@ class FusedDataParallel:
         self.graph_collectives = use_graph and collectives_capturable()
         self.check_every = int(check_every)
         self.device = e.device
+        self.p2p = None
+        self.exchange = "rccl"  # DP all-gather transport (mode dp: _open_p2p may pick "p2p")
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
             from .dist import broadcast_tensors
@@ -184,9 +187,17 @@ class FusedDataParallel:
             self.off_cnt = P
             self.off_keys = P + 4
             self.off_rows = self.off_keys + cap
-            self.S = self.off_rows + cap * Kp
+            self.S = (self.off_rows + cap * Kp + 3) // 4 * 4  # float4 payload (p2p push)
             self.send = torch.zeros(self.S, dtype=torch.float32, device=e.device)
-            self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+            self.p2p = self._open_p2p(exchange)
+            if self.p2p is not None:  # rank slots live in the uncached, peer-mapped receive buffer
+                self.graph_collectives = use_graph  # the push kernel is capturable whatever the backend
+                self.recv = None
+                self._recv_ptr = self.p2p.recv_ptr
+                self.p2p_params = self.p2p.params(self.send.data_ptr(), self.S)
+            else:
+                self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+                self._recv_ptr = self.recv.data_ptr()
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
             # merge maps (merge.hip): position of each key in every rank's list, representative rank
@@ -208,9 +219,9 @@ class FusedDataParallel:
                 ex.out_cap = cap
                 self.export_params.append(ex)
                 mp_ = H.MergeParams()  # merge the gathered lists: Σ over ranks per id → row optimizer
-                mp_.keys = self.recv[self.off_keys:].data_ptr()
-                mp_.rows = self.recv[self.off_rows:].data_ptr()
-                mp_.counts = self.recv[self.off_cnt:].data_ptr()
+                mp_.keys = self._recv_ptr + 4 * self.off_keys
+                mp_.rows = self._recv_ptr + 4 * self.off_rows
+                mp_.counts = self._recv_ptr + 4 * self.off_cnt
                 mp_.key_stride = mp_.row_stride = mp_.count_stride = self.S
                 mp_.W, mp_.cap, mp_.Kp, mp_.K1 = self.world, cap, Kp, e.K1
                 mp_.key_div, mp_.Vmap = 1, e.V
@@ -223,10 +234,9 @@ class FusedDataParallel:
                 mp_.overflow = self.overflow.data_ptr()
                 self.merge_params.append(mp_)
                 da = e.dense_apply_params[p]
-                da.apply, da.grads, da.grad_scale = 1, self.recv.data_ptr(), 1.0 / self.world
+                da.apply, da.grads, da.grad_scale = 1, self._recv_ptr, 1.0 / self.world
                 da.nseg, da.seg_stride = self.world, self.S
             H.merge_init(self.merge_params[0], e.stream_ptr)
-            self.recv2d = self.recv.view(self.world, self.S)
         for p in range(2):
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
         self._graphs = {}
@@ -267,7 +277,36 @@ class FusedDataParallel:
             e._join(side)
         return side
 
+    def _open_p2p(self, exchange: Optional[str]):
+        """The DP all-gather transport: ``p2p`` (one-shot push over IPC-mapped peer buffers,
+        rocfm.parallel.p2p) or ``rccl``.  ``auto`` (default; env ROCFM_DP_EXCHANGE) picks p2p when
+        every rank is on this node and a self-test of the mapped buffers passes on every rank."""
+        choice = (exchange or os.environ.get("ROCFM_DP_EXCHANGE", "auto")).lower()
+        if choice not in ("auto", "p2p", "rccl"):
+            raise ValueError(f"exchange must be auto, p2p or rccl, got {choice!r}")
+        self.exchange = "rccl"
+        if self.world == 1 or choice == "rccl":
+            return None
+        from . import p2p as P
+
+        if not P.single_node():
+            if choice == "p2p":
+                raise RuntimeError("exchange=p2p needs every rank on one node")
+            return None
+        ex = P.P2PExchange(self.S, self.device)  # collective; local failures land in ex.init_error
+        if not P.selftest(ex, self.S):            # agreed by every rank
+            err = ex.init_error
+            ex.close()
+            if choice == "p2p":
+                raise RuntimeError(f"p2p exchange unavailable: {err or 'self-test failed'}")
+            return None
+        self.exchange = "p2p"
+        return ex
+
     def _exchange(self):
+        if self.p2p is not None:
+            self.p2p.push(self.p2p_params)
+            return
         if self.world == 1:  # single rank (profiling the DP step on one GPU): nothing to exchange
             if self.mode == "dp":
                 self.recv.copy_(self.send)
@@ -353,7 +392,7 @@ class FusedDataParallel:
                     ed.grad_scale = 1.0 / self.world
                     row.append((rows, wp, ep, da, ed, None))
                     continue
-                da.grads, da.nseg, da.seg_stride = self.recv.data_ptr(), self.world, self.S
+                da.grads, da.nseg, da.seg_stride = self._recv_ptr, self.world, self.S
                 ex = H.EmbUpdateParams()  # export: compacted (id, Σ grad row) into the send buffer
                 ex.skeys, ex.svals, ex.n = ep.skeys, ep.svals, n
                 ex.val_base, ex.id_offset, ex.sorted_contrib, ex.chunk_end = ep.val_base, ep.id_offset, 1, ep.chunk_end
@@ -428,11 +467,17 @@ class FusedDataParallel:
         RCCL collectives)."""
         torch.cuda.synchronize(self.device)
         self._graphs = {}
+        if self.p2p is not None:
+            self.p2p.close()
+            self.p2p = None
 
     def check(self) -> None:
         """Raise if a rank exported more unique rows than the exchange capacity (rows past the
-        capacity would have been dropped from that step's update)."""
+        capacity would have been dropped from that step's update), or if a p2p exchange wait
+        timed out (a peer never arrived: its data for that step is missing)."""
         self.eng.check()
+        if self.p2p is not None and self.p2p.errored():
+            raise RuntimeError("DP p2p exchange: a peer wait timed out (rank missing or stalled)")
         if self.overflowed():
             raise RuntimeError(f"DP exchange overflow: a rank exported more unique rows than capacity {self.cap}; "
                                "rebuild with a larger capacity (default batch_size*field_size never overflows)")

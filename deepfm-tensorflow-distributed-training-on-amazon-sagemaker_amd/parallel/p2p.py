@@ -1,0 +1,195 @@
+"""One-shot xGMI push exchange over IPC-mapped peer buffers (csrc/kernels/p2p.hip).
+
+SURVEY §5.8 item 2 / N14 / §7.2 P6.  The DP step exchanges ≈1 MB per rank per step (MLP
+gradients + compacted embedding rows, ``rocfm.parallel.dp``).  RCCL's all-gather of that bucket is
+latency-bound: on one node of fully connected xGMI a ring needs W−1 dependent hops.  Here every
+rank maps every other rank's receive buffer and flag block once (``hipIpcGetMemHandle`` /
+``hipIpcOpenMemHandle``, handles exchanged over the process group), and ONE kernel pushes the
+payload to all peers at once — W−1 links, one hop each — with a flag hand-off instead of a
+collective protocol.  The launch advances its own device-side exchange counter, so it is captured
+into the multi-step HIP graphs like any other kernel (also when the process group is gloo).
+
+Receive buffers and flags are allocated uncached (``hipDeviceMallocUncached``) so that a peer's
+writes are visible to the kernels that read them next without any L2 maintenance.  Every wait in
+the kernel is bounded: a peer that never arrives raises a sticky error flag (``errored()``)
+instead of hanging the GPU.
+
+The reference has no equivalent: Horovod hands the gradients to NCCL (HVD:296).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+KIND_UNCACHED, KIND_FINEGRAINED, KIND_PLAIN = 0, 1, 2
+
+
+def _hip():
+    from ..ops import hip
+
+    return hip()
+
+
+def single_node(group=None) -> bool:
+    """True when every rank of the group runs on this host (IPC mapping needs one node)."""
+    if not dist.is_initialized():
+        return True
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    if lw is not None and int(lw) == dist.get_world_size(group):
+        return True
+    names: List[Optional[str]] = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, os.uname().nodename, group=group)
+    return len(set(names)) == 1
+
+
+class P2PExchange:
+    """W receive slots of ``slot_floats`` f32 per rank, mapped into every peer.
+
+    ``push(params)`` launches the exchange on the current stream: destination ``d`` receives
+    ``n_floats`` floats from ``src + d * src_stride`` (``src_stride=0``: all-gather) into its
+    slot ``rank``.  After the launch completes, ``recv_ptr + r * slot_floats * 4`` holds rank r's
+    payload on every rank.
+    """
+
+    def __init__(self, slot_floats: int, device, group=None, kind: int = KIND_UNCACHED,
+                 spin_limit: int = 1 << 25):
+        H = self.H = _hip()
+        self.group = group
+        self.W = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if self.W > H.p2p_max_world():
+            raise ValueError(f"p2p exchange supports at most {H.p2p_max_world()} ranks, got {self.W}")
+        self.device = torch.device(device)
+        self.slot = (int(slot_floats) + 3) // 4 * 4
+        self.spin_limit = int(spin_limit)
+        self.kind = kind
+        self._own: List[int] = []
+        self._opened: List[int] = []
+        self.init_error: Optional[BaseException] = None
+        self.peers: List[Tuple[int, int]] = []
+        # every rank takes part in every collective below even if a step fails on it, so that a
+        # local failure becomes an agreed fallback (selftest) instead of a hang
+        mine = None
+        with torch.cuda.device(self.device):
+            self.ctrl = torch.zeros(2, dtype=torch.int32, device=self.device)   # exchange count, arrivals
+            self.error = torch.zeros(1, dtype=torch.int32, device=self.device)
+            try:
+                self.recv_ptr = H.p2p_malloc(self.W * self.slot * 4, kind)
+                self._own.append(self.recv_ptr)
+                self.sig_ptr = H.p2p_malloc(max(256, 8 * self.W), kind)
+                self._own.append(self.sig_ptr)
+                mine = (H.p2p_ipc_handle(self.recv_ptr), H.p2p_ipc_handle(self.sig_ptr))
+            except Exception as exc:
+                self.init_error = exc
+            handles: List[Optional[Tuple[bytes, bytes]]] = [mine]
+            if self.W > 1:
+                handles = [None] * self.W
+                dist.all_gather_object(handles, mine, group=group)
+            if any(h is None for h in handles):
+                self.init_error = self.init_error or RuntimeError("p2p buffer setup failed on a peer")
+            else:
+                try:
+                    for r in range(self.W):
+                        if r == self.rank:
+                            self.peers.append((self.recv_ptr, self.sig_ptr))
+                            continue
+                        a = H.p2p_ipc_open(handles[r][0])
+                        self._opened.append(a)
+                        b = H.p2p_ipc_open(handles[r][1])
+                        self._opened.append(b)
+                        self.peers.append((a, b))
+                except Exception as exc:
+                    self.init_error = exc
+        if self.W > 1:
+            dist.barrier(group=group)  # every rank's buffers are zeroed and mapped before any push
+
+    def params(self, src_ptr: int, n_floats: int, src_stride_floats: int = 0, chunks: Optional[int] = None):
+        if n_floats % 4 or src_stride_floats % 4 or src_ptr % 16:
+            raise ValueError("p2p payloads must be whole, 16-byte aligned float4 runs")
+        if n_floats > self.slot:
+            raise ValueError(f"payload of {n_floats} floats exceeds the {self.slot}-float slot")
+        p = self.H.P2PParams()
+        p.src = src_ptr
+        p.n4 = n_floats // 4
+        p.src_stride4 = src_stride_floats // 4
+        p.slot4 = self.slot // 4
+        for r, (a, b) in enumerate(self.peers):
+            p.set_peer(r, a, b)
+        p.ctrl = self.ctrl.data_ptr()
+        p.error = self.error.data_ptr()
+        p.W, p.rank = self.W, self.rank
+        # ≈16 KiB per workgroup, ≤64 chunks per destination (≤1024 workgroups at W=16)
+        p.chunks = int(chunks or max(1, min(64, math.ceil(n_floats * 4 / 16384))))
+        p.spin_limit = self.spin_limit
+        return p
+
+    def push(self, p, stream: Optional[int] = None) -> None:
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.H.p2p_push(p, stream)
+
+    def slot_ptr(self, r: int) -> int:
+        return self.recv_ptr + r * self.slot * 4
+
+    def copy_out(self, out: torch.Tensor) -> torch.Tensor:
+        """Copy the W receive slots into ``out`` ([W * slot] f32, same device) on the current stream."""
+        if out.numel() < self.W * self.slot or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("copy_out needs a contiguous f32 tensor of W*slot elements")
+        self.H.memcpy_d2d(out.data_ptr(), self.recv_ptr, self.W * self.slot * 4,
+                          torch.cuda.current_stream(self.device).cuda_stream)
+        return out
+
+    def errored(self) -> bool:
+        return bool(int(self.error.item()))
+
+    def close(self) -> None:
+        """Unmap the peers' buffers and free this rank's (call on every rank, GPU idle)."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True  # set on every rank: the barriers below are matched
+        torch.cuda.synchronize(self.device)
+        if self.W > 1 and dist.is_initialized():
+            dist.barrier(group=self.group)  # no peer still writes into our buffers
+        with torch.cuda.device(self.device):
+            for a in self._opened:
+                self.H.p2p_ipc_close(a)
+            if self.W > 1 and dist.is_initialized():
+                dist.barrier(group=self.group)  # every peer has unmapped ours before we free it
+            for a in self._own:
+                self.H.p2p_free(a)
+        self._own, self._opened = [], []
+
+
+def selftest(ex: P2PExchange, n_floats: int, rounds: int = 3) -> bool:
+    """Push rank-tagged patterns through ``ex`` and check every slot on every rank.  Returns the
+    agreement of all ranks (every rank returns the same value)."""
+    dev = ex.device
+    ok = ex.init_error is None
+    try:
+        if not ok:
+            raise RuntimeError("p2p setup failed")
+        n = max(4, n_floats // 4 * 4)
+        src = torch.empty(n, dtype=torch.float32, device=dev)
+        out = torch.empty(ex.W * ex.slot, dtype=torch.float32, device=dev)
+        idx = torch.arange(n, dtype=torch.float32, device=dev)
+        p = ex.params(src.data_ptr(), n)
+        for it in range(rounds):
+            src.copy_(idx * 0.5 + (1000.0 * ex.rank + 7.0 * it))
+            ex.push(p)
+            ex.copy_out(out)
+            got = out.view(ex.W, ex.slot)[:, :n]
+            want = idx.unsqueeze(0) * 0.5 + (1000.0 * torch.arange(ex.W, device=dev).unsqueeze(1) + 7.0 * it)
+            ok = ok and bool(torch.equal(got, want))
+        ok = ok and not ex.errored()
+    except Exception:  # a mapping / launch failure on this rank: agree on the fallback below
+        ok = False
+    if ex.W > 1 and dist.is_initialized():
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                            device=dev if dist.get_backend(ex.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ex.group)
+        ok = bool(int(flag.item()))
+    return ok
