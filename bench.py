@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--dp_exchange", default="auto", choices=["auto", "p2p", "rccl"],
+                    help="N>1 dp all-gather: p2p push over IPC-mapped peer buffers (one node) or RCCL")
     ap.add_argument("--steps_per_graph", type=int, default=64, help="fused engine: steps captured per HIP graph")
     ap.add_argument("--capacity", default="auto",
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
@@ -139,7 +141,7 @@ def main():
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
                                     mode=parallelism, seed=a.seed, use_graph=not a.no_graph, capacity=cap,
-                                    compute_dtype=a.compute_dtype)
+                                    compute_dtype=a.compute_dtype, exchange=a.dp_exchange)
         else:
             from rocfm.models.fused import FusedDeepFM
 
@@ -220,6 +222,7 @@ def main():
             "engine": a.engine,
             "embedding_update": a.embedding_update,
             "exchange_capacity": cap,
+            "exchange": getattr(eng, "exchange", None) if world > 1 else None,
         },
     }
     if rank == 0:

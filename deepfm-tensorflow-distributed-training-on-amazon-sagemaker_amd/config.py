@@ -119,6 +119,7 @@ class Config:
     dist_timeout_s: int = 600
     watchdog_s: int = 0  # >0: dump stacks and exit(3) when no step completes for this long (§5.3)
     exchange_capacity: int = 0  # rows per rank (dp) / per owner (rowshard) in the exchange buffers; 0 = B*F (safe)
+    dp_exchange: str = "auto"  # dp all-gather transport: auto | p2p (IPC push over xGMI, one node) | rccl
 
     # ------------------------------------------------------------------------------------
     @property
@@ -150,6 +151,8 @@ class Config:
             raise ValueError(f"unknown optimizer {self.optimizer!r}")
         if self.loss_type not in ("log_loss", "square_loss"):
             raise ValueError(f"unknown loss_type {self.loss_type!r}")
+        if self.dp_exchange not in ("auto", "p2p", "rccl"):
+            raise ValueError(f"unknown dp_exchange {self.dp_exchange!r}")
         if self.task_type not in ("train", "eval", "infer", "export"):
             raise ValueError(f"unknown task_type {self.task_type!r}")
         if self.embedding_update not in ("sparse", "exact"):

@@ -109,7 +109,8 @@ class Estimator:
                 mode = "dense_dp" if (cfg.embedding_update == "exact" or cfg.parallelism == "dense_dp") else "dp"
                 return FusedDataParallel(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                          embedding_update=cfg.embedding_update, mode=mode, seed=cfg.seed,
-                                         use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype)
+                                         use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,
+                                         exchange=cfg.dp_exchange)
             from .models.fused import FusedDeepFM
 
             return FusedDeepFM(self.spec, self.hp, cfg.batch_size, self.device, embedding_update=cfg.embedding_update,
