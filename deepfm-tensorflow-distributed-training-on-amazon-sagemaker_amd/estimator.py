@@ -139,7 +139,8 @@ class Estimator:
                                num_threads=max(1, min(cfg.num_threads, 16)), verify_crc=cfg.crc_check,
                                skip_bad=cfg.on_bad_record == "skip",
                                shuffle_buffer=(cfg.batch_size * 8 if (training and cfg.perform_shuffle) else 0),
-                               seed=cfg.seed + self.info.rank, stream_mode=bool(cfg.pipe_mode))
+                               seed=cfg.seed + self.info.rank, stream_mode=bool(cfg.pipe_mode),
+                               hold=2)  # _device_batches syncs batch t's H2D copy while t+1 is current
 
     def _host_batches(self, ds: Iterable):
         chk = ids_check_enabled()
@@ -149,8 +150,12 @@ class Estimator:
             yield b
 
     def _device_batches(self, ds: Iterable):
-        """Host (pinned) batches → device tensors; waits for each H2D copy before the loader may
-        recycle its pinned slot (the iterator releases the previous slot on advance)."""
+        """Host (pinned) batches → device tensors.  Batch t's H2D copy is waited for in the body
+        of batch t+1, so the loader must keep t's pinned slot until batch t+2 is requested
+        (``hold=2`` in _dataset); with hold=1 the slot was recycled by the decoders while its copy
+        could still be queued behind the GPU's work (a rare corrupted batch)."""
+        if getattr(ds, "hold", 2) < 2:
+            raise ValueError("_device_batches needs a dataset with hold >= 2")
         prev_ev = None
         chk = ids_check_enabled()
         for ids, vals, labels in ds:
