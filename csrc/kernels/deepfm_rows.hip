@@ -188,7 +188,9 @@ struct CtShape {
     if (p.stamps != nullptr && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime();   \
   } while (0)
 
-template <int KP4, class SH>
+// FP8 is a template parameter (not a runtime branch on p.fp8): the fp8 input-layer path kept in the
+// bf16 kernel raised its register demand past the 256 VGPRs of a 2-wave/SIMD workgroup and spilled.
+template <int KP4, class SH, bool FP8>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         cterm += S * S - Q;
       }
     }
-    if (p.fp8) {  // row max |bf16(e)| = bf16(max |e|) (rounding is monotonic)
+    if (FP8) {  // row max |bf16(e)| = bf16(max |e|) (rounding is monotonic)
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o, 64));
       if (q == 0) s_amax[r] = bf2f(f2bf(amx));
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SH::kStatic) {
         const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
-        if (l == 0 && p.fp8) {
+        if (l == 0 && FP8) {
           // fp8-e4m3 MFMA: weights quantised per output column (this wave owns whole columns, all
           // of K in registers), activations per row; the product is de-scaled in the epilogue
           float wm = 0.f;
@@ -912,15 +914,15 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
   return L;
 }
 
-template <int KP4, class SH>
-static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
+template <int KP4, class SH, bool FP8>
+static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
   static bool attr_set = false;
   static int max_dyn = 0;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
     hipFuncAttributes fa{};
-    ROCFM_HIP_CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>)));
+    ROCFM_HIP_CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>)));
     max_dyn = 160 * 1024 - (int)fa.sharedSizeBytes;
-    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>),
+    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn));
     attr_set = true;
   }
@@ -928,7 +930,7 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   if (p.bn && p.train) {  // grid barriers: every workgroup must be resident at once
     int per_cu = 0, dev = 0, cus = 0;
     ROCFM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH>), kRowThreads, p.lds.total));
+        &per_cu, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>), kRowThreads, p.lds.total));
     ROCFM_HIP_CHECK(hipGetDevice(&dev));
     ROCFM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     // the occupancy query can over-report by one block per CU: trust one fewer when it says > 1
@@ -936,8 +938,19 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
     ROCFM_REQUIRE(p.Bp / kRowTile <= limit, "deepfm_rows: batch_norm needs every workgroup of the batch resident "
                                             "at once (batch too large for one launch; use engine=torch)");
   }
-  hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
+  hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH, FP8>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
                      p);
+}
+
+template <int KP4, class SH>
+static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
+  if constexpr (SH::kStatic) {
+    if (p.fp8) {
+      launch_rows_impl<KP4, SH, true>(p, stream);
+      return;
+    }
+  }
+  launch_rows_impl<KP4, SH, false>(p, stream);
 }
 
 // Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
