@@ -52,6 +52,28 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
   const uint32_t row = key / p.key_div;
   if (p.rep[row] != r) return;
   const int W = p.W;
+  const size_t base = (size_t)row * KP4;
+  // the table row and its optimizer slots depend only on the row: issued now, in the same round
+  // trip as the other sources' positions (one dependent global round trip less per row)
+  // (mode 1 does not need them; the loads are harmless there: emb / slots are always valid)
+  // Absent slots read the table instead and are zeroed after the load: a `ptr ? load : 0` here
+  // became a select between a global and a private address (flat access + scratch).
+  float4 w[KP4], a[KP4], b[KP4];
+  const float4* e4r = reinterpret_cast<const float4*>(p.emb) + base;
+  const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
+  const float4* b4r = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb) + base;
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) {
+    w[c] = e4r[c];
+    a[c] = a4r[c];
+    b[c] = b4r[c];
+  }
+  if (!p.s0)
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!p.s1)
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) b[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc[KP4];
 #pragma unroll
   for (int c = 0; c < KP4; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -98,7 +120,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
   for (int q = r; q < W; ++q) p.pos[(size_t)q * p.Vmap + row] = -1;
   p.rep[row] = W;
 
-  const size_t base = (size_t)row * KP4;
   if (p.mode == 1) {
     float4* dg = reinterpret_cast<float4*>(p.dense_grad) + base;
 #pragma unroll
@@ -116,13 +137,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
   float4* e4 = reinterpret_cast<float4*>(p.emb) + base;
   float4* a4 = p.s0 ? reinterpret_cast<float4*>(p.s0) + base : nullptr;
   float4* b4 = p.s1 ? reinterpret_cast<float4*>(p.s1) + base : nullptr;
-  float4 w[KP4], a[KP4], b[KP4];
-#pragma unroll
-  for (int c = 0; c < KP4; ++c) {
-    w[c] = e4[c];
-    a[c] = a4 ? a4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-    b[c] = b4 ? b4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
 #pragma unroll
   for (int c = 0; c < KP4; ++c) {
     float* wc = &w[c].x;

@@ -168,9 +168,11 @@ __global__ __launch_bounds__(256) void shard_serve_kernel(ShardServeParams p) {
   const bool ok = !pad && (int)(id % (uint32_t)p.W) == p.rank && lr < p.Vs;
   if (!pad && !ok && p.bad) *p.bad = 1;
   if (p.rows_out) {
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    reinterpret_cast<float4*>(p.rows_out)[(size_t)r * KP4 + c] =
-        ok ? reinterpret_cast<const float4*>(p.table)[(size_t)lr * KP4 + c] : z;
+    // load row 0 for requests this owner does not serve and zero the value: `ok ? load : 0`
+    // compiled to a select between a global and a private address (flat access + scratch)
+    float4 v = reinterpret_cast<const float4*>(p.table)[(size_t)(ok ? lr : 0u) * KP4 + c];
+    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<float4*>(p.rows_out)[(size_t)r * KP4 + c] = v;
   }
   if (c == 0 && p.lkeys) p.lkeys[r] = ok ? lr : p.Vs;
 }
