@@ -59,11 +59,19 @@ __device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st,
       break;
     }
     case kFtrl: {
-      float pw = -o.ftrl_lr_power;
-      float acc_new = s0 + g * g;
-      float sigma = (powf(acc_new, pw) - powf(s0, pw)) / o.lr;
+      const float acc_new = s0 + g * g;
+      // TF's ApplyFtrl special-cases the default lr_power = -0.5 with sqrt; powf otherwise
+      float pn, po;
+      if (o.ftrl_lr_power == -0.5f) {
+        pn = sqrtf(acc_new);
+        po = sqrtf(s0);
+      } else {
+        pn = powf(acc_new, -o.ftrl_lr_power);
+        po = powf(s0, -o.ftrl_lr_power);
+      }
+      const float sigma = (pn - po) / o.lr;
       s1 += g - sigma * p;
-      float quad = powf(acc_new, pw) / o.lr + 2.f * o.ftrl_l2;
+      const float quad = pn / o.lr + 2.f * o.ftrl_l2;
       p = fabsf(s1) > o.ftrl_l1 ? (copysignf(o.ftrl_l1, s1) - s1) / quad : 0.f;
       s0 = acc_new;
       break;

@@ -480,10 +480,14 @@ class Estimator:
                 self._log({"event": "checkpoint", "path": path})
             dist.barrier(group=self._ctrl_group())
             return path
-        if not self.info.is_chief:
-            return None
-        path = ckpt.save_checkpoint(self.model_dir, sd, step, self.cfg.keep_checkpoint_max, extra=extra)
-        self._log({"event": "checkpoint", "path": path})
+        path = None
+        if self.info.is_chief:
+            path = ckpt.save_checkpoint(self.model_dir, sd, step, self.cfg.keep_checkpoint_max, extra=extra)
+            self._log({"event": "checkpoint", "path": path})
+        if self.world > 1:
+            # replicas wait (GPU drained by state_dict) while rank 0 writes: no rank's exchange
+            # kernel spins on a peer that is busy on the host
+            dist.barrier(group=self._ctrl_group())
         return path
 
     def restore(self, prefix: Optional[str] = None) -> Optional[str]:

@@ -86,11 +86,14 @@ def _update(hp: OptHParams, p: torch.Tensor, g: torch.Tensor, slots: List[torch.
         p.sub_(hp.lr * a)
     elif hp.name == "ftrl":
         acc, lin = slots
-        pw = -hp.ftrl_lr_power
         acc_new = acc + g * g
-        sigma = (acc_new.pow(pw) - acc.pow(pw)) / hp.lr
+        if hp.ftrl_lr_power == -0.5:  # TF's ApplyFtrl special case (sqrt instead of pow)
+            pn, po = acc_new.sqrt(), acc.sqrt()
+        else:
+            pn, po = acc_new.pow(-hp.ftrl_lr_power), acc.pow(-hp.ftrl_lr_power)
+        sigma = (pn - po) / hp.lr
         lin.add_(g - sigma * p)
-        quad = acc_new.pow(pw) / hp.lr + 2.0 * hp.ftrl_l2
+        quad = pn / hp.lr + 2.0 * hp.ftrl_l2
         pnew = torch.where(lin.abs() > hp.ftrl_l1, (torch.sign(lin) * hp.ftrl_l1 - lin) / quad, torch.zeros_like(p))
         p.copy_(pnew)
         acc.copy_(acc_new)

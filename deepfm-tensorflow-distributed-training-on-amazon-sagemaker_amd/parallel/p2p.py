@@ -12,7 +12,9 @@ into the multi-step HIP graphs like any other kernel (also when the process grou
 Receive buffers and flags are allocated uncached (``hipDeviceMallocUncached``) so that a peer's
 writes are visible to the kernels that read them next without any L2 maintenance.  Every wait in
 the kernel is bounded: a peer that never arrives raises a sticky error flag (``errored()``)
-instead of hanging the GPU.
+instead of hanging the GPU.  The default bound (2^30 polls, about a minute) only fires when a
+peer is gone: ranks that stall on host work (rank 0 writing a checkpoint) are drained and joined
+by a barrier first (Estimator._save), so healthy peers never wait that long.
 
 The reference has no equivalent: Horovod hands the gradients to NCCL (HVD:296).
 """
@@ -56,7 +58,7 @@ class P2PExchange:
     """
 
     def __init__(self, slot_floats: int, device, group=None, kind: int = KIND_UNCACHED,
-                 spin_limit: int = 1 << 25):
+                 spin_limit: int = 1 << 30):
         H = self.H = _hip()
         self.group = group
         self.W = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -107,7 +109,8 @@ class P2PExchange:
         if self.W > 1:
             dist.barrier(group=group)  # every rank's buffers are zeroed and mapped before any push
 
-    def params(self, src_ptr: int, n_floats: int, src_stride_floats: int = 0, chunks: Optional[int] = None):
+    def params(self, src_ptr: int, n_floats: int, src_stride_floats: int = 0, chunks: Optional[int] = None,
+               spin_limit: Optional[int] = None):
         if n_floats % 4 or src_stride_floats % 4 or src_ptr % 16:
             raise ValueError("p2p payloads must be whole, 16-byte aligned float4 runs")
         if n_floats > self.slot:
@@ -124,7 +127,7 @@ class P2PExchange:
         p.W, p.rank = self.W, self.rank
         # ≈16 KiB per workgroup, ≤64 chunks per destination (≤1024 workgroups at W=16)
         p.chunks = int(chunks or max(1, min(64, math.ceil(n_floats * 4 / 16384))))
-        p.spin_limit = self.spin_limit
+        p.spin_limit = int(spin_limit or self.spin_limit)
         return p
 
     def push(self, p, stream: Optional[int] = None) -> None:
@@ -176,7 +179,7 @@ def selftest(ex: P2PExchange, n_floats: int, rounds: int = 3) -> bool:
         src = torch.empty(n, dtype=torch.float32, device=dev)
         out = torch.empty(ex.W * ex.slot, dtype=torch.float32, device=dev)
         idx = torch.arange(n, dtype=torch.float32, device=dev)
-        p = ex.params(src.data_ptr(), n)
+        p = ex.params(src.data_ptr(), n, spin_limit=1 << 24)  # ≈1 s: a missing peer fails fast here
         for it in range(rounds):
             src.copy_(idx * 0.5 + (1000.0 * ex.rank + 7.0 * it))
             ex.push(p)
