@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--dp_exchange", default="auto", choices=["auto", "p2p", "rccl"],
-                    help="N>1 dp all-gather: p2p push over IPC-mapped peer buffers (one node) or RCCL")
+                    help="N>1 exchanges (dp all-gather, row-shard all-to-all + all-reduce): p2p push over "
+                         "IPC-mapped peer buffers (one node) or RCCL")
     ap.add_argument("--steps_per_graph", type=int, default=64, help="fused engine: steps captured per HIP graph")
     ap.add_argument("--capacity", default="auto",
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
@@ -135,7 +136,8 @@ def main():
             from rocfm.parallel.emb_shard import FusedRowShard
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
-                                use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype)
+                                use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype,
+                                exchange=a.dp_exchange)
         elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 

@@ -119,7 +119,7 @@ class Config:
     dist_timeout_s: int = 600
     watchdog_s: int = 0  # >0: dump stacks and exit(3) when no step completes for this long (§5.3)
     exchange_capacity: int = 0  # rows per rank (dp) / per owner (rowshard) in the exchange buffers; 0 = B*F (safe)
-    dp_exchange: str = "auto"  # dp all-gather transport: auto | p2p (IPC push over xGMI, one node) | rccl
+    dp_exchange: str = "auto"  # dp / rowshard exchange transport: auto | p2p (IPC push over xGMI, one node) | rccl
 
     # ------------------------------------------------------------------------------------
     @property

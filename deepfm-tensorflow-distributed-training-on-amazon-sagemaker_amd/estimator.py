@@ -99,7 +99,8 @@ class Estimator:
             if self.engine_name == "fused":
                 return FusedRowShard(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                      embedding_update=cfg.embedding_update, seed=cfg.seed,
-                                     use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype)
+                                     use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,
+                                     exchange=cfg.dp_exchange)
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
                                  seed=cfg.seed)
         if self.engine_name == "fused":

@@ -160,7 +160,7 @@ class FusedDataParallel:
         self.check_every = int(check_every)
         self.device = e.device
         self.p2p = None
-        self.exchange = "rccl"  # DP all-gather transport (mode dp: _open_p2p may pick "p2p")
+        self.exchange = "rccl"  # DP all-gather transport (mode dp: p2p.open_exchanges may pick "p2p")
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
             from .dist import broadcast_tensors
@@ -189,8 +189,12 @@ class FusedDataParallel:
             self.off_rows = self.off_keys + cap
             self.S = (self.off_rows + cap * Kp + 3) // 4 * 4  # float4 payload (p2p push)
             self.send = torch.zeros(self.S, dtype=torch.float32, device=e.device)
-            self.p2p = self._open_p2p(exchange)
+            from .p2p import open_exchanges
+
+            exs = open_exchanges([self.S], self.device, exchange)  # transport: p2p push or RCCL
+            self.p2p = exs[0] if exs else None
             if self.p2p is not None:  # rank slots live in the uncached, peer-mapped receive buffer
+                self.exchange = "p2p"
                 self.graph_collectives = use_graph  # the push kernel is capturable whatever the backend
                 self.recv = None
                 self._recv_ptr = self.p2p.recv_ptr
@@ -276,32 +280,6 @@ class FusedDataParallel:
         if join_side:
             e._join(side)
         return side
-
-    def _open_p2p(self, exchange: Optional[str]):
-        """The DP all-gather transport: ``p2p`` (one-shot push over IPC-mapped peer buffers,
-        rocfm.parallel.p2p) or ``rccl``.  ``auto`` (default; env ROCFM_DP_EXCHANGE) picks p2p when
-        every rank is on this node and a self-test of the mapped buffers passes on every rank."""
-        choice = (exchange or os.environ.get("ROCFM_DP_EXCHANGE", "auto")).lower()
-        if choice not in ("auto", "p2p", "rccl"):
-            raise ValueError(f"exchange must be auto, p2p or rccl, got {choice!r}")
-        self.exchange = "rccl"
-        if self.world == 1 or choice == "rccl":
-            return None
-        from . import p2p as P
-
-        if not P.single_node():
-            if choice == "p2p":
-                raise RuntimeError("exchange=p2p needs every rank on one node")
-            return None
-        ex = P.P2PExchange(self.S, self.device)  # collective; local failures land in ex.init_error
-        if not P.selftest(ex, self.S):            # agreed by every rank
-            err = ex.init_error
-            ex.close()
-            if choice == "p2p":
-                raise RuntimeError(f"p2p exchange unavailable: {err or 'self-test failed'}")
-            return None
-        self.exchange = "p2p"
-        return ex
 
     def _exchange(self):
         if self.p2p is not None:

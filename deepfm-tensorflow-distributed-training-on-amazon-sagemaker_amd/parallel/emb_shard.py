@@ -384,7 +384,8 @@ class FusedRowShard:
 
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
-                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16"):
+                 capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
+                 exchange: Optional[str] = None):
         from ..models.fused import FusedDeepFM
 
         W, r = _world_rank()
@@ -414,7 +415,8 @@ class FusedRowShard:
         n = e.n_lookup
         self.n = n
         cap = int(capacity) if capacity else min(n, int(math.ceil(1.25 * n / W)) + 64)
-        self.cap = cap = max(1, min(cap, n))
+        cap = max(1, min(cap, n))
+        self.cap = cap = (cap + 3) // 4 * 4  # whole float4 runs per owner segment (p2p push)
         M = W * cap
         self.M = M
         i32 = dict(dtype=torch.int32, device=dev)
@@ -434,11 +436,30 @@ class FusedRowShard:
                                       device=dev)
         # ---- exchange buffers ----
         f32 = dict(dtype=torch.float32, device=dev)
-        self.recv_ids = torch.full((M,), PAD, **i32)
         self.rows_out = torch.zeros(M, Kp, **f32)
-        self.rows_in = torch.zeros(M, Kp, **f32)
         self.grad_stage = torch.zeros(M, Kp, **f32)
-        self.grad_back = torch.zeros(M, Kp, **f32)
+        # X1-X3 all-to-all and X4 MLP all-reduce: one-shot push over IPC-mapped peer buffers on one
+        # node (rocfm.parallel.p2p; the receive buffers ARE the peer-mapped slots), else RCCL
+        from .p2p import open_exchanges
+
+        self.P = e.layout.total
+        exs = open_exchanges([cap, cap * Kp, cap * Kp, self.P], dev, exchange)
+        self.exchange = "p2p" if exs else "rccl"
+        self.p2p_x = {}
+        if exs:
+            self.x_ids, self.x_rows, self.x_grad, self.x_mlp = exs
+            self.recv_ids = self.x_ids.recv_tensor(torch.int32, (M,))
+            self.recv_ids.fill_(PAD)
+            self.rows_in = self.x_rows.recv_tensor(torch.float32, (M, Kp))
+            self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
+            for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
+                self.p2p_x[t.data_ptr()] = ex
+            self.graph_collectives = use_graph  # push kernels are capturable whatever the backend
+        else:
+            self.recv_ids = torch.full((M,), PAD, **i32)
+            self.rows_in = torch.zeros(M, Kp, **f32)
+            self.grad_back = torch.zeros(M, Kp, **f32)
+        self._p2p_params = {}
         # owner merge maps (merge.hip): position of each local row in every source's request list
         self.pos = torch.empty(W * Vs, **i32)
         self.rep = torch.empty(Vs, **i32)
@@ -505,7 +526,8 @@ class FusedRowShard:
                 op.mode = 0
             self.owner_params.append(op)
             da = e.dense_apply_params[p]
-            da.apply, da.grads, da.grad_scale = 1, e.dense_grads_flat.data_ptr(), 1.0 / self.W
+            da.apply, da.grad_scale = 1, 1.0 / self.W
+            self._set_mlp_grads(da)
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
         pp = e.pred_params
         pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
@@ -600,10 +622,39 @@ class FusedRowShard:
         g.replay()
 
     def _exchange(self, out, inp):
-        if self.W > 1:
+        """Equal-split all-to-all of ``inp`` into ``out`` (X1-X3)."""
+        ex = self.p2p_x.get(out.data_ptr())
+        if ex is not None:
+            key = (out.data_ptr(), inp.data_ptr())
+            prm = self._p2p_params.get(key)
+            if prm is None:
+                chunk = out.numel() // self.W
+                prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
+            ex.push(prm)
+        elif self.W > 1:
             all_to_all_equal(out, inp)
         else:
             out.copy_(inp)
+
+    def _set_mlp_grads(self, da) -> None:
+        """Point a dense-apply block at the X4 result: the W gathered rank segments (p2p, summed in
+        rank order by the kernel) or the RCCL all-reduced flat gradient."""
+        e = self.eng
+        if self.exchange == "p2p":
+            da.grads, da.nseg, da.seg_stride = self.x_mlp.recv_ptr, self.W, self.x_mlp.slot
+        else:
+            da.grads, da.nseg = e.dense_grads_flat.data_ptr(), 1
+
+    def _allreduce_mlp(self) -> None:
+        """X4: the MLP gradients of every rank (p2p all-gather; the sum happens in dense_apply)."""
+        e = self.eng
+        if self.exchange == "p2p":
+            prm = self._p2p_params.get("mlp")
+            if prm is None:
+                prm = self._p2p_params["mlp"] = self.x_mlp.params(e.dense_grads_flat.data_ptr(), self.P)
+            self.x_mlp.push(prm)
+        elif self.W > 1:
+            all_reduce_(e.dense_grads_flat)
 
     def _step_body(self, p: int) -> None:
         e = self.eng
@@ -613,8 +664,7 @@ class FusedRowShard:
         self._exchange(self.rows_in, self.rows_out)                             # X2 rows
         self._phase_compute(p, with_side=False)
         self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
-        if self.W > 1:
-            all_reduce_(e.dense_grads_flat)                                     # X4 MLP grads
+        self._allreduce_mlp()                                                   # X4 MLP grads
         self._phase_update(p)
         e._join(side)
 
@@ -632,8 +682,7 @@ class FusedRowShard:
             self._exchange(self.rows_in, self.rows_out)
             self._run(("compute", p), lambda: self._phase_compute(p))
             self._exchange(self.grad_back, self.grad_stage)
-            if self.W > 1:
-                all_reduce_(e.dense_grads_flat)
+            self._allreduce_mlp()
             self._run(("update", p), lambda: self._phase_update(p))
         self._warm += 1
         e._i += 1
@@ -679,9 +728,15 @@ class FusedRowShard:
 
     def close(self) -> None:
         """Release the captured graphs (required before destroy_process_group when they hold
-        RCCL collectives)."""
+        RCCL collectives) and the peer-mapped exchange buffers."""
         torch.cuda.synchronize(self.device)
         self._graphs = {}
+        if self.exchange == "p2p":
+            self.recv_ids = self.rows_in = self.grad_back = None  # views of the buffers freed below
+            self.p2p_x = {}
+            for ex in (self.x_ids, self.x_rows, self.x_grad, self.x_mlp):
+                ex.close()
+            self.exchange = "closed"
 
     # ---- multi-step graphs (pool mode, capturable collectives) -----------------------------------
     # FusedDeepFM's multi-step pipeline with row-shard routing: the side chain of a graph fetches
@@ -720,7 +775,8 @@ class FusedRowShard:
                 ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
                 ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
                 ep.grad_scale = 1.0
-                da.apply, da.grads, da.grad_scale = 1, e.dense_grads_flat.data_ptr(), 1.0 / W
+                da.apply, da.grad_scale = 1, 1.0 / W
+                self._set_mlp_grads(da)
                 mg = H.MergeParams()
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
@@ -754,8 +810,7 @@ class FusedRowShard:
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
-            if self.W > 1:
-                all_reduce_(e.dense_grads_flat)                                 # X4 MLP grads
+            self._allreduce_mlp()                                               # X4 MLP grads
             H.merge_scatter_dense(mg, da, s)                                    # owner scatter ‖ MLP opt
             H.merge_apply(mg, s)
             if ed is not None:
@@ -802,6 +857,8 @@ class FusedRowShard:
                                f"rebuild with capacity >= {c} (or capacity=batch_size*field_size)")
         if bad:
             raise RuntimeError("row-shard routing error: a rank received ids it does not own")
+        if self.exchange == "p2p" and any(x.errored() for x in (self.x_ids, self.x_rows, self.x_grad, self.x_mlp)):
+            raise RuntimeError("row-shard p2p exchange: a peer wait timed out (rank missing or stalled)")
 
     # ---- inference (collective) ------------------------------------------------------------------
     @torch.no_grad()

@@ -146,6 +146,24 @@ class P2PExchange:
                           torch.cuda.current_stream(self.device).cuda_stream)
         return out
 
+    def recv_tensor(self, dtype: torch.dtype, shape) -> torch.Tensor:
+        """The W receive slots as a torch tensor (no copy; 4-byte dtypes, ≤ W·slot elements).
+        The tensor borrows the buffer: keep this exchange open while it is used."""
+        if torch.empty(0, dtype=dtype).element_size() != 4:
+            raise ValueError("recv_tensor supports 4-byte dtypes")
+        n = int(math.prod(shape))
+        if n > self.W * self.slot:
+            raise ValueError(f"{n} elements exceed the {self.W}x{self.slot} receive slots")
+        typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+
+        class _Raw:  # __cuda_array_interface__ v3 view of the uncached HIP allocation
+            pass
+
+        raw = _Raw()
+        raw.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (self.recv_ptr, False),
+                                        "version": 3, "strides": None}
+        return torch.as_tensor(raw, device=self.device).view(*shape)
+
     def errored(self) -> bool:
         return bool(int(self.error.item()))
 
@@ -196,3 +214,34 @@ def selftest(ex: P2PExchange, n_floats: int, rounds: int = 3) -> bool:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ex.group)
         ok = bool(int(flag.item()))
     return ok
+
+
+def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None) -> Optional[List[P2PExchange]]:
+    """One P2PExchange per slot size, or None for the RCCL path.
+
+    ``choice`` (default: env ROCFM_DP_EXCHANGE, else ``auto``): ``rccl`` → None; ``p2p`` → the
+    exchanges or an error; ``auto`` → the exchanges when there is more than one rank, every rank
+    is on this node and the self-test of every exchange passes on every rank (agreed), else None.
+    Collective: every rank of the default group must call it with the same arguments."""
+    choice = (choice or os.environ.get("ROCFM_DP_EXCHANGE", "auto")).lower()
+    if choice not in ("auto", "p2p", "rccl"):
+        raise ValueError(f"exchange must be auto, p2p or rccl, got {choice!r}")
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world == 1 or choice == "rccl":
+        return None
+    if not single_node():
+        if choice == "p2p":
+            raise RuntimeError("exchange=p2p needs every rank on one node")
+        return None
+    exs = [P2PExchange(n, device) for n in slot_floats]  # collective; failures land in init_error
+    ok = True
+    for ex, n in zip(exs, slot_floats):
+        ok = selftest(ex, n) and ok  # every rank runs every self-test (each one is agreed)
+    if ok:
+        return exs
+    err = next((ex.init_error for ex in exs if ex.init_error is not None), None)
+    for ex in exs:
+        ex.close()
+    if choice == "p2p":
+        raise RuntimeError(f"p2p exchange unavailable: {err or 'self-test failed'}")
+    return None

@@ -159,16 +159,22 @@ def test_fused_reference_gradients_vs_autograd():
     torch.testing.assert_close(ref["dw_out"], Q["Deep-part/deep_out/weights"].grad.reshape(-1), rtol=0.05, atol=2e-3)
 
 
-def test_fused_reference_batch_norm_vs_autograd():
+@pytest.mark.parametrize("exact", [True, False])
+def test_fused_reference_batch_norm_vs_autograd(monkeypatch, exact):
     """The kernel oracle's batch-norm forward/backward (batch moments, γ/β gradients, dz through
-    the normalisation) equals autograd of the f32 DeepFM with batch_norm=True."""
+    the normalisation) equals autograd of the f32 DeepFM with batch_norm=True: exactly with the
+    oracle's bf16 operand rounding switched off, within bf16 tolerance with it (fixed γ/β: at 24
+    rows the normalisation amplifies bf16 rounding by up to ~15× for some draws)."""
+    if exact:
+        monkeypatch.setattr(R, "bf16", lambda x: x)
     spec = _spec(feature_size=40, layers=[16, 8])
     spec.batch_norm = True
     P = init_params(spec, 5)
+    g = torch.Generator().manual_seed(3)
     with torch.no_grad():  # non-trivial γ / β
         for i in range(2):
-            P[f"Deep-part/bn_{i}/gamma"].uniform_(0.5, 1.5)
-            P[f"Deep-part/bn_{i}/beta"].uniform_(-0.2, 0.2)
+            P[f"Deep-part/bn_{i}/gamma"].uniform_(0.5, 1.5, generator=g)
+            P[f"Deep-part/bn_{i}/beta"].uniform_(-0.2, 0.2, generator=g)
     ids, vals, labels = _batch(spec, 24)
     K = spec.embedding_size
     emb = torch.zeros(40, 8)
@@ -184,7 +190,7 @@ def test_fused_reference_batch_norm_vs_autograd():
     Q = {k: v.clone().requires_grad_(k in names) for k, v in P.items()}
     y = forward(Q, ids, vals, spec, train=True)
     torch.nn.functional.binary_cross_entropy_with_logits(y, labels).backward()
-    tol = dict(rtol=0.06, atol=3e-3)
+    tol = dict(rtol=1e-4, atol=1e-6) if exact else dict(rtol=0.06, atol=3e-3)
     torch.testing.assert_close(ref["dW"][0], Q[names[0]].grad, **tol)
     torch.testing.assert_close(ref["db"][1], Q[names[1]].grad, **tol)
     torch.testing.assert_close(ref["dgamma"][0], Q[names[2]].grad, **tol)
@@ -192,4 +198,5 @@ def test_fused_reference_batch_norm_vs_autograd():
     torch.testing.assert_close(ref["dbeta"][0], Q[names[4]].grad, **tol)
     torch.testing.assert_close(ref["dgamma"][1], Q[names[5]].grad, **tol)
     # the oracle's probabilities match the model's training-mode forward
-    torch.testing.assert_close(ref["prob"], torch.sigmoid(y.detach()), rtol=2e-2, atol=2e-3)
+    ptol = dict(rtol=1e-5, atol=1e-6) if exact else dict(rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(ref["prob"], torch.sigmoid(y.detach()), **ptol)
