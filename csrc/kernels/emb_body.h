@@ -222,6 +222,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         }
       } else if (p.mode == 1) {
         reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];
+        if (p.touched && u4 == 0) p.touched[idx4[u] / KP4] = (uint32_t)*p.step + 1u;
       } else {
         float* wc = &w[u].x;
         float* ac = &a[u].x;

@@ -34,6 +34,7 @@ struct EmbUpdateParams {
   uint32_t val_base;   // subtracted from svals (a batch's segment of a multi-batch sort)
   int sorted_contrib;  // 1: contrib rows are already in sorted order (row i ↔ sorted entry i; svals unused)
   const int32_t* chunk_end;  // nullable: per workgroup chunk, end of the run holding its last entry
+  uint32_t* touched;   // mode 1 (nullable): touched[row] = step + 1 for every row whose gradient it wrote
 };
 
 struct EmbDenseParams {
@@ -47,6 +48,10 @@ struct EmbDenseParams {
   float grad_scale;
   OptParams opt;
   const int64_t* step;
+  // nullable: touched[row] == step + 1 marks the rows whose dense_grad holds this step's gradient
+  // (written by the mode-1 scatter / merge).  Other rows read no gradient row (g = λ·θ only) and
+  // their dense_grad stays zero — the update never reads or clears the whole gradient table.
+  const uint32_t* touched;
 };
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream);

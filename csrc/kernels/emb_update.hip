@@ -57,9 +57,12 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
   float4* A = reinterpret_cast<float4*>(p.s0);
   float4* Bv = reinterpret_cast<float4*>(p.s1);
   const int kp4 = p.Kp >> 2;
+  const uint32_t tag = (uint32_t)(p.step ? *p.step : 0) + 1u;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.n4; i += (long long)gridDim.x * 256) {
     const int c0 = (int)(i % kp4) * 4;
-    float4 w = E[i], g = G[i];
+    const bool has_g = p.touched == nullptr || p.touched[i / kp4] == tag;
+    float4 w = E[i], g = make_float4(0, 0, 0, 0);
+    if (has_g) g = G[i];
     float4 a = A ? A[i] : make_float4(0, 0, 0, 0), b = Bv ? Bv[i] : make_float4(0, 0, 0, 0);
     float* wp = &w.x;
     float* gp = &g.x;
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
     for (int u = 0; u < 4; ++u)
       if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], gp[u] * p.grad_scale + p.l2 * wp[u], ap[u], bp[u]);
     E[i] = w;
-    G[i] = make_float4(0, 0, 0, 0);
+    if (has_g) G[i] = make_float4(0, 0, 0, 0);
     if (A) A[i] = a;
     if (Bv) Bv[i] = b;
   }

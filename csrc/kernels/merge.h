@@ -39,6 +39,7 @@ struct MergeParams {
   int mode;           // 0: lazy L2 + optimizer on the rows; 1: dense_grad[row] = Σ · grad_scale
   float* dense_grad;  // mode 1
   int32_t* overflow;  // nullable: sticky flag, set when a source's count exceeds cap
+  uint32_t* touched;  // mode 1 (nullable): touched[row] = step + 1 (EmbDenseParams::touched)
 };
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);

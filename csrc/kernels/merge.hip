@@ -131,6 +131,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
       g.w *= p.grad_scale;
       dg[c] = g;
     }
+    if (p.touched) p.touched[row] = (uint32_t)*p.step + 1u;
     return;
   }
   const OptStep st = opt_step(p.opt, *p.step);

@@ -197,6 +197,11 @@ class FusedDeepFM:
         tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
         self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
         self.dense_grad = (torch.zeros_like(self.emb) if embedding_update == "exact" else None)
+        # exact mode: rows whose dense_grad holds this step's gradient carry touched[row] = step + 1,
+        # so the dense update reads / clears gradient rows only there (None: read every row —
+        # dense_dp, whose gradient table arrives all-reduced)
+        self.touched = (torch.zeros(self.V, dtype=torch.int32, device=dev) if embedding_update == "exact"
+                        else None)
         self.dense_grads_flat = torch.zeros(L.total, dtype=torch.float32, device=dev)
         self.sort_stream = torch.cuda.Stream(device=dev)
         self.aux_stream = torch.cuda.Stream(device=dev)  # mlp_wgrad runs concurrently with the embedding update
@@ -348,12 +353,15 @@ class FusedDeepFM:
         ep.mode = 1 if self.embedding_update == "exact" else 0
         if self.dense_grad is not None:
             ep.dense_grad = self.dense_grad.data_ptr()
+        if self.touched is not None:
+            ep.touched = self.touched.data_ptr()
         ed = None
         if self.embedding_update == "exact":
             ed = H.EmbDenseParams()
             ed.emb = self.emb.data_ptr()
             ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
             ed.dense_grad = self.dense_grad.data_ptr()
+            ed.touched = self.touched.data_ptr() if self.touched is not None else 0
             ed.step = step_ptr
             ed.n4 = self.V * self.Kp // 4
             ed.Kp, ed.K1 = self.Kp, self.K1

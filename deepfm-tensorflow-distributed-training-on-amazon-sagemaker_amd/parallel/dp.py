@@ -173,6 +173,7 @@ class FusedDataParallel:
             # one flat bucket: [dense table grad (V*Kp) | MLP grads (P)]
             self.bucket = torch.zeros(e.V * e.Kp + P, dtype=torch.float32, device=e.device)
             e.dense_grad = self.bucket[: e.V * e.Kp].view(e.V, e.Kp)
+            e.touched = None  # every row's gradient comes from the all-reduce
             e.dense_grads_flat = self.bucket[e.V * e.Kp:]
             e._build_params()
             for p in range(2):

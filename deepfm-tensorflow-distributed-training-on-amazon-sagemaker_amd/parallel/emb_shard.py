@@ -508,6 +508,7 @@ class FusedRowShard:
             lp = e.emb_params[p]  # local: Σ lookup grads per received row → grad_stage
             lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
+            lp.touched = 0  # writes the exchange stage, not the table's gradient rows
             op = H.MergeParams()  # owner: Σ over source ranks per local row → optimizer
             op.keys, op.key_stride = self.recv_ids.data_ptr(), self.cap
             op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
@@ -521,6 +522,7 @@ class FusedRowShard:
             op.opt, op.step = e._opt(p), e.steps[p:].data_ptr()
             if self.embedding_update == "exact":
                 op.mode, op.dense_grad = 1, e.dense_grad.data_ptr()
+                op.touched = e.touched.data_ptr()  # the owner's dense update reads these rows
                 e.emb_dense_params[p].grad_scale = 1.0
             else:
                 op.mode = 0
@@ -774,6 +776,7 @@ class FusedRowShard:
                 wp.grads = e.dense_grads_flat.data_ptr()
                 ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
                 ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
+                ep.touched = 0
                 ep.grad_scale = 1.0
                 da.apply, da.grad_scale = 1, 1.0 / W
                 self._set_mlp_grads(da)
@@ -781,7 +784,7 @@ class FusedRowShard:
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "dense_grad"):
+                          "dense_grad", "touched"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 if ed is not None:

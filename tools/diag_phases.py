@@ -64,6 +64,22 @@ def main():
     report("mlp_wgrad (tile WGs)", wg[wg[:, 1] > 0], [0, 1, 2], ["MFMA + LDS reduce", "epilogue (opt+bf16)"])
     report("emb_rows_update", s_emb.view(-1, 16).cpu(), [0, 1, 2, 3, 4],
            ["keys+rows+scan+heads", "end search", "continuation", "optimizer items"])
+    # the slowest embedding workgroups of the last step, with their chunk's run-head count
+    p = (eng._i - 1) % 2
+    sk = eng.skeys[p].cpu().long()
+    heads = torch.ones_like(sk, dtype=torch.bool)
+    heads[1:] = sk[1:] != sk[:-1]
+    chunk = 512 if eng.Kp <= 32 else 256  # step_tail's / emb_update's entries per workgroup
+    st = s_emb.view(-1, 16).cpu().double()
+    nwg = (sk.numel() + chunk - 1) // chunk
+    tot = (st[:nwg, 4] - st[:nwg, 0]) * 0.01
+    opt = (st[:nwg, 4] - st[:nwg, 3]) * 0.01
+    order = torch.argsort(tot, descending=True)[:6]
+    for w in order.tolist():
+        h = int(heads[w * chunk:(w + 1) * chunk].sum())
+        print(f"   slow emb WG {w:3d}: total {tot[w]:.2f} us, optimizer items {opt[w]:.2f} us, run heads {h}")
+    hs = [int(heads[w * chunk:(w + 1) * chunk].sum()) for w in range(nwg)]
+    print(f"   run heads per chunk: min {min(hs)} mean {sum(hs) / len(hs):.0f} max {max(hs)}")
 
 
 if __name__ == "__main__":
