@@ -122,7 +122,7 @@ def main():
     explicit_dp = a.parallelism in ("dp", "dense_dp")
     parallelism = a.parallelism
     if parallelism == "auto":
-        parallelism = "dp" if a.embedding_update == "sparse" else "dense_dp"
+        parallelism = "dp"  # either update; dense_dp (dense all-reduce) only when asked for
     cap = None
     if a.engine == "fused" and (world > 1 or a.parallelism in ("dp", "rowshard")) and parallelism != "dense_dp":
         if a.capacity == "auto":

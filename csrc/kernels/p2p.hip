@@ -54,10 +54,14 @@ __global__ __launch_bounds__(kP2PThreads) void p2p_push_kernel(P2PParams p) {
     for (int u = 0; u < U; ++u) o[i + u * kP2PThreads] = v[u];
   }
   for (; i < hi; i += kP2PThreads) o[i] = s[i];
-  __threadfence_system();  // this thread's peer stores are performed before the arrival below
+  // Publish (counter form, system scope): every wave waits for its own payload stores → barrier →
+  // lane 0 release fence → an explicit wait (the compiler may drop the fence's own) → the ticket.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // "" = system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t prev = __hip_atomic_fetch_add(p.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {  // last workgroup: every payload store of this rank is done
       __hip_atomic_store(p.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -107,7 +107,7 @@ class Estimator:
             if self.world > 1 or cfg.parallelism in ("dp", "dense_dp"):
                 from .parallel.dp import FusedDataParallel
 
-                mode = "dense_dp" if (cfg.embedding_update == "exact" or cfg.parallelism == "dense_dp") else "dp"
+                mode = "dense_dp" if cfg.parallelism == "dense_dp" else "dp"
                 return FusedDataParallel(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                          embedding_update=cfg.embedding_update, mode=mode, seed=cfg.seed,
                                          use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,

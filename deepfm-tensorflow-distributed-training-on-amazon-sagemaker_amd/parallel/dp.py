@@ -3,20 +3,22 @@
 Every rank holds a full replica (rank-0 initial values, like BroadcastGlobalVariablesHook(0)),
 trains on its own shard of the data and, each step, exchanges gradients:
 
-``dense_dp`` (``embedding_update=exact``)
-    Horovod-faithful: the full-table L2 makes the fm_w/fm_v gradients dense, so the
-    whole dense gradient — table + MLP in ONE flat bucket — is all-reduced and averaged (the
-    16.2 MB/step of the notebook config), then every rank applies the same dense
-    optimizer update.
+``dense_dp`` (``parallelism=dense_dp``, always ``embedding_update=exact``)
+    Horovod-faithful transport: the full-table L2 makes the fm_w/fm_v gradients dense,
+    so the whole dense gradient — table + MLP in ONE flat bucket — is all-reduced and averaged
+    (the 16.2 MB/step of the notebook config), then every rank applies the same
+    dense optimizer update.
 
-``dp`` (``embedding_update=sparse``, the default)
+``dp`` (the default, either embedding update)
     Each rank reduces its lookups to (unique id, Σ grad row) pairs (emb_update.hip mode 2) and
-    packs them next to its MLP gradient in one send buffer; ONE ``all_gather`` moves every rank's
-    buffer to every rank (xGMI is fully connected point-to-point, so RCCL's all-gather uses all
-    links); each rank then sums the MLP gradients over ranks in rank order and merges the gathered
-    rows with the same sort + segmented-sum kernel it uses locally (rank-major order ⇒ bitwise
-    identical results on every rank), applies lazy L2 once and the row optimizer.  Replicas stay
-    bit-identical without a broadcast.
+    packs them next to its MLP gradient in one send buffer; ONE all-gather (the p2p push over
+    xGMI, or RCCL) moves every rank's buffer to every rank; each rank then sums the MLP gradients
+    over ranks in rank order and merges the gathered rows by direct addressing (rank order ⇒
+    bitwise identical results on every rank).  ``sparse``: lazy L2 and the row optimizer on the
+    touched rows.  ``exact``: the merged rows become this step's rows of the dense gradient table
+    and every rank runs the dense full-table update (λ·θ on every row) — the same mathematics as
+    dense_dp, because rows no rank touched have a zero data gradient on every rank, without
+    moving the dense table.  Replicas stay bit-identical without a broadcast.
 
 Gradients are averaged over ranks and the learning rate is scaled by the world size (HVD:171;
 ``lr_scaling``).  Both the fused HIP engine and the eager engine are supported.
@@ -148,9 +150,8 @@ class FusedDataParallel:
             raise ValueError(f"FusedDataParallel mode must be dp or dense_dp, got {mode}")
         if mode == "dense_dp" and embedding_update != "exact":
             embedding_update = "exact"
-        if mode == "dp" and embedding_update == "exact":
-            mode = "dense_dp"
         self.mode = mode
+        self.exact = embedding_update == "exact"
         self.eng = FusedDeepFM(spec, hp, batch_size, device, embedding_update=embedding_update, seed=seed,
                                params=params, use_graph=False, fuse_dense_opt=False,
                                dropout_seed=seed + 7919 * self.rank, compute_dtype=compute_dtype)
@@ -236,6 +237,9 @@ class FusedDataParallel:
                 mp_.l2, mp_.grad_scale = float(spec.l2_reg), 1.0 / self.world
                 mp_.opt, mp_.step = e._opt(p), e.steps[p:].data_ptr()
                 mp_.mode = 0
+                if self.exact:  # merged rows → the dense gradient table, then the full-table update
+                    mp_.mode, mp_.dense_grad, mp_.touched = 1, e.dense_grad.data_ptr(), e.touched.data_ptr()
+                    e.emb_dense_params[p].grad_scale = 1.0  # the merge applied 1/W
                 mp_.overflow = self.overflow.data_ptr()
                 self.merge_params.append(mp_)
                 da = e.dense_apply_params[p]
@@ -303,9 +307,11 @@ class FusedDataParallel:
             e.H.emb_dense_update(e.emb_dense_params[p], s)
             return
         # MLP: Σ over the gathered rank segments (rank order) + optimizer as extra workgroups of
-        # the row-scatter launch, then the row merge + optimizer
+        # the row-scatter launch, then the row merge + optimizer (exact: + the dense table update)
         e.H.merge_scatter_dense(self.merge_params[p], e.dense_apply_params[p], s)
         e.H.merge_apply(self.merge_params[p], s)
+        if self.exact:
+            e.H.emb_dense_update(e.emb_dense_params[p], s)
 
     def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:
@@ -386,11 +392,13 @@ class FusedDataParallel:
                 src = self.merge_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "overflow"):
+                          "overflow", "dense_grad", "touched"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 rows.zero_word = self.send[self.off_cnt:].data_ptr()
-                row.append((rows, wp, ex, da, None, mg))
+                if ed is not None:
+                    ed.grad_scale = 1.0  # the merge applied 1/W
+                row.append((rows, wp, ex, da, ed if self.exact else None, mg))
             self.m_dp.append(row)
         self._m_dp_S = Smax
 
@@ -406,6 +414,8 @@ class FusedDataParallel:
             if self.mode == "dp":
                 H.merge_scatter_dense(mg, da, s)  # row scatter ‖ MLP optimizer, one launch
                 H.merge_apply(mg, s)
+                if ed is not None:
+                    H.emb_dense_update(ed, s)
             else:
                 H.dense_apply(da, s)
                 H.emb_dense_update(ed, s)

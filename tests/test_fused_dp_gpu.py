@@ -35,7 +35,7 @@ def _batches(B, n, seed):
     return [gen.batch(B, "cpu", g) for _ in range(n)]
 
 
-def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0):
+def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, update=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,8 +45,9 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0):
 
     spec, hp = _cfg()
     B = 64
+    update = update or ("exact" if mode == "dense_dp" else "sparse")
     eng = FusedDataParallel(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3),
-                            embedding_update="exact" if mode == "dense_dp" else "sparse", mode=mode,
+                            embedding_update=update, mode=mode,
                             use_graph=spg > 0, exchange=exchange)
     assert eng.exchange == exchange or mode == "dense_dp", eng.exchange
     batches = _batches(2 * B, steps, 11)
@@ -68,20 +69,22 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,exchange,steps,spg", [("dp", "rccl", 3, 0), ("dense_dp", "rccl", 3, 0),
-                                                     ("dp", "p2p", 3, 0), ("dp", "p2p", 11, 4)])
-def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode, exchange, steps, spg):
-    """exchange=rccl runs the backend's collective (gloo here); p2p the IPC push kernel."""
+@pytest.mark.parametrize("mode,exchange,steps,spg,update", [
+    ("dp", "rccl", 3, 0, "sparse"), ("dense_dp", "rccl", 3, 0, "exact"), ("dp", "p2p", 3, 0, "sparse"),
+    ("dp", "p2p", 11, 4, "sparse"), ("dp", "p2p", 3, 0, "exact"), ("dp", "p2p", 11, 4, "exact")])
+def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode, exchange, steps, spg, update):
+    """exchange=rccl runs the backend's collective (gloo here); p2p the IPC push kernel.  dp+exact
+    merges the sparse exchange into the dense gradient table, then updates the whole table."""
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out, exchange, steps, spg), nprocs=2, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out, exchange, steps, spg, update), nprocs=2,
+                       join=True, start_method="spawn")
     dp = torch.load(out, weights_only=True)
     from rocfm.models.deepfm import init_params
     from rocfm.models.fused import FusedDeepFM
 
     spec, hp = _cfg()
     single = FusedDeepFM(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
-                         embedding_update="exact" if mode == "dense_dp" else "sparse")
+                         embedding_update=update)
     batches = _batches(128, steps, 11)
     single.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
                        torch.stack([b[2] for b in batches]).cuda())
@@ -96,8 +99,8 @@ def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode, exchange, steps,
     torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=atol)
 
 
-@pytest.mark.parametrize("mode", ["dp", "dense_dp"])
-def test_dp_multistep_graphs_world1_equal_single(mode):
+@pytest.mark.parametrize("mode,upd", [("dp", "sparse"), ("dense_dp", "exact"), ("dp", "exact")])
+def test_dp_multistep_graphs_world1_equal_single(mode, upd):
     """Single-process DP (no process group: the exchange is a copy) through the multi-step graph
     pipeline (export → exchange → merge / dense apply inside the graph) ≡ the single-GPU engine."""
     from rocfm.models.deepfm import init_params
@@ -105,7 +108,6 @@ def test_dp_multistep_graphs_world1_equal_single(mode):
     from rocfm.parallel.dp import FusedDataParallel
 
     spec, hp = _cfg()
-    upd = "exact" if mode == "dense_dp" else "sparse"
     batches = _batches(128, 5, 11)
     pool = [torch.stack([b[i] for b in batches]).cuda() for i in range(3)]
     dp = FusedDataParallel(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=upd,
