@@ -201,8 +201,9 @@ class FusedDataParallel:
                 self.recv = None
                 self._recv_ptr = self.p2p.recv_ptr
                 self.p2p_params = self.p2p.params(self.send.data_ptr(), self.S)
-            else:
-                self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+            else:  # one rank: the gathered list IS the send buffer (no copy)
+                self.recv = (torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+                             if self.world > 1 else self.send)
                 self._recv_ptr = self.recv.data_ptr()
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
@@ -290,9 +291,7 @@ class FusedDataParallel:
         if self.p2p is not None:
             self.p2p.push(self.p2p_params)
             return
-        if self.world == 1:  # single rank (profiling the DP step on one GPU): nothing to exchange
-            if self.mode == "dp":
-                self.recv.copy_(self.send)
+        if self.world == 1:  # single rank: recv aliases send (dp) / the bucket is already the sum
             return
         if self.mode == "dense_dp":
             _all_reduce(self.bucket)
