@@ -50,7 +50,7 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
                             embedding_update=update, mode=mode,
                             use_graph=spg > 0, exchange=exchange)
     assert eng.exchange == exchange or mode == "dense_dp", eng.exchange
-    batches = _batches(2 * B, steps, 11)
+    batches = _batches(world * B, steps, 11)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
             for b in batches]
     eng.attach_pool(torch.stack([x[0] for x in pool]).cuda(), torch.stack([x[1] for x in pool]).cuda(),
@@ -75,17 +75,28 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
 def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode, exchange, steps, spg, update):
     """exchange=rccl runs the backend's collective (gloo here); p2p the IPC push kernel.  dp+exact
     merges the sparse exchange into the dense gradient table, then updates the whole table."""
+    _check_dp_vs_single(tmp_path, 2, mode, exchange, steps, spg, update)
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_dp_world4_p2p_graphs(tmp_path, update):
+    """4 ranks on one GPU: the p2p push fans out to 3 peers and the merge sums 4 rank lists (the
+    W>2 paths the 8-GPU node runs), through multi-step graphs."""
+    _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
+
+
+def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update):
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out, exchange, steps, spg, update), nprocs=2,
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out, exchange, steps, spg, update), nprocs=world,
                        join=True, start_method="spawn")
     dp = torch.load(out, weights_only=True)
     from rocfm.models.deepfm import init_params
     from rocfm.models.fused import FusedDeepFM
 
     spec, hp = _cfg()
-    single = FusedDeepFM(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
+    single = FusedDeepFM(spec, hp, 64 * world, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
                          embedding_update=update)
-    batches = _batches(128, steps, 11)
+    batches = _batches(64 * world, steps, 11)
     single.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
                        torch.stack([b[2] for b in batches]).cuda())
     for _ in range(steps):
