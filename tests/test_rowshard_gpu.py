@@ -1,4 +1,4 @@
-"""Row-shard HIP path: routing kernels vs the numpy oracle; the fused row-shard step (1 rank, and 2
+"""Row-shard HIP path: routing kernels vs the numpy oracle; the fused row-shard step (1 rank, and 2 or 4
 ranks sharing one GPU over gloo) ≡ the single-GPU fused step on the union batch."""
 import os
 import socket
@@ -101,7 +101,7 @@ def _single(update, nsteps, B=128, opt="Adam"):
     spec, hp = _cfg(opt)
     single = FusedDeepFM(spec, hp, B, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
                          embedding_update=update)
-    batches = _batches(128, nsteps, 11)
+    batches = _batches(B, nsteps, 11)
     single.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
                        torch.stack([b[2] for b in batches]).cuda())
     for _ in range(nsteps):
@@ -150,7 +150,7 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     eng = FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), embedding_update=update,
                         use_graph=spg > 0, exchange=exchange)
     assert eng.exchange == exchange, eng.exchange
-    batches = _batches(2 * B, steps, 11)
+    batches = _batches(world * B, steps, 11)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
             for b in batches]
     eng.attach_pool(torch.stack([x[0] for x in pool]).cuda(), torch.stack([x[1] for x in pool]).cuda(),
@@ -186,6 +186,24 @@ def test_fused_rowshard_2ranks_equals_single_gpu_union_batch(tmp_path, update, e
     atol = 2e-5 if steps <= 3 else 1e-4  # rank-partial sums reorder fp32 additions (see test_fused_dp_gpu)
     for k in exp:
         torch.testing.assert_close(got["P"][k], exp[k], rtol=2e-3, atol=atol)
+    ids, vals, _ = _batches(100, 1, 5)[0]
+    pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
+    torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_rowshard_4ranks_p2p_graphs(tmp_path, update):
+    """4 ranks on one GPU: every table is split 4 ways and each all-to-all pushes to 3 peers (the
+    W>2 routing the 8-GPU node runs), through multi-step graphs."""
+    out = str(tmp_path / "rs4.pt")
+    steps = 10
+    mp.start_processes(_worker, args=(4, _free_port(), update, out, "p2p", steps, 4), nprocs=4, join=True,
+                       start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    ref = _single(update, steps, B=256)
+    exp = ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got["P"][k], exp[k], rtol=2e-3, atol=1e-4)
     ids, vals, _ = _batches(100, 1, 5)[0]
     pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
     torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
