@@ -9,6 +9,9 @@ namespace {
 
 constexpr uint32_t kPadKey = 0xFFFFFFFFu;
 constexpr int kMergeThreads = 256;
+// merge_apply: ≈cap·W threads, each a chain of dependent loads: one wave per workgroup spreads the
+// few waves over as many CUs (and their L1 / address units) as possible instead of 4 per CU
+constexpr int kApplyThreads = 64;
 constexpr int kMaxW = 64;
 
 __device__ __forceinline__ bool entry_valid(const MergeParams& p, int r, int j, uint32_t key) {
@@ -43,8 +46,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParam
 // One thread per source entry; only representatives (lowest rank holding the key) do work.
 // WMAX = 8 (one node): every later source's position and row are loaded before any is summed.
 template <int KP4, int WMAX>
-__global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams p) {
-  const int i = blockIdx.x * kMergeThreads + threadIdx.x;
+__global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams p) {
+  const int i = blockIdx.x * kApplyThreads + threadIdx.x;
   if (i >= p.W * p.cap) return;
   const int r = i / p.cap, j = i - r * p.cap;
   const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
@@ -85,6 +88,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
     float4 v[WMAX][KP4];
 #pragma unroll
     for (int q = 0; q < WMAX; ++q) {
+      if (q >= W) break;  // wave-uniform: no loads for ranks that do not exist
       const float4* src = reinterpret_cast<const float4*>(
           p.rows + (pj[q] >= 0 ? (size_t)q * p.row_stride + (size_t)pj[q] * p.Kp : 0));
 #pragma unroll
@@ -92,6 +96,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_apply_kernel(MergeParams 
     }
 #pragma unroll
     for (int q = 0; q < WMAX; ++q) {  // rank order: deterministic sum
+      if (q >= W) break;
       if (pj[q] < 0) continue;
 #pragma unroll
       for (int c = 0; c < KP4; ++c) {
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_dense_kernel(Merg
 
 template <int KP4>
 void launch_apply_t(const MergeParams& p, hipStream_t stream) {
-  const dim3 grid(cdiv(p.W * p.cap, kMergeThreads)), block(kMergeThreads);
+  const dim3 grid(cdiv(p.W * p.cap, kApplyThreads)), block(kApplyThreads);
   if (p.W <= 8)
     hipLaunchKernelGGL((merge_apply_kernel<KP4, 8>), grid, block, 0, stream, p);
   else
