@@ -29,9 +29,5 @@ PYBIND11_MODULE(_rocfm_hip, m) {
     return py::make_tuple(std::string(prop.gcnArchName), prop.multiProcessorCount,
                           (long long)prop.totalGlobalMem);
   });
-  m.def("probe", [](uintptr_t out, int n, uintptr_t stream) { launch_probe(P<float>(out), n, S(stream)); });
-  m.def("frag_probe", [](uintptr_t W, int K, int swz, int nblocks, uintptr_t st, uintptr_t sink, uintptr_t stream) {
-    launch_frag_probe(P<const uint16_t>(W), K, swz, nblocks, P<unsigned long long>(st), P<uint32_t>(sink), S(stream));
-  });
 #include "bindings.inc"
 }

@@ -342,7 +342,9 @@ size_t scan_records(const uint8_t* buf, size_t n, bool verify_crc, bool skip_bad
       }
       throw std::runtime_error("TFRecord: corrupt length CRC at offset " + std::to_string(off));
     }
-    if (off + 12 + len + 4 > n) {
+    // no wraparound: a corrupt or hostile 64-bit length must not pass the bounds check
+    // (RecordRef stores 32-bit lengths, so anything wider is rejected as well)
+    if (len > n - off - 12 || n - off - 12 - len < 4 || len > UINT32_MAX) {
       if (skip_bad) {
         ++*bad_records;
         break;

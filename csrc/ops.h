@@ -15,11 +15,6 @@
 
 namespace rocfm {
 
-// probe.hip
-void launch_probe(float* out, int n, hipStream_t stream);
-void launch_frag_probe(const uint16_t* W, int K, int swz, int nblocks, unsigned long long* st, uint32_t* sink,
-                       hipStream_t stream);
-
 // deepfm_rows.hip
 RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0);
 void launch_deepfm_rows(RowsParams p, hipStream_t stream);

@@ -107,6 +107,7 @@ class Config:
     seed: int = 1234
     save_checkpoints_steps: int = 0  # 0 → only at end (plus save_checkpoints_secs)
     save_checkpoints_secs: int = 600  # Estimator default cadence
+    ckpt_poll_steps: int = 200  # world > 1: steps between rank 0's broadcasts of the time-based save decision
     keep_checkpoint_max: int = 5
     eval_every_epoch: bool = True
     deterministic: bool = True

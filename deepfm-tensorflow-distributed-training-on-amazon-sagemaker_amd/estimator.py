@@ -239,7 +239,7 @@ class Estimator:
                 log_line(step, self.batch_loss())
             if cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0:
                 self.save()
-            elif cfg.save_checkpoints_secs and time.time() - self._last_save_t > cfg.save_checkpoints_secs:
+            elif cfg.save_checkpoints_secs and self._time_to_save(step):
                 self.save()
             for h in hooks:
                 h(self, step)
@@ -315,6 +315,22 @@ class Estimator:
         t = torch.tensor([n if n is not None else -1], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctrl_group())
         return int(t.item()) if int(t.item()) >= 0 else None
+
+    def _time_to_save(self, step: int) -> bool:
+        """Time-based checkpoint cadence (Estimator's save_checkpoints_secs).  Saving is
+        collective (state gathers, barriers), so with several ranks the decision is rank 0's
+        clock, broadcast on the host control group at an agreed step cadence
+        (``ckpt_poll_steps``); every rank then saves at the same step.  Deciding on each rank's
+        own clock let two ranks cross the interval on different steps and deadlock."""
+        due = time.time() - self._last_save_t > self.cfg.save_checkpoints_secs
+        if self.world == 1:
+            return due
+        poll = max(1, int(self.cfg.ckpt_poll_steps))
+        if step % poll != 0:
+            return False
+        t = torch.tensor([1 if due else 0], dtype=torch.int64)
+        dist.broadcast(t, src=0, group=self._ctrl_group())
+        return bool(int(t.item()))
 
     def _lockstep(self, batches):
         """Stream mode (or skip_bad): agree per step, on the host control group, that every rank
@@ -437,6 +453,13 @@ class Estimator:
         if not done:
             return 0, 0
         per_epoch = self._dataset(files, 1, training=True).num_batches()
+        if self.world > 1:
+            # train() runs the MIN over ranks of the shard batch counts (_agreed_steps); the
+            # resume split must use that same agreed count on every rank, or ranks with one
+            # more batch per epoch skip differently and run different numbers of collective steps
+            t = torch.tensor([per_epoch if per_epoch is not None else -1], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctrl_group())
+            per_epoch = int(t.item()) if int(t.item()) >= 0 else None
         if not per_epoch:
             return 0, 0
         return min(done // per_epoch, num_epochs), done % per_epoch

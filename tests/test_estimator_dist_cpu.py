@@ -90,3 +90,91 @@ def test_unequal_shards_lockstep(tmp_path):
                        join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
     assert got["step"] == 3
+
+
+def _ckpt_worker(rank, world, port, data_dir, model_dir, out):
+    """Time-based checkpoints with skewed rank clocks: rank 1 is slow every step, so each rank's own
+    clock would cross save_checkpoints_secs on different steps (deadlock)."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rocfm.config import parse_flags
+    from rocfm.estimator import Estimator
+
+    argv = _argv(data_dir, model_dir, "dp")
+    i = argv.index("--save_checkpoints_secs")
+    argv[i + 1] = "1"
+    argv += ["--ckpt_poll_steps", "1", "--keep_checkpoint_max", "100"]
+    est = Estimator(parse_flags(argv))
+    saved = []
+    orig = est._save
+
+    def spy():
+        saved.append(est.global_step)
+        return orig()
+
+    est._save = spy
+
+    def slow(e, step):
+        time.sleep(0.35 if rank == 1 else 0.0)
+
+    est.train([os.path.join(data_dir, "tr.tfrecords")], num_epochs=1, hooks=[slow])
+    torch.save(saved, out + f".{rank}")
+    est.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_time_based_checkpoint_is_collective(tmp_path):
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+
+    d = tmp_path / "data"
+    d.mkdir()
+    write_synthetic_tfrecord(str(d / "tr.tfrecords"), 2 * 128 * 8, 2000, seed=1)  # 8 steps per rank
+    out = str(tmp_path / "o.pt")
+    mp.start_processes(_ckpt_worker, args=(2, _port(), str(d), str(tmp_path / "m"), out), nprocs=2, join=True,
+                       start_method="spawn")
+    s0, s1 = torch.load(out + ".0"), torch.load(out + ".1")
+    assert s0 == s1, (s0, s1)  # every rank saved at the same steps
+    assert len(s0) >= 2  # at least one time-based save before the final one
+
+
+def _resume_worker(rank, world, port, data_dir, model_dir, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rocfm.config import parse_flags
+    from rocfm.estimator import Estimator
+
+    est = Estimator(parse_flags(_argv(data_dir, model_dir, "dp")))
+    rp = est.resume_point([os.path.join(data_dir, "tr.tfrecords")], 2)
+    torch.save({"step": est.global_step, "rp": rp}, out + f".{rank}")
+    est.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_resume_point_agreed_over_unequal_shards(tmp_path):
+    """512 / 511 records at batch 128 → 4 vs 3 batches per epoch; a job restored at step 5 must
+    split (epoch, skip) with the agreed count 3 on both ranks: (1, 2)."""
+    from rocfm import checkpoint as ckpt
+    from rocfm.config import parse_flags
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.estimator import Estimator
+
+    d = tmp_path / "data"
+    d.mkdir()
+    write_synthetic_tfrecord(str(d / "tr.tfrecords"), 1023, 2000, seed=1)
+    md = str(tmp_path / "m")
+    one = Estimator(parse_flags(_argv(str(d), md, "auto")))
+    sd = one.state_dict()
+    sd["global_step"] = torch.tensor(5, dtype=torch.int64)
+    ckpt.save_checkpoint(md, sd, 5)
+    out = str(tmp_path / "o.pt")
+    mp.start_processes(_resume_worker, args=(2, _port(), str(d), md, out), nprocs=2, join=True,
+                       start_method="spawn")
+    r0, r1 = torch.load(out + ".0"), torch.load(out + ".1")
+    assert r0["step"] == r1["step"] == 5
+    assert tuple(r0["rp"]) == tuple(r1["rp"]) == (1, 2)
