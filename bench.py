@@ -91,7 +91,15 @@ def main():
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # ROCFM_FORCE_COLLECTIVES=1 (one process): a 1-rank process group whose exchanges still run the
+    # backend's collectives (rehearses the RCCL calls the multi-GPU node captures)
+    pg = world > 1 or os.environ.get("ROCFM_FORCE_COLLECTIVES", "0") == "1"
+    if pg:
+        if world == 1:  # plain `python bench.py` (no launcher): a local 1-rank rendezvous
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -185,20 +193,23 @@ def main():
     if hasattr(eng, "precapture"):
         eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(a.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
+    # every rank's own timed window → the slowest (reported) and fastest rank
+    t = torch.tensor([dt, -dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    dt, dt_min = float(t[0].item()), -float(t[1].item())
+    if hasattr(eng, "check"):
+        eng.check()  # sticky device flags (exchange overflow, p2p peer timeout, BN barrier): fail loudly
     ms = dt / a.steps * 1e3
     value = B * world * a.steps / dt
     base = EAGER_BASELINE.get(a.embedding_update)
@@ -224,8 +235,11 @@ def main():
             "engine": a.engine,
             "embedding_update": a.embedding_update,
             "exchange_capacity": cap,
-            "exchange": getattr(eng, "exchange", None) if world > 1 else None,
+            "exchange": getattr(eng, "exchange", None) if pg else None,
         },
+        "world_size": dist.get_world_size() if pg else 1,
+        "backend": (dist.get_backend() if pg else None),
+        "rank_ms_per_step": {"max": round(ms, 4), "min": round(dt_min / a.steps * 1e3, 4)},
     }
     if rank == 0:
         line = json.dumps(out)
@@ -235,7 +249,7 @@ def main():
                 f.write(line + "\n")
     if hasattr(eng, "close"):
         eng.close()  # graphs holding RCCL collectives must go before the process group
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -48,6 +48,14 @@ def _world() -> int:
     return dist.get_world_size() if dist.is_initialized() else 1
 
 
+def force_collectives() -> bool:
+    """ROCFM_FORCE_COLLECTIVES=1: with a process group of ONE rank, still run every exchange
+    through the backend's collective (RCCL at world 1 copies through its own kernels) instead of
+    the world-1 shortcut (alias / no-op).  Lets a one-GPU box capture and replay the exact RCCL
+    calls (all_gather_into_tensor, all_to_all_single, all_reduce) the multi-GPU node runs."""
+    return os.environ.get("ROCFM_FORCE_COLLECTIVES", "0") == "1" and dist.is_initialized()
+
+
 def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor) -> None:
     """all_gather into a [world*n] buffer; RCCL fast path, host-staged fallback for gloo."""
     if dist.get_backend() == "nccl":
@@ -161,6 +169,7 @@ class FusedDataParallel:
         self.check_every = int(check_every)
         self.device = e.device
         self.p2p = None
+        self.force = force_collectives()
         self.exchange = "rccl"  # DP all-gather transport (mode dp: p2p.open_exchanges may pick "p2p")
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
@@ -203,7 +212,7 @@ class FusedDataParallel:
                 self.p2p_params = self.p2p.params(self.send.data_ptr(), self.S)
             else:  # one rank: the gathered list IS the send buffer (no copy)
                 self.recv = (torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
-                             if self.world > 1 else self.send)
+                             if self.world > 1 or self.force else self.send)
                 self._recv_ptr = self.recv.data_ptr()
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
@@ -291,7 +300,7 @@ class FusedDataParallel:
         if self.p2p is not None:
             self.p2p.push(self.p2p_params)
             return
-        if self.world == 1:  # single rank: recv aliases send (dp) / the bucket is already the sum
+        if self.world == 1 and not self.force:  # one rank: recv aliases send (dp) / the bucket is the sum
             return
         if self.mode == "dense_dp":
             _all_reduce(self.bucket)

@@ -406,6 +406,9 @@ class FusedRowShard:
         from .dp import collectives_capturable
 
         self.graph_collectives = use_graph and collectives_capturable()
+        from .dp import force_collectives
+
+        self.force = force_collectives()
         if W > 1:
             from .dist import broadcast_tensors
 
@@ -633,7 +636,7 @@ class FusedRowShard:
                 chunk = out.numel() // self.W
                 prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
             ex.push(prm)
-        elif self.W > 1:
+        elif self.W > 1 or self.force:
             all_to_all_equal(out, inp)
         else:
             out.copy_(inp)
@@ -655,7 +658,7 @@ class FusedRowShard:
             if prm is None:
                 prm = self._p2p_params["mlp"] = self.x_mlp.params(e.dense_grads_flat.data_ptr(), self.P)
             self.x_mlp.push(prm)
-        elif self.W > 1:
+        elif self.W > 1 or self.force:
             all_reduce_(e.dense_grads_flat)
 
     def _step_body(self, p: int) -> None:

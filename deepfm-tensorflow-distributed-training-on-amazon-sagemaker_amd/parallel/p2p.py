@@ -20,6 +20,7 @@ The reference has no equivalent: Horovod hands the gradients to NCCL (HVD:296).
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 from typing import List, Optional, Tuple
@@ -28,6 +29,30 @@ import torch
 import torch.distributed as dist
 
 KIND_UNCACHED, KIND_FINEGRAINED, KIND_PLAIN = 0, 1, 2
+log = logging.getLogger("rocfm")
+
+
+def _pci_key(dev: torch.device) -> Tuple[int, int, int]:
+    pr = torch.cuda.get_device_properties(dev)
+    return (int(pr.pci_domain_id), int(pr.pci_bus_id), int(pr.pci_device_id))
+
+
+def peer_access_problem(device, keys: List[Tuple[int, int, int]], rank: int) -> Optional[str]:
+    """Why this rank's GPU cannot write into a peer rank's GPU, or None.  ``keys`` are every
+    rank's PCI (domain, bus, device).  A peer GPU that is visible in this process is checked with
+    hipDeviceCanAccessPeer; a peer on the SAME GPU (ranks sharing a card) needs no peer path; a
+    peer GPU this process cannot see (per-rank device masks) is left to the self-test."""
+    dev = torch.device(device)
+    mine = keys[rank]
+    local = {}
+    for d in range(torch.cuda.device_count()):
+        local[_pci_key(torch.device("cuda", d))] = d
+    for r, k in enumerate(keys):
+        if r == rank or k == mine or k not in local:
+            continue
+        if not torch.cuda.can_device_access_peer(dev.index, local[k]):
+            return f"GPU {dev.index} cannot access peer GPU {local[k]} (rank {r}): no xGMI/PCIe peer path"
+    return None
 
 
 def _hip():
@@ -76,10 +101,22 @@ class P2PExchange:
         # every rank takes part in every collective below even if a step fails on it, so that a
         # local failure becomes an agreed fallback (selftest) instead of a hang
         mine = None
+        if self.W > 1:  # peer-access check first (a failure becomes an agreed RCCL fallback below)
+            keys: List = [None] * self.W
+            dist.all_gather_object(keys, _pci_key(self.device), group=group)
+            try:
+                why = peer_access_problem(self.device, keys, self.rank)
+            except Exception as exc:  # property queries failing: leave the verdict to the self-test
+                why = None
+                log.debug("p2p peer-access check skipped: %s", exc)
+            if why:
+                self.init_error = RuntimeError(why)
         with torch.cuda.device(self.device):
             self.ctrl = torch.zeros(2, dtype=torch.int32, device=self.device)   # exchange count, arrivals
             self.error = torch.zeros(1, dtype=torch.int32, device=self.device)
             try:
+                if self.init_error is not None:
+                    raise self.init_error
                 self.recv_ptr = H.p2p_malloc(self.W * self.slot * 4, kind)
                 self._own.append(self.recv_ptr)
                 self.sig_ptr = H.p2p_malloc(max(256, 8 * self.W), kind)
@@ -238,10 +275,15 @@ def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None)
     for ex, n in zip(exs, slot_floats):
         ok = selftest(ex, n) and ok  # every rank runs every self-test (each one is agreed)
     if ok:
+        log.info("exchange: p2p push over IPC-mapped peer buffers (%d ranks, self-test passed)", world)
         return exs
     err = next((ex.init_error for ex in exs if ex.init_error is not None), None)
     for ex in exs:
         ex.close()
     if choice == "p2p":
         raise RuntimeError(f"p2p exchange unavailable: {err or 'self-test failed'}")
+    reason = f"{err}" if err else "self-test failed on some rank"
+    log.warning("exchange: falling back to RCCL (p2p unavailable: %s)", reason)
+    if dist.get_rank() == 0:
+        print(f"[rocfm] exchange: falling back to RCCL (p2p unavailable: {reason})", flush=True)
     return None
