@@ -185,12 +185,20 @@ struct CtShape {
 // adds no global store (and no vmcnt wait) inside the measured phases.
 #define ROWS_STAMP(i)                                                                             \
   do {                                                                                            \
-    if (p.stamps != nullptr && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime();   \
+    if (DIAG && p.stamps != nullptr && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // FP8 is a template parameter (not a runtime branch on p.fp8): the fp8 input-layer path kept in the
 // bf16 kernel raised its register demand past the 256 VGPRs of a 2-wave/SIMD workgroup and spilled.
-template <int KP4, class SH, bool FP8>
+// MODE (kInfer / kTrain / kDynamic = read p.train) and DIAG (phase stamps + ablations) are template
+// parameters as well: in the compile-time-shape kernels a runtime `if (train)` around the backward
+// weight prefetch, or an ablation test around a phase, splits the memory-op stream into branches,
+// and the waitcnt insertion then merges them pessimistically — it waited for EVERY outstanding
+// load and activation store (vmcnt(0..5)) at each hidden layer instead of only that layer's
+// prefetched fragments.  Branch-free static kernels wait only for what they consume.
+constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
+
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
@@ -208,6 +216,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   float* s_prm = reinterpret_cast<float*>(smem + L.prm);
 
   constexpr int Kp = KP4 * 4;
+  const bool train = MODE == kDynamic ? (p.train != 0) : (MODE == kTrain);
+  const int ablate = DIAG ? p.ablate : 0;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int row0 = blockIdx.x * kRowTile;
   const int F = sh.F, K = sh.K, NL = sh.nl;
@@ -224,29 +234,32 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // issued first; the layer-0 weight prefetch is issued behind them and lands during phase A.
   bf16x8 fw0[SH::KSF0];
   if constexpr (SH::kStatic) {
+    // every load unconditional (clamped index, value selected afterwards): no exec branches in
+    // the memory-op stream (see MODE above); the kernarg pointers are read up front
     constexpr int kItems = (kRowTile * SH::F + kRowThreads - 1) / kRowThreads;
+    const int32_t* ids_g = p.ids;
+    const float* vals_g = p.vals;
+    const int32_t* pos_g = p.contrib_pos ? p.contrib_pos : p.ids;  // any valid [B][F] int32 buffer
+    const bool has_pos = p.contrib_pos != nullptr;
+    const int nvalid = max(0, min(kRowTile, p.B - row0)) * F;  // valid lookups of this tile
+    const int last = max(p.B * F - 1, 0);                        // clamp target: a valid lookup
     int32_t idr[kItems];
     float vlr[kItems];
-#pragma unroll
-    for (int u = 0; u < kItems; ++u) {
-      const int i = t + u * kRowThreads;
-      const bool valid = i < kRowTile * F && row0 + fdiv(i, magicF) < p.B;
-      idr[u] = valid ? p.ids[(size_t)row0 * F + i] : 0;
-      vlr[u] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
-    }
     int32_t psr[kItems];
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
-      const bool valid = p.contrib_pos && i < kRowTile * F && row0 + fdiv(i, magicF) < p.B;
-      psr[u] = valid ? p.contrib_pos[(size_t)row0 * F + i] : (int32_t)((size_t)row0 * F + i);
+      const size_t gi = (size_t)min(row0 * F + i, last);
+      idr[u] = ids_g[gi];
+      vlr[u] = vals_g[gi];
+      psr[u] = pos_g[gi];
     }
     float br[SH::nl];
 #pragma unroll
-    for (int l = 0; l < SH::nl; ++l) br[l] = t < sh.dim(l + 1) ? p.bias[l][t] : 0.f;
-    const float wo = t < sh.dim(SH::nl) ? p.w_out[t] : 0.f;
-    const float lab = (t < kRowTile && row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
-    const float bo = t == 0 ? *p.b_out : 0.f, fb = t == 0 ? *p.fm_bias : 0.f;
+    for (int l = 0; l < SH::nl; ++l) br[l] = p.bias[l][min(t, sh.dim(l + 1) - 1)];
+    const float wo = p.w_out[min(t, sh.dim(SH::nl) - 1)];
+    const float lab = p.labels[min(row0 + (t & (kRowTile - 1)), max(p.B - 1, 0))];
+    const float bo = *p.b_out, fb = *p.fm_bias;
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
     for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
@@ -254,9 +267,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
       if (i < kRowTile * F) {
-        s_ids[i] = idr[u];
-        s_vals[i] = vlr[u];
-        s_pos[i] = psr[u];
+        const bool valid = i < nvalid;
+        s_ids[i] = valid ? idr[u] : 0;
+        s_vals[i] = valid ? vlr[u] : 0.f;
+        s_pos[i] = (valid && has_pos) ? psr[u] : (int32_t)((size_t)row0 * F + i);
       }
     }
 #pragma unroll
@@ -267,7 +281,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       s_prm[L.prm_bout] = bo;
       s_prm[L.prm_fmb] = fb;
     }
-    if (t < kRowTile) s_prm[L.prm_lab + t] = lab;
+    if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? lab : 0.f;
   } else {
     for (int i = t; i < kRowTile * F; i += kRowThreads) {
       const bool valid = row0 + fdiv(i, magicF) < p.B;
@@ -302,18 +316,28 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const int rf = idx / KP4, c4 = idx - rf * KP4;
         v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
       }
+      // every gathered row is consumed (scaled) in straight-line code before any branch, so the
+      // four loads are waited for once; the branches below hold LDS stores only
+      float ev[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = min(base + u * kRowThreads + t, nitems - 1);
+        const float x = s_vals[idx / KP4];
+        ev[u][0] = v[u].x * x;
+        ev[u][1] = v[u].y * x;
+        ev[u][2] = v[u].z * x;
+        ev[u][3] = v[u].w * x;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int idx = base + u * kRowThreads + t;
         if (idx < nitems) {
           const int rf = idx / KP4, c4 = idx - rf * KP4;
           const int r = fdiv(rf, magicF), f = rf - r * F;
-          const float x = s_vals[rf];
-          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int k = c4 * 4 + c;
-            const float e = vv[c] * x;
+            const float e = ev[u][c];
             if (k < K) {
               s_f32[r * D0p + f * K + k] = e;
               h0[r * lda + f * K + k] = f2bf(e);
@@ -333,7 +357,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   ROWS_STAMP(2);
 
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
-  if (!(p.ablate & 2)) {
+  if (!(ablate & 2)) {
     const int r = t >> 5, q = t & 31;
     float cterm = 0.f, yw = 0.f, amx = 0.f;
     // G = ⌊32/K⌋ lanes per embedding column split the F fields (field f → group f mod G); the
@@ -388,7 +412,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
     if (q == 0) s_ylin[r] = s_prm[L.prm_fmb] + yw + 0.5f * cterm;
   }
-  if (p.train && !(p.ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
+  if (train && !(ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
     for (int it = t; it < D0p * 2; it += kRowThreads) {
@@ -404,7 +428,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
   bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
   bf16x8 bw0[SH::NJB0][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
-  if constexpr (SH::kStatic) if (!(p.ablate & 4)) {
+  if constexpr (SH::kStatic) if (!(ablate & 4)) {
     if constexpr (SH::nl >= 2) {
       const int nt = min(wave, sh.dim(2) / 16 - 1);
 #pragma unroll
@@ -415,7 +439,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
       for (int u = 0; u < SH::KSF2; ++u) fw2[u] = ld_frag(p.WTs[2] + frag_at(nt, u, sh.dim(2), lane));
     }
-    if (p.train) {
+    if (train) {
       // backward of layer 0: dh0 tiles w + 8j of dims[0]/16, k = dims[1]
 #pragma unroll
       for (int j = 0; j < SH::NJB0; ++j) {
@@ -444,7 +468,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     uint16_t* O = reinterpret_cast<uint16_t*>(smem + L.act[l + 1]);
     const int lda = L.lda[l], ldo = L.lda[l + 1];
     const float keep = p.keep[l];
-    const bool drop = p.train && keep < 1.f;
+    const bool drop = train && keep < 1.f;
     const float inv_keep = 1.f / keep;
     lds_barrier();  // previous layer's tile (and phase A/B) complete
     ROWS_STAMP(3 + l);
@@ -494,10 +518,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float a = fmaxf(acc[i] + bc, 0.f);
-            if (!p.train)
+            if (!train)
               a = (a - p.bn_mean[l][c]) * rsqrtf(p.bn_var[l][c] + p.bn_eps) * p.bn_gamma[l][c] + p.bn_beta[l][c];
             if (row0 + rb + i >= p.B) a = 0.f;
-            if (p.train)
+            if (train)
               R[(rb + i) * Dout + c] = a;
             else
               O[(rb + i) * ldo + c] = f2bf(a);
@@ -516,12 +540,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         hv[i] = a;
         O[(rb + i) * ldo + c] = f2bf(a);
       }
-      if (p.train)
+      if (train)
         *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
     }
     if constexpr (!SH::kStatic) {
-      if (p.bn && p.train) {
+      if (p.bn && train) {
         // batch moments of r over all B rows: this workgroup's (mean, M2) per column → grid
         // barrier → Chan's combination in workgroup order (deterministic) → normalise, dropout
         lds_barrier();
@@ -614,10 +638,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         p.prob[gr] = pr;
         if (p.loss_rows) p.loss_rows[gr] = loss;
       }
-      if (p.train) p.g_out[gr] = g;
+      if (train) p.g_out[gr] = g;
     }
   }
-  if (!p.train) return;
+  if (!train) return;
 
   // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E)
   const int nitemsF = kRowTile * F * KP4;
@@ -823,33 +847,40 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
       }
     }
+    // all four items' gradient rows are computed in straight-line code (clamped items, LDS reads
+    // and the prefetched rows) before the first store: one wait for rowsF, and no store of an
+    // earlier item is waited for by a later one
+    float o[4][4];
+    int dst[4];
+    bool ok[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int idx = base + u * kRowThreads + t;
-      if (idx >= nitemsF) continue;
+      const int idx0 = base + u * kRowThreads + t;
+      const int idx = min(idx0, nitemsF - 1);
       const int rf = idx / KP4, c4 = idx - rf * KP4;
       const int r = fdiv(rf, magicF), f = rf - r * F;
-      if (row0 + r >= p.B) continue;
+      ok[u] = idx0 < nitemsF && row0 + r < p.B;
       const float g = s_g[r], x = s_vals[rf];
       const float* S = s_S + r * K;
       const float* dh = s_f32 + r * D0p + f * K;
       const float vv[4] = {rowsF[u].x, rowsF[u].y, rowsF[u].z, rowsF[u].w};
-      float o[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int k = c4 * 4 + c;
-        o[c] = (k < K) ? x * (g * (S[k] - vv[c] * x) + dh[k]) : ((k == K) ? g * x : 0.f);
+        o[u][c] = (k < K) ? x * (g * (S[min(k, K - 1)] - vv[c] * x) + dh[min(k, K - 1)]) : ((k == K) ? g * x : 0.f);
       }
-      reinterpret_cast<float4*>(p.contrib + (size_t)s_pos[r * F + f] * Kp)[c4] =
-          make_float4(o[0], o[1], o[2], o[3]);
+      dst[u] = s_pos[rf] * KP4 + c4;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
   }
   lds_barrier();
   ROWS_STAMP(12);
   if constexpr (!SH::kStatic) {
     if (p.bn) bn_grid_exit(p);
   }
-  if (p.stamps != nullptr) {
+  if (DIAG && p.stamps != nullptr) {
     lds_barrier();
     if (t < 13) p.stamps[blockIdx.x * 16 + t] = s_stamp[t];
   }
@@ -914,23 +945,24 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
   return L;
 }
 
-template <int KP4, class SH, bool FP8>
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG>
 static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
+  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG>;
   static bool attr_set = false;
   static int max_dyn = 0;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
     hipFuncAttributes fa{};
-    ROCFM_HIP_CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>)));
+    ROCFM_HIP_CHECK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)));
     max_dyn = 160 * 1024 - (int)fa.sharedSizeBytes;
-    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>),
+    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn));
     attr_set = true;
   }
   ROCFM_REQUIRE(p.lds.total <= max_dyn, "deepfm_rows: LDS layout exceeds the 160 KiB per workgroup");
   if (p.bn && p.train) {  // grid barriers: every workgroup must be resident at once
     int per_cu = 0, dev = 0, cus = 0;
-    ROCFM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(deepfm_rows_kernel<KP4, SH, FP8>), kRowThreads, p.lds.total));
+    ROCFM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern),
+                                                                 kRowThreads, p.lds.total));
     ROCFM_HIP_CHECK(hipGetDevice(&dev));
     ROCFM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     // the occupancy query can over-report by one block per CU: trust one fewer when it says > 1
@@ -938,19 +970,38 @@ static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
     ROCFM_REQUIRE(p.Bp / kRowTile <= limit, "deepfm_rows: batch_norm needs every workgroup of the batch resident "
                                             "at once (batch too large for one launch; use engine=torch)");
   }
-  hipLaunchKernelGGL((deepfm_rows_kernel<KP4, SH, FP8>), dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream,
-                     p);
+  hipLaunchKernelGGL(kern, dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream, p);
 }
 
+// Static shapes: branch-free train / inference kernels; the diagnostic (stamps, ablations)
+// instantiation only for the benchmark shape's training kernel.
 template <int KP4, class SH>
 static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   if constexpr (SH::kStatic) {
+    const bool diag = p.stamps != nullptr || p.ablate != 0;
+    if (diag) {
+      if constexpr (SH::F == 39 && SH::K == 10 && SH::nl == 3) {
+        ROCFM_REQUIRE(!p.fp8 && p.train, "deepfm_rows: diagnostics are built for the bf16 training kernel only");
+        launch_rows_impl<KP4, SH, false, kTrain, true>(p, stream);
+        return;
+      } else {
+        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 shape");
+      }
+    }
     if (p.fp8) {
-      launch_rows_impl<KP4, SH, true>(p, stream);
+      if (p.train)
+        launch_rows_impl<KP4, SH, true, kTrain, false>(p, stream);
+      else
+        launch_rows_impl<KP4, SH, true, kInfer, false>(p, stream);
       return;
     }
+    if (p.train)
+      launch_rows_impl<KP4, SH, false, kTrain, false>(p, stream);
+    else
+      launch_rows_impl<KP4, SH, false, kInfer, false>(p, stream);
+    return;
   }
-  launch_rows_impl<KP4, SH, false>(p, stream);
+  launch_rows_impl<KP4, SH, false, kDynamic, true>(p, stream);
 }
 
 // Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
