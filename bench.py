@@ -61,7 +61,9 @@ def parse():
     ap.add_argument("--dp_exchange", default="auto", choices=["auto", "p2p", "rccl"],
                     help="N>1 exchanges (dp all-gather, row-shard all-to-all + all-reduce): p2p push over "
                          "IPC-mapped peer buffers (one node) or RCCL")
-    ap.add_argument("--steps_per_graph", type=int, default=64, help="fused engine: steps captured per HIP graph")
+    ap.add_argument("--steps_per_graph", type=int, default=0,
+                    help="fused engine: steps captured per HIP graph (0 = min(64, steps): a graph's side chain "
+                         "prepares exactly the next graph's batches, none beyond the timed window)")
     ap.add_argument("--capacity", default="auto",
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
                          "over the batch pool, 'safe' = batch_size*field_size (never overflows), or a number")
@@ -189,6 +191,8 @@ def main():
     if world > 1 and hasattr(eng, "set_lr_scale"):
         eng.set_lr_scale(float(world))  # Horovod linear LR scaling (HVD:171)
 
+    if a.steps_per_graph <= 0:
+        a.steps_per_graph = max(2, min(64, a.steps))
     run(a.warmup)
     if hasattr(eng, "precapture"):
         eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region

@@ -152,6 +152,9 @@ __device__ __forceinline__ int bn_rows(int B, int w) { return max(0, min(kRowTil
 struct RtShape {
   static constexpr bool kStatic = false;
   static constexpr int KSF0 = 1, KSF1 = 1, KSF2 = 1, NJB0 = 1, KSB0 = 1, KSB1 = 1, KSB2 = 1;
+  static constexpr int GU = 4;                 // gathered rows per thread per batch (phases A, F)
+  static constexpr int KSF0E = 1, NJB0H = 1;
+  static constexpr bool kLateBw0 = false;
   int F, K, nl, d[kMaxHidden + 1];
   __device__ explicit RtShape(const RowsParams& p) : F(p.F), K(p.K), nl(p.nl) {
 #pragma unroll
@@ -161,9 +164,14 @@ struct RtShape {
 };
 
 // Compile-time shape: F fields, K embedding dims, hidden widths D1 ≥ … (0 = absent), ≤ 3 layers of
-// ≤ 128 units, F·K ≤ 512 (host-checked).  Fragment-prefetch counts per wave:
+// ≤ 128 units, F·K ≤ 1280 (host-checked).  Fragment-prefetch counts per wave:
 //   forward layer l : one 16-column tile (wave w owns tile w), dims[l]/32 k-steps   → KSF_l
 //   backward li     : tiles w, w+8, … of dims[li]/16 (NJB_li of them), dims[li+1]/32 k-steps → KSB_li
+// GU: gathered table rows per thread (phases A and F issue all of a tile's loads at once).
+// kLateBw0: the layer-0 forward and backward fragments together exceed the register budget (wide
+// input layers, e.g. the notebook's 39×32 = 1248): the backward ones are then prefetched at the
+// last hidden layer's forward GEMM (under it, the head and the upper backward layers) instead of
+// before layer 0, and phase F re-gathers its rows after the layer-0 backward GEMM.
 template <int F_, int K_, int D1, int D2, int D3>
 struct CtShape {
   static constexpr bool kStatic = true;
@@ -174,9 +182,19 @@ struct CtShape {
   static constexpr int KSF0 = D0 / 32, KSF1 = D1 / 32 > 0 ? D1 / 32 : 1, KSF2 = D2 / 32 > 0 ? D2 / 32 : 1;
   static constexpr int NJB0 = (D0 / 16 + kWaves - 1) / kWaves;
   static constexpr int KSB0 = D1 / 32, KSB1 = D2 / 32 > 0 ? D2 / 32 : 1, KSB2 = D3 / 32 > 0 ? D3 / 32 : 1;
+  static constexpr int KP4 = (K_ + 1 + 3) / 4;
+  static constexpr int GU = (kRowTile * F_ * KP4 + kRowThreads - 1) / kRowThreads;
+  static constexpr bool kLateBw0 = (KSF0 + NJB0 * KSB0) * 4 > 128;
+  // layer-0 forward fragments prefetched at kernel entry; kLateBw0 shapes load the rest after the
+  // gather (phase A holds GU gathered rows + their scaled copies in registers)
+  static constexpr int KSF0E = kLateBw0 ? 8 : KSF0;
+  // registers for layer-0 backward fragments: all NJB0 tiles, or (kLateBw0) the first half — each
+  // slot is refilled with tile j + NJB0H right after tile j's MFMAs have been issued
+  static constexpr int NJB0H = kLateBw0 ? (NJB0 + 1) / 2 : NJB0;
   __device__ explicit CtShape(const RowsParams&) {}
-  static_assert(D0 <= 512 && D1 <= 128 && D2 <= 128 && D3 <= 128, "CtShape limits");
+  static_assert(D0 <= 1280 && D1 <= 128 && D2 <= 128 && D3 <= 128, "CtShape limits");
   static_assert(D1 % 32 == 0 && D2 % 32 == 0 && D3 % 32 == 0, "hidden dims padded to 32");
+  static_assert(GU <= 12, "CtShape: at most 12 gathered rows per thread");
 };
 
 }  // namespace
@@ -262,7 +280,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float bo = *p.b_out, fb = *p.fm_bias;
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-    for (int u = 0; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
+    for (int u = 0; u < SH::KSF0E; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
@@ -308,19 +326,20 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     uint16_t* h0 = reinterpret_cast<uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
     const int nitems = kRowTile * F * KP4;
-    for (int base = 0; base < nitems; base += kRowThreads * 4) {
-      float4 v[4];
+    constexpr int U = SH::GU;  // static shapes: the whole tile's rows in one batch
+    for (int base = 0; base < nitems; base += kRowThreads * U) {
+      float4 v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitems - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
         v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
       }
       // every gathered row is consumed (scaled) in straight-line code before any branch, so the
       // four loads are waited for once; the branches below hold LDS stores only
-      float ev[4][4];
+      float ev[U][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitems - 1);
         const float x = s_vals[idx / KP4];
         ev[u][0] = v[u].x * x;
@@ -329,7 +348,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         ev[u][3] = v[u].w * x;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int idx = base + u * kRowThreads + t;
         if (idx < nitems) {
           const int rf = idx / KP4, c4 = idx - rf * KP4;
@@ -355,6 +374,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   lds_barrier();
   ROWS_STAMP(2);
+
+  if constexpr (SH::kStatic && SH::KSF0E < SH::KSF0) {  // the rest of layer 0's forward fragments
+    const int nt = min(wave, sh.dim(1) / 16 - 1);
+#pragma unroll
+    for (int u = SH::KSF0E; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
+  }
 
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
   if (!(ablate & 2)) {
@@ -427,8 +452,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 
   // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
   bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
-  bf16x8 bw0[SH::NJB0][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
-  if constexpr (SH::kStatic) if (!(ablate & 4)) {
+  bf16x8 bw0[SH::NJB0H][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
+  // forward layers 1..2 and the upper backward layers' fragments (a few KiB per wave)
+  auto prefetch_upper = [&]() {
+    if constexpr (SH::kStatic) {
     if constexpr (SH::nl >= 2) {
       const int nt = min(wave, sh.dim(2) / 16 - 1);
 #pragma unroll
@@ -440,13 +467,6 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       for (int u = 0; u < SH::KSF2; ++u) fw2[u] = ld_frag(p.WTs[2] + frag_at(nt, u, sh.dim(2), lane));
     }
     if (train) {
-      // backward of layer 0: dh0 tiles w + 8j of dims[0]/16, k = dims[1]
-#pragma unroll
-      for (int j = 0; j < SH::NJB0; ++j) {
-        const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
-#pragma unroll
-        for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
-      }
       if constexpr (SH::nl >= 2) {
         const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
@@ -456,6 +476,21 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const int nt = min(wave, sh.dim(2) / 16 - 1);
 #pragma unroll
         for (int u = 0; u < SH::KSB2; ++u) bw2[u] = ld_frag(p.Wbs[2] + frag_at(nt, u, sh.dim(3), lane));
+      }
+    }
+    }
+  };
+  if constexpr (SH::kStatic) if (!(ablate & 4)) {
+    if constexpr (!SH::kLateBw0) {  // wide input layers: issued once layer 0's forward fragments are dead
+      prefetch_upper();
+      if (train) {
+        // backward of layer 0: dh0 tiles w + 8j of dims[0]/16, k = dims[1]
+#pragma unroll
+        for (int j = 0; j < SH::NJB0; ++j) {
+          const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
+#pragma unroll
+          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+        }
       }
     }
   }
@@ -472,6 +507,19 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float inv_keep = 1.f / keep;
     lds_barrier();  // previous layer's tile (and phase A/B) complete
     ROWS_STAMP(3 + l);
+    if constexpr (SH::kStatic && SH::kLateBw0) {
+      if (l == 1 && !(ablate & 4)) prefetch_upper();
+      // from the last hidden layer on, only its own forward fragments are live: the layer-0 backward
+      // ones now (hidden under that layer, the head and the upper backward layers)
+      if (l == SH::nl - 1 && train && !(ablate & 4)) {
+#pragma unroll
+        for (int j = 0; j < SH::NJB0H; ++j) {
+          const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
+#pragma unroll
+          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+        }
+      }
+    }
     const int ntiles = Dout >> 4;
     for (int nt = wave; nt < ntiles; nt += kWaves) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -643,14 +691,18 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   if (!train) return;
 
-  // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E)
+  // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E);
+  // kLateBw0 shapes re-read them after the layer-0 backward GEMM (register budget)
   const int nitemsF = kRowTile * F * KP4;
-  float4 rowsF[4];
+  constexpr int UF = SH::GU;
+  float4 rowsF[UF];
+  if constexpr (!SH::kLateBw0) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int idx = min(u * kRowThreads + t, nitemsF - 1);
-    const int rf = idx / KP4, c4 = idx - rf * KP4;
-    rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+    for (int u = 0; u < UF; ++u) {
+      const int idx = min(u * kRowThreads + t, nitemsF - 1);
+      const int rf = idx / KP4, c4 = idx - rf * KP4;
+      rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+    }
   }
   lds_barrier();
 
@@ -769,13 +821,31 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const uint16_t* ap = dz_cur + (lane & 15) * ldz + 8 * (lane >> 4);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) accs[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (li == 0) {
+        if (li == 0 && SH::kLateBw0) {
+          // tile-major, software-pipelined over the NJB0H fragment slots (see CtShape::NJB0H)
+          bf16x8 av[SH::KSB0];
+#pragma unroll
+          for (int u = 0; u < SH::KSB0; ++u) av[u] = ld_frag(ap + 32 * u);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int slot = j < SH::NJB0H ? j : j - SH::NJB0H;
+            if (nt0 + kWaves * j < ntiles) {
+#pragma unroll
+              for (int u = 0; u < SH::KSB0; ++u) accs[j] = mfma16x16x32(av[u], bw0[slot][u], accs[j]);
+            }
+            if (j < SH::NJB0H && j + SH::NJB0H < SH::NJB0) {
+              const int nt = min(wave + kWaves * (j + SH::NJB0H), sh.dim(0) / 16 - 1);
+#pragma unroll
+              for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+            }
+          }
+        } else if (li == 0) {
 #pragma unroll
           for (int u = 0; u < SH::KSB0; ++u) {
             const bf16x8 av = ld_frag(ap + 32 * u);
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
-              if (j < SH::NJB0 && nt0 + kWaves * j < ntiles) accs[j] = mfma16x16x32(av, bw0[j][u], accs[j]);
+              if (j < SH::NJB0H && nt0 + kWaves * j < ntiles) accs[j] = mfma16x16x32(av, bw0[j][u], accs[j]);
           }
         } else if (li == 1) {
 #pragma unroll
@@ -838,10 +908,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   ROWS_STAMP(11);
 
   // ---- phase F: FM backward → per-lookup gradient rows -----------------------------------------
-  for (int base = 0; base < nitemsF; base += kRowThreads * 4) {
-    if (base > 0) {  // more than 4 items per thread (large F·Kp): load this batch now
+  for (int base = 0; base < nitemsF; base += kRowThreads * UF) {
+    if (base > 0 || SH::kLateBw0) {  // more rows than one batch (large F·Kp), or not prefetched
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < UF; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitemsF - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
         rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
@@ -850,11 +920,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     // all four items' gradient rows are computed in straight-line code (clamped items, LDS reads
     // and the prefetched rows) before the first store: one wait for rowsF, and no store of an
     // earlier item is waited for by a later one
-    float o[4][4];
-    int dst[4];
-    bool ok[4];
+    float o[UF][4];
+    int dst[UF];
+    bool ok[UF];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UF; ++u) {
       const int idx0 = base + u * kRowThreads + t;
       const int idx = min(idx0, nitemsF - 1);
       const int rf = idx / KP4, c4 = idx - rf * KP4;
@@ -872,7 +942,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       dst[u] = s_pos[rf] * KP4 + c4;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < UF; ++u)
       if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
   }
   lds_barrier();
@@ -989,11 +1059,15 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
       }
     }
     if (p.fp8) {
-      if (p.train)
-        launch_rows_impl<KP4, SH, true, kTrain, false>(p, stream);
-      else
-        launch_rows_impl<KP4, SH, true, kInfer, false>(p, stream);
-      return;
+      if constexpr (SH::kLateBw0) {  // the fp8 quantisation of a wide input layer's fragments spills
+        throw std::invalid_argument("deepfm_rows: compute_dtype=fp8 supports input layers up to 512 wide");
+      } else {
+        if (p.train)
+          launch_rows_impl<KP4, SH, true, kTrain, false>(p, stream);
+        else
+          launch_rows_impl<KP4, SH, true, kInfer, false>(p, stream);
+        return;
+      }
     }
     if (p.train)
       launch_rows_impl<KP4, SH, false, kTrain, false>(p, stream);
@@ -1037,13 +1111,14 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   }
   if (!p.force_generic && !p.bn) {
     if (try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
-        try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream)) {
+        try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream) ||
+        try_static<39, 32, 128, 64, 32>(p, stream)) {
       ROCFM_HIP_CHECK(hipGetLastError());
       return;
     }
   }
   ROCFM_REQUIRE(!p.fp8, "deepfm_rows: compute_dtype=fp8 needs a compile-time-shape instantiation (39 fields, "
-                        "k in {8,10,12}, MLP 128-64-32 or 64-32) or compute_dtype=bf16");
+                        "k in {8,10,12,32}, MLP 128-64-32 or 64-32) or compute_dtype=bf16");
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N)                          \
   case N:                                     \

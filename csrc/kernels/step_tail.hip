@@ -11,6 +11,7 @@
 namespace rocfm {
 
 constexpr int kTailThreads = 512;
+constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
 template <int KP4>
@@ -24,7 +25,8 @@ __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradPara
 }
 
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
-  ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= 32 && e.K1 <= e.Kp, "step_tail: Kp must be a multiple of 4 and <= 32");
+  ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= kTailMaxKp && e.K1 <= e.Kp,
+                "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
   const int n_wg = wgrad_prepare(w);
   const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
@@ -35,9 +37,11 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
     hipLaunchKernelGGL(step_tail_kernel<N>, grid, block, 0, stream, w, e, n_emb); \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12)
 #undef ROCFM_KP4
-    default:  // the 512-entry row staging of larger rows + the wgrad tiles exceed 160 KiB of LDS
-      throw std::invalid_argument("step_tail: Kp > 32 unsupported (use mlp_wgrad + emb_rows_update)");
+    default:  // the 512-entry row staging of larger rows (8 KiB per float4 column) + the wgrad
+              // reduction tiles exceed 160 KiB of LDS beyond Kp = 48
+      throw std::invalid_argument("step_tail: Kp > 48 unsupported (use mlp_wgrad + emb_rows_update)");
   }
   ROCFM_HIP_CHECK(hipGetLastError());
 }

@@ -654,7 +654,7 @@ class FusedDeepFM:
                 rows, _, _, ep, _ = self.m_params[q][k]
                 rows.contrib_pos = self.m_pos[q, k * n:].data_ptr()
                 ep.sorted_contrib = 1
-                if self.Kp <= 32:  # the fused tail's 512-entry chunks
+                if self.Kp <= self.H.tail_max_kp():  # the fused tail's 512-entry chunks
                     ep.chunk_end = self.m_cend[q, k * self.m_nch:].data_ptr()
         self._m_graphs = {}
         self._m_primed = False
@@ -781,7 +781,7 @@ class FusedDeepFM:
     def _tail(self, wp, ep, ed, s: int) -> None:
         """MLP weight gradients + embedding update: one launch (step_tail.hip) when the rows fit."""
         H = self.H
-        if self.Kp <= 32:
+        if self.Kp <= H.tail_max_kp():
             H.step_tail(wp, ep, s)
         else:
             H.mlp_wgrad(wp, s)

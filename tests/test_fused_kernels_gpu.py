@@ -41,7 +41,8 @@ def _ref_inputs(eng: FusedDeepFM, spec: ModelSpec, step: int, keeps):
 
 @pytest.mark.parametrize("K,layers,generic", [(10, [128, 64, 32], False), (10, [128, 64, 32], True),
                                               (32, [256, 128, 64], False), (8, [48, 16], False),
-                                              (10, [64, 32], False)])
+                                              (10, [64, 32], False), (32, [128, 64, 32], False),
+                                              (32, [128, 64, 32], True)])
 def test_fused_step_gradients_match_oracle(K, layers, generic):
     torch.manual_seed(0)
     dev = torch.device("cuda")
@@ -329,3 +330,61 @@ def test_fused_batch_norm_multistep_graph_equals_per_step():
     a.check()
     b.check()
     assert torch.equal(a.dense, b.dense) and torch.equal(a.emb, b.emb) and torch.equal(a.bn_stats, b.bn_stats)
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+@pytest.mark.parametrize("opt", ["Adam", "Adagrad", "Momentum", "ftrl", "GD"])
+def test_fused_optimizers_match_tf_formulas(opt, update):
+    """Every HIP optimizer (MLP dense apply inside the step tail, embedding row update, exact-mode
+    full-table update) against optim/tf_optim.py over two steps.  Each step's gradients come from
+    a GD(lr=1) engine started from the optimizer engine's current variables; the TF formula is
+    then applied to the variables and slots read back from the optimizer engine."""
+    from rocfm.optim import apply_dense, slot_names
+
+    dev = torch.device("cuda")
+    V, F, K, B = 3000, 39, 10, 128
+    spec = ModelSpec(feature_size=V, field_size=F, embedding_size=K, layers=[64, 32], keep_probs=[1.0, 1.0],
+                     l2_reg=1e-3)
+    hp = OptHParams(name=opt, lr=1e-2)
+    eng = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 21), use_graph=False, embedding_update=update)
+    gen = torch.Generator().manual_seed(4)
+    batches = [_batch(B, F, V, gen) for _ in range(2)]
+    names = slot_names(opt)
+    # g is recovered as (θ − θ_GD) / 1024 from a GD(lr = 1024) step: the f32 rounding of θ_GD then
+    # costs ≈ ulp(θ)/1024 of g.  Adam / Adagrad / FTRL normalise by |g|, so elements with tiny |g|
+    # may still move by a slightly different fraction of lr: 0.5 % of one step is allowed
+    # (a wrong formula term is off by ≫ 1 %)
+    glr = 1024.0
+    atol = 5e-3 * hp.lr if opt in ("Adam", "Adagrad", "ftrl") else 2e-6
+    for step, (ids, vals, labels) in enumerate(batches, start=1):
+        sd0 = eng.state_dict()
+        params0 = {k: v for k, v in sd0.items() if "/" not in k or k.startswith("Deep-part/")}
+        params0 = {k: v for k, v in params0.items() if not any(k.endswith("/" + n) for n in names)}
+        params0.pop("global_step", None)
+        params0.pop("beta1_power", None)
+        params0.pop("beta2_power", None)
+        gd = FusedDeepFM(spec, OptHParams(name="GD", lr=glr), B, dev, params=params0, use_graph=False,
+                         embedding_update=update)
+        for e in (gd, eng):
+            e.load_batch(ids.to(dev), vals.to(dev), labels.to(dev))
+            e.train_step()
+        torch.cuda.synchronize()
+        gdp = gd.parameters_tf()
+        got = eng.state_dict()
+        for name, p0 in params0.items():
+            g = (p0 - gdp[name]) / glr  # this step's gradient (incl. the lazy / dense L2 term of the tables)
+            p = p0.clone()
+            slots = [sd0[f"{name}/{n}"].clone() for n in names]
+            if name in ("fm_v", "fm_w") and update == "sparse":
+                rows = torch.unique(ids.long())
+                pr, sr = p[rows], [t[rows] for t in slots]
+                apply_dense(hp, pr, g[rows], sr, step)
+                p[rows] = pr
+                for t, tr in zip(slots, sr):
+                    t[rows] = tr
+            else:
+                apply_dense(hp, p, g, slots, step)
+            torch.testing.assert_close(got[name], p, rtol=2e-4, atol=atol, msg=lambda m: f"{opt} {name}: {m}")
+            for n, t in zip(names, slots):
+                torch.testing.assert_close(got[f"{name}/{n}"], t, rtol=2e-3, atol=max(atol, 1e-6),
+                                           msg=lambda m: f"{opt} {name}/{n}: {m}")

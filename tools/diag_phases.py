@@ -30,10 +30,15 @@ def report(name, st, idx, labels):
 
 def main():
     B = int(os.environ.get("B", "1024"))
+    V = int(os.environ.get("V", "1000000"))
+    K = int(os.environ.get("K", "10"))
+    generic = os.environ.get("GENERIC", "0") == "1"  # runtime-shape row kernel (the only one with stamps
+    #                                                   besides the 39x10 128-64-32 training kernel)
     dev = torch.device("cuda")
-    spec = ModelSpec(1_000_000, 39, 10, [128, 64, 32], [0.5] * 3, l2_reg=1e-4)
-    eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=False)
-    gen = SyntheticCriteo(1_000_000, 39, seed=1)
+    spec = ModelSpec(V, 39, K, [128, 64, 32], [0.5] * 3, l2_reg=1e-4)
+    eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=False,
+                      force_generic_kernels=generic)
+    gen = SyntheticCriteo(V, 39, seed=1)
     g = torch.Generator(device=dev).manual_seed(1)
     pool = [gen.batch(B, dev, g) for _ in range(8)]
     eng.attach_pool(torch.stack([x[0] for x in pool]), torch.stack([x[1] for x in pool]),
