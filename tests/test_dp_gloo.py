@@ -52,7 +52,7 @@ def _worker(rank, world, port, update, opt, out):
     broadcast_tensors(list(eng.P.values()))
     attach_torch_dp(eng, update)
     B = 16
-    for ids, vals, labels in _batches(3, 2 * B, 7):
+    for ids, vals, labels in _batches(3, world * B, 7):
         sl = slice(rank * B, (rank + 1) * B)
         eng.train_step(ids[sl], vals[sl], labels[sl])
     if rank == 0:
@@ -61,10 +61,14 @@ def _worker(rank, world, port, update, opt, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("update,opt", [("sparse", "Adam"), ("exact", "Adam"), ("sparse", "Adagrad")])
-def test_torch_dp_equals_single_process_union_batch(tmp_path, update, opt):
+@pytest.mark.parametrize("world,update,opt", [(2, "sparse", "Adam"), (2, "exact", "Adam"), (2, "sparse", "Adagrad"),
+                                              (4, "sparse", "Adam"), (4, "exact", "Adam"), (8, "sparse", "Adam"),
+                                              (8, "exact", "Adagrad")])
+def test_torch_dp_equals_single_process_union_batch(tmp_path, world, update, opt):
+    """the DP path at 2, 4 and 8 ranks ≡ one process on the union batch."""
     out = str(tmp_path / "p.pt")
-    mp.start_processes(_worker, args=(2, _port(), update, opt, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _port(), update, opt, out), nprocs=world, join=True,
+                       start_method="spawn")
     got = torch.load(out, weights_only=True)
     from rocfm.models.deepfm import init_params
     from rocfm.models.torch_engine import TorchDeepFM
@@ -72,7 +76,7 @@ def test_torch_dp_equals_single_process_union_batch(tmp_path, update, opt):
 
     spec = _spec()
     ref = TorchDeepFM(spec, OptHParams(name=opt, lr=0.01), embedding_update=update, params=init_params(spec, 100))
-    for ids, vals, labels in _batches(3, 32, 7):
+    for ids, vals, labels in _batches(3, 16 * world, 7):
         ref.train_step(ids, vals, labels)
     for k in ref.P:
         torch.testing.assert_close(got[k], ref.P[k], rtol=1e-5, atol=1e-6)

@@ -47,7 +47,7 @@ def _worker(rank, world, port, update, opt, out, ckpt_dir):
     eng = TorchRowShard(spec, OptHParams(name=opt, lr=0.01), embedding_update=update, params=init_params(spec, 100))
     eng.set_lr_scale(float(world))
     B = 16
-    for ids, vals, labels in _batches(3, 2 * B, 7):
+    for ids, vals, labels in _batches(3, world * B, 7):
         sl = slice(rank * B, (rank + 1) * B)
         eng.train_step(ids[sl], vals[sl], labels[sl])
     full = eng.parameters_tf()  # collective gather of the tables
@@ -69,11 +69,16 @@ def _worker(rank, world, port, update, opt, out, ckpt_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("update,opt", [("sparse", "Adam"), ("exact", "Adam"), ("sparse", "Adagrad")])
-def test_rowshard_equals_single_process_union_batch(tmp_path, update, opt):
+@pytest.mark.parametrize("world,update,opt", [(2, "sparse", "Adam"), (2, "exact", "Adam"), (2, "sparse", "Adagrad"),
+                                              (4, "sparse", "Adam"), (4, "exact", "Adam"), (8, "sparse", "Adam"),
+                                              (8, "exact", "Adagrad")])
+def test_rowshard_equals_single_process_union_batch(tmp_path, world, update, opt):
+    """the row-shard (PS-equivalent) path at 2, 4 and 8 ranks ≡ one process on the
+    union batch; the W-shard checkpoint reassembles and restores on one process."""
     out = str(tmp_path / "p.pt")
     cdir = str(tmp_path / "ckpt")
-    mp.start_processes(_worker, args=(2, _port(), update, opt, out, cdir), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _port(), update, opt, out, cdir), nprocs=world, join=True,
+                       start_method="spawn")
     got = torch.load(out, weights_only=True)
     from rocfm import checkpoint as ckpt
     from rocfm.models.deepfm import init_params
@@ -81,9 +86,9 @@ def test_rowshard_equals_single_process_union_batch(tmp_path, update, opt):
     from rocfm.optim import OptHParams
 
     spec = _spec()
-    hp = OptHParams(name=opt, lr=0.02)  # single process: lr × world (linear scaling)
+    hp = OptHParams(name=opt, lr=0.01 * world)  # single process: lr × world (linear scaling)
     ref = TorchDeepFM(spec, hp, embedding_update=update, params=init_params(spec, 100))
-    for ids, vals, labels in _batches(3, 32, 7):
+    for ids, vals, labels in _batches(3, 16 * world, 7):
         ref.train_step(ids, vals, labels)
     for k in ref.P:
         torch.testing.assert_close(got["P"][k], ref.P[k], rtol=1e-5, atol=1e-6)
@@ -100,7 +105,7 @@ def test_rowshard_equals_single_process_union_batch(tmp_path, update, opt):
     # and restores into a 1-rank row-shard engine / a replicated engine
     from rocfm.parallel.emb_shard import TorchRowShard
 
-    one = TorchRowShard(spec, OptHParams(name=opt, lr=0.02), embedding_update=update)
+    one = TorchRowShard(spec, OptHParams(name=opt, lr=0.01 * world), embedding_update=update)
     one.load_state_dict(sd)
     torch.testing.assert_close(one.base.P["fm_v"], ref.P["fm_v"], rtol=1e-5, atol=1e-6)
 
