@@ -7,7 +7,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-REF_DATA = "/root/reference/data/val.tfrecords"
+# the reference's bundled 10k-record validation file (data/val.tfrecords), shipped with the tests
+# so that the GPU box (no /root/reference there) runs the data-driven tests too
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "val.tfrecords")
 
 
 def pytest_configure(config):
@@ -27,5 +29,5 @@ def gpu_available() -> bool:
 @pytest.fixture(scope="session")
 def ref_data_path():
     if not os.path.exists(REF_DATA):
-        pytest.skip("reference data/val.tfrecords not available")
+        pytest.skip("tests/fixtures/val.tfrecords not available")
     return REF_DATA
