@@ -180,9 +180,17 @@ PYBIND11_MODULE(_rocfm_io, m) {
       [](const std::string& in_path, const std::string& out_path, int num_threads) {
         Schema s = make_schema(0, "label", "ids", "values");
         py::gil_scoped_release nogil;
-        return convert_libsvm(in_path, out_path, s, num_threads);
+        return convert_libsvm(in_path, std::vector<std::string>{out_path}, s, num_threads);
       },
       py::arg("in_path"), py::arg("out_path"), py::arg("num_threads") = 4);
+  m.def(
+      "convert_libsvm_sharded",
+      [](const std::string& in_path, const std::vector<std::string>& out_paths, int num_threads) {
+        Schema s = make_schema(0, "label", "ids", "values");
+        py::gil_scoped_release nogil;
+        return convert_libsvm(in_path, out_paths, s, num_threads);
+      },
+      py::arg("in_path"), py::arg("out_paths"), py::arg("num_threads") = 4);
 
   py::class_<BatchLoader>(m, "BatchLoader")
       .def(py::init([](std::vector<std::string> files, int field_size, int64_t max_id, int batch_size,

@@ -535,7 +535,9 @@ bool parse_libsvm_line(const char* p, const char* end, float* label, std::vector
 }
 }  // namespace
 
-size_t convert_libsvm(const std::string& in_path, const std::string& out_path, const Schema& s, int num_threads) {
+size_t convert_libsvm(const std::string& in_path, const std::vector<std::string>& out_paths, const Schema& s,
+                      int num_threads) {
+  if (out_paths.empty()) throw std::invalid_argument("convert_libsvm: no output path");
   auto c = map_file(in_path);
   const char* base = reinterpret_cast<const char*>(c->data);
   size_t n = c->size;
@@ -551,7 +553,7 @@ size_t convert_libsvm(const std::string& in_path, const std::string& out_path, c
   cuts.push_back(n);
   int parts = (int)cuts.size() - 1;
   std::vector<std::string> outs(parts);
-  std::vector<size_t> counts(parts, 0);
+  std::vector<std::vector<size_t>> ends(parts);  // end offset of every framed record in outs[t]
   std::vector<std::string> errs(parts);
   std::vector<std::thread> th;
   for (int t = 0; t < parts; ++t) {
@@ -569,7 +571,7 @@ size_t convert_libsvm(const std::string& in_path, const std::string& out_path, c
           ex.clear();
           encode_example(s, label, ids.data(), vals.data(), (int)ids.size(), &ex);
           frame_record(reinterpret_cast<const uint8_t*>(ex.data()), ex.size(), &outs[t]);
-          ++counts[t];
+          ends[t].push_back(outs[t].size());
         } else {
           const char* q = p;
           while (q < le && (*q == ' ' || *q == '\t' || *q == '\r')) ++q;
@@ -582,17 +584,33 @@ size_t convert_libsvm(const std::string& in_path, const std::string& out_path, c
   for (auto& x : th) x.join();
   for (auto& e : errs)
     if (!e.empty()) throw std::runtime_error(e);
-  FILE* f = fopen(out_path.c_str(), "wb");
-  if (!f) throw std::runtime_error("cannot write " + out_path);
   size_t total = 0;
-  for (int t = 0; t < parts; ++t) {
-    if (fwrite(outs[t].data(), 1, outs[t].size(), f) != outs[t].size()) {
-      fclose(f);
-      throw std::runtime_error("short write to " + out_path);
+  for (int t = 0; t < parts; ++t) total += ends[t].size();
+  // shard k holds the contiguous records [k·N/S, (k+1)·N/S) in input order
+  const size_t S = out_paths.size();
+  int t = 0;
+  size_t r_in_t = 0;  // next record of part t
+  for (size_t k = 0; k < S; ++k) {
+    const size_t hi = total * (k + 1) / S, lo = total * k / S;
+    FILE* f = fopen(out_paths[k].c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + out_paths[k]);
+    size_t left = hi - lo;
+    while (left > 0) {
+      while (r_in_t >= ends[t].size()) {
+        ++t;
+        r_in_t = 0;
+      }
+      const size_t take = std::min(left, ends[t].size() - r_in_t);
+      const size_t b0 = r_in_t ? ends[t][r_in_t - 1] : 0, b1 = ends[t][r_in_t + take - 1];
+      if (fwrite(outs[t].data() + b0, 1, b1 - b0, f) != b1 - b0) {
+        fclose(f);
+        throw std::runtime_error("short write to " + out_paths[k]);
+      }
+      r_in_t += take;
+      left -= take;
     }
-    total += counts[t];
+    fclose(f);
   }
-  fclose(f);
   return total;
 }
 

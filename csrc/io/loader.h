@@ -110,7 +110,10 @@ size_t decode_file(const std::string& path, const Schema& s, int64_t max_id, boo
 // libsvm ("label id:val id:val ...") → TFRecord, multi-threaded, output order = input order.
 // Mirrors tools/libsvm_to_tfrecord.py:22-61 (one Example per line, every pair kept).
 // Returns number of records written.
-size_t convert_libsvm(const std::string& in_path, const std::string& out_path, const Schema& s, int num_threads);
+// libsvm lines "label id:val id:val …" → tf.train.Example records (TOOL:22-61), written to
+// out_paths.size() shards of contiguous records (input order kept).  Returns the record count.
+size_t convert_libsvm(const std::string& in_path, const std::vector<std::string>& out_paths, const Schema& s,
+                      int num_threads);
 
 }  // namespace io
 }  // namespace rocfm

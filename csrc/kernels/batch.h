@@ -23,6 +23,10 @@ struct FetchParams {
   float* lrt_dst;  // nullable: lr_t for the step published in step_dst (Adam bias correction)
   float lr, beta1, beta2;
   int opt_type;
+  // device-side id guard (ROCFM_CHECK_IDS): ids outside [0, max_id) set *bad_ids and are fetched
+  // as row 0, so no kernel indexes outside the table; the host raises at its next check()
+  int32_t* bad_ids;  // nullable (guard off)
+  uint32_t max_id;
 };
 
 void launch_fetch_batch(const FetchParams& p, hipStream_t stream);
@@ -55,6 +59,8 @@ struct FetchMultiParams {
   float* lrt;       // [S] lr_t of each prepared step
   float lr, beta1, beta2;
   int opt_type;
+  int32_t* bad_ids;  // nullable: device-side id guard, as in FetchParams
+  uint32_t max_id;
 };
 
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream);

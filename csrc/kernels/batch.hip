@@ -10,6 +10,16 @@
 
 namespace rocfm {
 
+// ROCFM_CHECK_IDS guard: an id outside [0, max_id) is flagged (sticky, vector atomic) and replaced
+// by row 0 before any kernel can index the table with it
+__device__ __forceinline__ int32_t guard_id(int32_t id, int32_t* bad, uint32_t max_id) {
+  if (bad != nullptr && (uint32_t)id >= max_id) {
+    atomicOr(bad, 1);
+    return 0;
+  }
+  return id;
+}
+
 __global__ __launch_bounds__(256) void fetch_batch_kernel(const FetchParams p) {
   const long long nb = p.pool_batches;
   long long b = (*p.cur_src + p.advance) % nb;
@@ -21,11 +31,18 @@ __global__ __launch_bounds__(256) void fetch_batch_kernel(const FetchParams p) {
   int4* dv = reinterpret_cast<int4*>(p.vals);
   const long long n4 = (n & 3) ? 0 : (n >> 2);  // vector path only when every batch is 16-B aligned
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    di[i] = si[i];
+    int4 v = si[i];
+    if (p.bad_ids != nullptr) {
+      v.x = guard_id(v.x, p.bad_ids, p.max_id);
+      v.y = guard_id(v.y, p.bad_ids, p.max_id);
+      v.z = guard_id(v.z, p.bad_ids, p.max_id);
+      v.w = guard_id(v.w, p.bad_ids, p.max_id);
+    }
+    di[i] = v;
     dv[i] = sv[i];
   }
   for (long long i = (n4 << 2) + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    p.ids[i] = p.ids_pool[b * n + i];
+    p.ids[i] = guard_id(p.ids_pool[b * n + i], p.bad_ids, p.max_id);
     p.vals[i] = p.vals_pool[b * n + i];
   }
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.B; i += (long long)gridDim.x * 256)
@@ -63,7 +80,7 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
   uint32_t* dk = p.keys ? p.keys + (long long)k * n : nullptr;
   const uint32_t kb = (uint32_t)k << p.id_bits;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const int32_t id = si[i];
+    const int32_t id = guard_id(si[i], p.bad_ids, p.max_id);
     di[i] = id;
     dv[i] = sv[i];
     if (dk) {

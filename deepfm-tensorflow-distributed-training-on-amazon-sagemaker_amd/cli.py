@@ -42,11 +42,27 @@ def run(cfg: Config) -> dict:
         dist.barrier()
     if info.is_chief:  # PS:398-414: print every flag
         logging.getLogger("rocfm").info("flags %s", json.dumps(cfg.to_dict(), default=str))
+    est = Estimator(cfg)
+    out: dict = {"task_type": cfg.task_type}
+    if cfg.pipe_mode and cfg.task_type == "train":
+        # SageMaker Pipe mode: one FIFO per channel and epoch, channels bound by SM_CHANNELS or the
+        # channel-name flags; one training pass over the epochs' streams, then evaluation on the
+        # evaluation channel (HVD:443-456; PS:505-521)
+        from .data.sharding import pipe_mode_sources
+
+        tr_fifos, va_fifos = pipe_mode_sources(cfg.num_epochs, info.local_rank, cfg.training_channel_name,
+                                               cfg.evaluation_channel_name)
+        out["channels"] = {"train": tr_fifos, "eval": va_fifos}
+        out["train"] = est.train(tr_fifos, 1, max_steps=cfg.max_steps or None)
+        if va_fifos:
+            out["eval"] = est.evaluate(va_fifos)
+        if cfg.servable_model_dir:
+            out["export"] = est.export(cfg.servable_model_dir)
+        est.close()
+        return out
     tr_files = discover_files(cfg.training_data_dir, "tr", shuffle=True, seed=cfg.seed)
     va_files = discover_files(cfg.val_data_dir, "va")
     te_files = discover_files(cfg.val_data_dir, "te")
-    est = Estimator(cfg)
-    out: dict = {"task_type": cfg.task_type}
     if cfg.task_type == "train":
         if not tr_files:
             raise FileNotFoundError(f"no tr*.tfrecords under {cfg.training_data_dir!r}")

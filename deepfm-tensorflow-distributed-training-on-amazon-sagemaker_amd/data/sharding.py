@@ -20,7 +20,9 @@ reference evaluates only rank 0's 1/N shard).
 """
 from __future__ import annotations
 
-from typing import Tuple
+import json
+import os
+from typing import List, Optional, Tuple
 
 from ..parallel.dist import RankInfo
 
@@ -57,3 +59,34 @@ def pipe_channel(channels, local_rank: int, training: bool = True) -> str:
     if not training:
         return channels[0]
     return channels[min(1 + local_rank, len(channels) - 1)]
+
+
+def sm_channels() -> List[str]:
+    """SageMaker's channel list (env SM_CHANNELS, a JSON list; PS:391, HVD:420)."""
+    raw = os.environ.get("SM_CHANNELS", "")
+    if not raw:
+        return []
+    ch = json.loads(raw)
+    if not isinstance(ch, list):
+        raise ValueError(f"SM_CHANNELS must be a JSON list, got {raw!r}")
+    return [str(c) for c in ch]
+
+
+def pipe_mode_sources(num_epochs: int, local_rank: int, training_channel_name: str = "",
+                      evaluation_channel_name: str = "", input_dir: Optional[str] = None):
+    """Pipe-mode input (``pipe_mode=1``): the FIFOs SageMaker creates per channel and epoch,
+    ``<SM_INPUT_DIR>/data/<channel>_<epoch>`` (what PipeModeDataset opens, PS:150 / HVD:136).
+
+    Channel binding: the explicit ``training_channel_name`` / ``evaluation_channel_name`` flags
+    (the PS script, PS:505-513), else SM_CHANNELS with the Horovod script's rule — evaluation =
+    channels[0], training = channels[1 + local_rank] (HVD:420-445; SageMaker lists ``evaluation``
+    first, README:81).  Returns (train FIFOs for every epoch in order, [eval FIFO])."""
+    channels = sm_channels()
+    tr = training_channel_name or (pipe_channel(channels, local_rank) if channels else "")
+    ev = evaluation_channel_name or (pipe_channel(channels, local_rank, training=False) if len(channels) > 1 else "")
+    if not tr:
+        raise ValueError("pipe_mode=1 needs SM_CHANNELS or --training_channel_name")
+    base = os.path.join(input_dir or os.environ.get("SM_INPUT_DIR", "/opt/ml/input"), "data")
+    train = [os.path.join(base, f"{tr}_{e}") for e in range(max(1, int(num_epochs)))]
+    evals = [os.path.join(base, f"{ev}_0")] if ev else []
+    return train, evals

@@ -211,6 +211,14 @@ class FusedDeepFM:
         self.pred_labels = torch.zeros(Bp, dtype=torch.float32, device=dev)
         self.pred_prob = torch.zeros(Bp, dtype=torch.float32, device=dev)
         self.pred_loss = torch.zeros(Bp, dtype=torch.float32, device=dev)
+        # ROCFM_CHECK_IDS=1: device-side id guard in the batch fetch (out-of-range ids flag a sticky
+        # error and are replaced by row 0, so no kernel indexes outside the table); check() raises.
+        # id_limit is the GLOBAL vocabulary (the row-shard engine's local table is smaller).
+        from ..utils.numerics import ids_check_enabled
+
+        self.id_guard = ids_check_enabled()
+        self.id_limit = self.V
+        self.bad_ids = torch.zeros(1, dtype=torch.int32, device=dev)
         # default batch source: a 2-slot ring fed by push_batch()
         self._ring = True
         self._set_pool(torch.zeros(2, B, F, dtype=torch.int32, device=dev),
@@ -402,7 +410,12 @@ class FusedDeepFM:
             f.lrt_dst = self.lrt[1 - p:].data_ptr()
             f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
             f.opt_type = OPT_ID[self.hp.name]
+            self._guard(f)
             self.fetch_params.append(f)
+
+    def _guard(self, f) -> None:
+        if self.id_guard:
+            f.bad_ids, f.max_id = self.bad_ids.data_ptr(), int(self.id_limit)
 
     def _set_pool(self, ids, vals, labels):
         if ids.dim() != 3 or ids.shape[1:] != (self.B, self.F) or vals.shape != ids.shape or \
@@ -514,6 +527,7 @@ class FusedDeepFM:
         f.step_src, f.step_dst, f.step_advance = self.steps[p:].data_ptr(), 0, 0
         f.ids, f.vals, f.labels = (self.slot_ids[p].data_ptr(), self.slot_vals[p].data_ptr(),
                                    self.slot_labels[p].data_ptr())
+        self._guard(f)
         self.H.fetch_batch(f, self.stream_ptr)
         self._sort(p, torch.cuda.current_stream(self.device))
         self._primed = True
@@ -679,6 +693,7 @@ class FusedDeepFM:
         f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
         f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
         f.opt_type = OPT_ID[self.hp.name]
+        self._guard(f)
         return f
 
     def _prepare_multi(self, q: int, advance: int, stream) -> None:
@@ -1092,6 +1107,9 @@ class FusedDeepFM:
         then invalid; a sticky device flag, read with one small copy)."""
         if self.bn and int(self.bn_error[0].item()) != 0:
             raise RuntimeError("deepfm_rows: a batch_norm grid barrier timed out (not every workgroup was resident)")
+        if self.id_guard and int(self.bad_ids.item()) != 0:
+            raise ValueError(f"ROCFM_CHECK_IDS: a batch held feature ids outside [0, {self.id_limit}) "
+                             "(they were trained as row 0)")
 
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
         tf = self._tf_views(self.emb, self.dense)

@@ -401,6 +401,8 @@ class FusedRowShard:
                                    params=P, use_graph=False, fuse_dense_opt=False,
                                    dropout_seed=seed + 7919 * r, compute_dtype=compute_dtype)
         del P
+        e.id_limit = self.V  # the id guard (ROCFM_CHECK_IDS) checks global ids, not local rows
+        e._build_fetch()
         self.H, self.device, self.embedding_update = e.H, e.device, embedding_update
         self.use_graph, self.check_every = use_graph, int(check_every)
         from .dp import collectives_capturable

@@ -100,3 +100,40 @@ def test_cli_train_infer(data_dir, tmp_path):
     res = run(_cfg(data_dir, md, task_type="infer"))
     assert os.path.exists(os.path.join(data_dir, "pred.txt")) and res["infer"]["n"] == 512
     os.remove(os.path.join(data_dir, "pred.txt"))
+
+
+def test_sagemaker_pipe_mode_channels(data_dir, tmp_path, monkeypatch):
+    """pipe_mode=1: channels bound from SM_CHANNELS (evaluation = channels[0], training =
+    channels[1 + local_rank], HVD:420-445), one FIFO per channel and epoch under
+    SM_INPUT_DIR/data/<channel>_<epoch> (PipeModeDataset), streamed by writer threads."""
+    import threading
+
+    from rocfm.cli import run
+
+    base = tmp_path / "input"
+    (base / "data").mkdir(parents=True)
+    monkeypatch.setenv("SM_INPUT_DIR", str(base))
+    monkeypatch.setenv("SM_CHANNELS", json.dumps(["evaluation", "training", "training-1"]))
+    src = {"training": os.path.join(data_dir, "tr.tfrecords"), "evaluation": os.path.join(data_dir, "va.tfrecords")}
+    fifos = [("training", 0), ("training", 1), ("evaluation", 0)]
+    writers = []
+    for ch, ep in fifos:
+        path = str(base / "data" / f"{ch}_{ep}")
+        os.mkfifo(path)
+
+        def feed(path=path, ch=ch):
+            with open(path, "wb") as w, open(src[ch], "rb") as r:  # open blocks until the reader opens
+                w.write(r.read())
+
+        t = threading.Thread(target=feed, daemon=True)
+        t.start()
+        writers.append(t)
+    cfg = _cfg(data_dir, str(tmp_path / "m"), pipe_mode=1, num_epochs=2)
+    out = run(cfg)
+    for t in writers:
+        t.join(timeout=30)
+        assert not t.is_alive()
+    assert out["channels"]["train"] == [str(base / "data" / "training_0"), str(base / "data" / "training_1")]
+    assert out["channels"]["eval"] == [str(base / "data" / "evaluation_0")]
+    assert out["train"]["steps"] == 2 * (6000 // 256)
+    assert out["eval"]["examples"] == (1500 // 256) * 256

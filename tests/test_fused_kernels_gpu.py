@@ -388,3 +388,28 @@ def test_fused_optimizers_match_tf_formulas(opt, update):
             for n, t in zip(names, slots):
                 torch.testing.assert_close(got[f"{name}/{n}"], t, rtol=2e-3, atol=max(atol, 1e-6),
                                            msg=lambda m: f"{opt} {name}/{n}: {m}")
+
+
+def test_device_id_guard(monkeypatch):
+    """ROCFM_CHECK_IDS=1: out-of-range ids are caught on the device (sticky flag; fetched as row 0
+    so no kernel reads outside the table) and check() raises; in-range batches pass."""
+    monkeypatch.setenv("ROCFM_CHECK_IDS", "1")
+    dev = torch.device("cuda")
+    V, F, K, B = 1000, 39, 10, 128
+    spec = ModelSpec(feature_size=V, field_size=F, embedding_size=K, layers=[64, 32], keep_probs=[1.0, 1.0])
+    gen = torch.Generator().manual_seed(2)
+    good = [_batch(B, F, V, gen) for _ in range(4)]
+    bad = [tuple(t.clone() for t in b) for b in good]
+    bad[2][0][5, 7] = V + 12345
+    bad[3][0][9, 3] = -4
+    for batches, should_fail in ((good, False), (bad, True)):
+        eng = FusedDeepFM(spec, OptHParams(name="Adam", lr=1e-3), B, dev, params=init_params(spec, 1))
+        eng.attach_pool(*[torch.stack([b[i] for b in batches]).to(dev) for i in range(3)])
+        eng.train_steps(8, 4)
+        torch.cuda.synchronize()
+        if should_fail:
+            with pytest.raises(ValueError, match="ROCFM_CHECK_IDS"):
+                eng.check()
+        else:
+            eng.check()
+        assert torch.isfinite(eng.emb).all()

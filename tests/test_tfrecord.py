@@ -221,3 +221,35 @@ def test_groups_match_batches_skip_limit_tail(tmp_path):
     got = list(ds.groups(8))
     assert got[-1][0].shape == (1000 - 62 * 16, 5)
     assert sum(g[0].shape[0] for g in got[:-1]) == 62
+
+
+def test_libsvm_cli_sharded(tmp_path):
+    """python -m rocfm.tools.libsvm_to_tfrecord with --shards: contiguous shards, input order kept,
+    every record decodes to the libsvm line it came from (TOOL:22-61 schema)."""
+    import subprocess
+    import sys
+
+    lines = []
+    for i in range(103):
+        feats = " ".join(f"{i * 7 + f}:{(f + 1) * 0.5:g}" for f in range(5))
+        lines.append(f"{i % 2} {feats}")
+    src = tmp_path / "train.libsvm"
+    src.write_text("\n".join(lines) + "\n")
+    out = tmp_path / "o" / "tr.tfrecords"
+    r = subprocess.run([sys.executable, "-m", "rocfm.tools.libsvm_to_tfrecord", str(src), str(out), "--shards", "4",
+                        "--threads", "3"], capture_output=True, text=True, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert r.returncode == 0, r.stderr
+    from rocfm.tools.libsvm_to_tfrecord import shard_paths
+
+    paths = shard_paths(str(out), 4)
+    assert [os.path.basename(p) for p in paths] == [f"tr-0000{k}-of-00004.tfrecords" for k in range(4)]
+    got = []
+    for p in paths:
+        L, I, V = T.decode_file(p, 5)
+        got += [(float(l), i.tolist(), v.tolist()) for l, i, v in zip(L, I, V)]
+    assert len(got) == 103
+    for i, (l, ids, vals) in enumerate(got):
+        assert l == float(i % 2) and ids == [i * 7 + f for f in range(5)]
+        assert vals == [(f + 1) * 0.5 for f in range(5)]
+    sizes = [len(T.decode_file(p, 5)[0]) for p in paths]
+    assert sizes == [25, 26, 26, 26]
