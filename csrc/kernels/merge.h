@@ -1,4 +1,5 @@
-// Multi-source row-gradient merge by direct addressing (merge.hip).
+// Multi-source row-gradient merge (merge.hip): direct addressing, or an open-addressing hash for
+// vocabularies whose W × V position maps would not fit a memory budget.
 //
 // W source lists (one per rank) each hold UNIQUE keys with one gradient row per key — the DP
 // all-gather of every rank's (id, Σ grad) export, or an owner's per-source requests in row-shard
@@ -8,6 +9,14 @@
 //   merge_apply   : the representative entry (r == rep[key]) sums the rows of key over r..W−1 in
 //                   rank order (deterministic, no float atomics), applies lazy L2 + the row
 //                   optimizer (or writes a dense gradient row), and restores pos/rep.
+// Hash mode (hash_slots > 0; O(W·cap) memory whatever the vocabulary — the 1B-row tables): a
+// linear-probing table of hash_slots ≥ 2·W·cap slots replaces the maps.  Every word carries the
+// step's tag T = global_step + 1 in its high half, so slots of earlier steps read as empty and
+// nothing is ever cleared (clearing while other threads still probe through a slot would break
+// their chains):
+//   hkeys[slot] = T<<32 | row                      (claimed by 64-bit CAS)
+//   hrep[slot]  = T<<32 | (0xFFFFFFFF − r)         (atomicMax → the lowest rank holding row)
+//   hpos[slot·W + r] = T<<32 | j
 #pragma once
 #include "../common.h"
 #include "optim.h"
@@ -40,6 +49,11 @@ struct MergeParams {
   float* dense_grad;  // mode 1
   int32_t* overflow;  // nullable: sticky flag, set when a source's count exceeds cap
   uint32_t* touched;  // mode 1 (nullable): touched[row] = step + 1 (EmbDenseParams::touched)
+  // hash mode (hash_slots > 0, a power of two ≥ 2·W·cap; pos/rep/Vmap maps unused)
+  int hash_slots;
+  unsigned long long* hkeys;  // [hash_slots], zero-initialised once
+  unsigned long long* hrep;   // [hash_slots]
+  unsigned long long* hpos;   // [hash_slots][W]
 };
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);

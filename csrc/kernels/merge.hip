@@ -20,6 +20,49 @@ __device__ __forceinline__ bool entry_valid(const MergeParams& p, int r, int j, 
   return key / p.key_div < p.Vmap;
 }
 
+// ---- hash mode ------------------------------------------------------------------------------
+typedef unsigned long long u64;
+__device__ __forceinline__ uint32_t hash_row(uint32_t x) {  // murmur3 finaliser
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t merge_tag(const MergeParams& p) { return (uint32_t)*p.step + 1u; }
+
+// Insert (or find) row in this step's table; returns its slot (the table has ≥ 2× the entries)
+__device__ __forceinline__ int hash_claim(const MergeParams& p, uint32_t row, uint32_t T) {
+  const uint32_t mask = (uint32_t)p.hash_slots - 1u;
+  const u64 mine = ((u64)T << 32) | row;
+  uint32_t slot = hash_row(row) & mask;
+  for (int probe = 0; probe < p.hash_slots; ++probe) {
+    u64 cur = __hip_atomic_load(p.hkeys + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((uint32_t)(cur >> 32) != T) {  // stale (earlier step) or never used: claim it
+      const u64 prev = atomicCAS(p.hkeys + slot, cur, mine);
+      if (prev == cur) return (int)slot;
+      cur = prev;
+    }
+    if ((uint32_t)cur == row) return (int)slot;
+    slot = (slot + 1u) & mask;
+  }
+  return -1;  // unreachable with hash_slots ≥ 2·W·cap
+}
+
+__device__ __forceinline__ int hash_find(const MergeParams& p, uint32_t row, uint32_t T) {
+  const uint32_t mask = (uint32_t)p.hash_slots - 1u;
+  const u64 mine = ((u64)T << 32) | row;
+  uint32_t slot = hash_row(row) & mask;
+  for (int probe = 0; probe < p.hash_slots; ++probe) {
+    const u64 cur = p.hkeys[slot];
+    if (cur == mine) return (int)slot;
+    if ((uint32_t)(cur >> 32) != T) return -1;  // an empty slot ends the chain
+    slot = (slot + 1u) & mask;
+  }
+  return -1;
+}
+
 __global__ __launch_bounds__(kMergeThreads) void merge_init_kernel(MergeParams p) {
   const long long i = (long long)blockIdx.x * kMergeThreads + threadIdx.x;
   const long long n = (long long)p.W * p.Vmap;
@@ -35,6 +78,17 @@ __device__ __forceinline__ void merge_scatter_body(const MergeParams& p, const i
   const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
   if (!entry_valid(p, r, j, key)) return;
   const uint32_t row = key / p.key_div;
+  if (p.hash_slots > 0) {
+    const uint32_t T = merge_tag(p);
+    const int slot = hash_claim(p, row, T);
+    if (slot < 0) {
+      if (p.overflow) *p.overflow = 1;
+      return;
+    }
+    p.hpos[(size_t)slot * p.W + r] = ((u64)T << 32) | (uint32_t)j;
+    atomicMax(p.hrep + slot, ((u64)T << 32) | (0xFFFFFFFFu - (uint32_t)r));
+    return;
+  }
   p.pos[(size_t)r * p.Vmap + row] = j;
   atomicMin(&p.rep[row], r);
 }
@@ -53,7 +107,25 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
   const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
   if (!entry_valid(p, r, j, key)) return;
   const uint32_t row = key / p.key_div;
-  if (p.rep[row] != r) return;
+  const bool hashed = p.hash_slots > 0;
+  const uint32_t T = hashed ? merge_tag(p) : 0u;
+  int slot = -1;
+  if (hashed) {
+    slot = hash_find(p, row, T);
+    if (slot < 0) return;
+    const u64 rv = p.hrep[slot];
+    if ((uint32_t)(rv >> 32) != T || 0xFFFFFFFFu - (uint32_t)rv != (uint32_t)r) return;
+  } else if (p.rep[row] != r) {
+    return;
+  }
+  // position of `row` in source q's list this step, or −1
+  auto pos_of = [&](int q) -> int {
+    if (hashed) {
+      const u64 v = p.hpos[(size_t)slot * p.W + q];
+      return (uint32_t)(v >> 32) == T ? (int)(uint32_t)v : -1;
+    }
+    return p.pos[(size_t)q * p.Vmap + row];
+  };
   const int W = p.W;
   const size_t base = (size_t)row * KP4;
   // the table row and its optimizer slots depend only on the row: issued now, in the same round
@@ -84,7 +156,7 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
     int pj[WMAX];
 #pragma unroll
     for (int q = 0; q < WMAX; ++q)
-      pj[q] = (q < W && q > r) ? p.pos[(size_t)q * p.Vmap + row] : (q == r ? j : -1);
+      pj[q] = (q < W && q > r) ? pos_of(q) : (q == r ? j : -1);
     float4 v[WMAX][KP4];
 #pragma unroll
     for (int q = 0; q < WMAX; ++q) {
@@ -108,7 +180,7 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
     }
   } else {
     for (int q = r; q < W; ++q) {  // rank order: deterministic sum
-      const int pq = q == r ? j : p.pos[(size_t)q * p.Vmap + row];
+      const int pq = q == r ? j : pos_of(q);
       if (pq < 0) continue;
       const float4* src = reinterpret_cast<const float4*>(p.rows + (size_t)q * p.row_stride + (size_t)pq * p.Kp);
 #pragma unroll
@@ -121,9 +193,12 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
       }
     }
   }
-  // restore the maps for the next step (no other thread reads them for this key any more)
-  for (int q = r; q < W; ++q) p.pos[(size_t)q * p.Vmap + row] = -1;
-  p.rep[row] = W;
+  // restore the maps for the next step (no other thread reads them for this key any more); the
+  // hash table needs no restore (its words are tagged with the step)
+  if (!hashed) {
+    for (int q = r; q < W; ++q) p.pos[(size_t)q * p.Vmap + row] = -1;
+    p.rep[row] = W;
+  }
 
   if (p.mode == 1) {
     float4* dg = reinterpret_cast<float4*>(p.dense_grad) + base;
@@ -183,14 +258,22 @@ void launch_apply_t(const MergeParams& p, hipStream_t stream) {
 void check(const MergeParams& p) {
   ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge: 1 <= W <= 64");
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
-  ROCFM_REQUIRE(p.key_div >= 1 && p.pos && p.rep, "merge: maps/key_div");
   ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
+  ROCFM_REQUIRE(p.key_div >= 1, "merge: key_div");
+  if (p.hash_slots > 0) {
+    ROCFM_REQUIRE((p.hash_slots & (p.hash_slots - 1)) == 0 && (long long)p.hash_slots >= 2ll * p.W * p.cap,
+                  "merge: hash_slots must be a power of two >= 2*W*cap");
+    ROCFM_REQUIRE(p.hkeys && p.hrep && p.hpos && p.step, "merge: hash buffers / step missing");
+  } else {
+    ROCFM_REQUIRE(p.pos && p.rep, "merge: maps missing");
+  }
 }
 
 }  // namespace
 
 void launch_merge_init(const MergeParams& p, hipStream_t stream) {
   check(p);
+  if (p.hash_slots > 0) return;  // the tagged hash table starts zeroed and is never reset
   const long long n = (long long)p.W * p.Vmap;
   hipLaunchKernelGGL(merge_init_kernel, dim3((unsigned)((n + kMergeThreads - 1) / kMergeThreads)),
                      dim3(kMergeThreads), 0, stream, p);

@@ -77,6 +77,51 @@ def _all_reduce(t: torch.Tensor) -> None:
     t.copy_(c)
 
 
+MERGE_MAP_BUDGET = 512 << 20  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
+
+
+class MergeMaps:
+    """Row-merge lookup structures of merge.hip for W sources of ≤ cap unique keys over a table of
+    ``rows`` rows.  Direct addressing ((W + 1) × rows int32 maps, the fastest: one load per source)
+    while it fits MERGE_MAP_BUDGET, else a step-tagged linear-probing hash table of
+    next_pow2(2·W·cap) slots — O(W·cap), independent of the vocabulary (1B-row tables).
+    ``ROCFM_MERGE=direct|hash`` forces one (tests)."""
+
+    def __init__(self, W: int, cap: int, rows: int, device):
+        choice = os.environ.get("ROCFM_MERGE", "auto")
+        if choice not in ("auto", "direct", "hash"):
+            raise ValueError(f"ROCFM_MERGE must be auto, direct or hash, got {choice!r}")
+        direct_bytes = (W + 1) * rows * 4
+        self.hashed = choice == "hash" or (choice == "auto" and direct_bytes > MERGE_MAP_BUDGET)
+        i32 = dict(dtype=torch.int32, device=device)
+        if self.hashed:
+            self.slots = 1 << max(4, math.ceil(math.log2(max(2 * W * cap, 2))))
+            self.hkeys = torch.zeros(self.slots, dtype=torch.int64, device=device)
+            self.hrep = torch.zeros(self.slots, dtype=torch.int64, device=device)
+            self.hpos = torch.zeros(self.slots * W, dtype=torch.int64, device=device)
+            self.pos = self.rep = torch.zeros(1, **i32)  # unused
+        else:
+            self.slots = 0
+            self.pos = torch.empty(W * rows, **i32)
+            self.rep = torch.empty(rows, **i32)
+
+    def bind(self, mp) -> None:
+        mp.pos, mp.rep = self.pos.data_ptr(), self.rep.data_ptr()
+        mp.hash_slots = self.slots
+        if self.hashed:
+            mp.hkeys, mp.hrep, mp.hpos = self.hkeys.data_ptr(), self.hrep.data_ptr(), self.hpos.data_ptr()
+
+    def reset(self) -> None:
+        """Forget every tag (the step counter went backwards: a checkpoint restore)."""
+        if self.hashed:
+            for t in (self.hkeys, self.hrep, self.hpos):
+                t.zero_()
+
+    def nbytes(self) -> int:
+        ts = (self.hkeys, self.hrep, self.hpos) if self.hashed else (self.pos, self.rep)
+        return sum(t.numel() * t.element_size() for t in ts)
+
+
 def pool_exchange_capacity(pool_ids: torch.Tensor, owners: int = 1) -> int:
     """Exact exchange capacity for training on a known batch pool ([NB, B, F] ids): the largest
     number of unique ids in any batch (``owners`` > 1: per owner ``id % owners``, the row-shard
@@ -217,8 +262,8 @@ class FusedDataParallel:
             e.dense_grads_flat = self.send[:P]
             self.send_count = self.send[self.off_cnt:self.off_cnt + 4].view(torch.int32)
             # merge maps (merge.hip): position of each key in every rank's list, representative rank
-            self.pos = torch.empty(self.world * e.V, dtype=torch.int32, device=e.device)
-            self.rep = torch.empty(e.V, dtype=torch.int32, device=e.device)
+            # (direct addressing, or a W·cap hash table for very large vocabularies)
+            self.maps = MergeMaps(self.world, cap, e.V, e.device)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=e.device)
             e._build_params()
             self.export_params, self.merge_params = [], []
@@ -241,7 +286,7 @@ class FusedDataParallel:
                 mp_.key_stride = mp_.row_stride = mp_.count_stride = self.S
                 mp_.W, mp_.cap, mp_.Kp, mp_.K1 = self.world, cap, Kp, e.K1
                 mp_.key_div, mp_.Vmap = 1, e.V
-                mp_.pos, mp_.rep = self.pos.data_ptr(), self.rep.data_ptr()
+                self.maps.bind(mp_)
                 mp_.emb = e.emb.data_ptr()
                 mp_.s0, mp_.s1 = e._slot_ptrs(e.emb_slots)
                 mp_.l2, mp_.grad_scale = float(spec.l2_reg), 1.0 / self.world
@@ -400,7 +445,7 @@ class FusedDataParallel:
                 src = self.merge_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "overflow", "dense_grad", "touched"):
+                          "overflow", "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 rows.zero_word = self.send[self.off_cnt:].data_ptr()
@@ -485,6 +530,12 @@ class FusedDataParallel:
         if self.mode != "dp":
             return False
         return bool(int(self.overflow.item()))
+
+    def load_state_dict(self, sd, strict: bool = True) -> None:
+        self.eng.load_state_dict(sd, strict=strict)
+        if self.mode == "dp":
+            self.maps.reset()  # the hash merge tags words with the step, which just moved
+        self._graphs = {}
 
     # ---- delegation ----------------------------------------------------------------------------
     def __getattr__(self, name):

@@ -466,8 +466,10 @@ class FusedRowShard:
             self.grad_back = torch.zeros(M, Kp, **f32)
         self._p2p_params = {}
         # owner merge maps (merge.hip): position of each local row in every source's request list
-        self.pos = torch.empty(W * Vs, **i32)
-        self.rep = torch.empty(Vs, **i32)
+        # (direct addressing over the local rows, or a W·cap hash table for very large shards)
+        from .dp import MergeMaps
+
+        self.maps = MergeMaps(W, cap, Vs, dev)
         # prediction routing (own buffers: never races the pipelined training route)
         self.pred_rsv = torch.zeros(n, **i32)
         self.pred_send = torch.full((M,), PAD, **i32)
@@ -520,7 +522,7 @@ class FusedRowShard:
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
             op.key_div, op.Vmap = self.W, self.Vs
-            op.pos, op.rep = self.pos.data_ptr(), self.rep.data_ptr()
+            self.maps.bind(op)
             op.emb = e.emb.data_ptr()
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
@@ -789,7 +791,7 @@ class FusedRowShard:
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "dense_grad", "touched"):
+                          "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 if ed is not None:
@@ -938,6 +940,7 @@ class FusedRowShard:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
+        self.maps.reset()  # the hash merge tags words with the step, which just moved
         self._graphs = {}
         self._warm = 0
 

@@ -110,14 +110,24 @@ def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update):
     torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=atol)
 
 
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_dp_world4_hash_merge(tmp_path, monkeypatch, update):
+    """The O(W·cap) step-tagged hash merge (ROCFM_MERGE=hash; what 1B-row vocabularies use) through
+    4 ranks, multi-step graphs and the p2p push ≡ the single-GPU union batch."""
+    monkeypatch.setenv("ROCFM_MERGE", "hash")
+    _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
+
+
+@pytest.mark.parametrize("merge", ["direct", "hash"])
 @pytest.mark.parametrize("mode,upd", [("dp", "sparse"), ("dense_dp", "exact"), ("dp", "exact")])
-def test_dp_multistep_graphs_world1_equal_single(mode, upd):
+def test_dp_multistep_graphs_world1_equal_single(mode, upd, merge, monkeypatch):
     """Single-process DP (no process group: the exchange is a copy) through the multi-step graph
     pipeline (export → exchange → merge / dense apply inside the graph) ≡ the single-GPU engine."""
     from rocfm.models.deepfm import init_params
     from rocfm.models.fused import FusedDeepFM
     from rocfm.parallel.dp import FusedDataParallel
 
+    monkeypatch.setenv("ROCFM_MERGE", merge)
     spec, hp = _cfg()
     batches = _batches(128, 5, 11)
     pool = [torch.stack([b[i] for b in batches]).cuda() for i in range(3)]
@@ -135,3 +145,5 @@ def test_dp_multistep_graphs_world1_equal_single(mode, upd):
     torch.testing.assert_close(dp.emb, one.emb, rtol=2e-3, atol=2e-5)
     torch.testing.assert_close(dp.dense, one.dense, rtol=2e-3, atol=2e-5)
     dp.check()
+    if mode == "dp":
+        assert dp.maps.hashed == (merge == "hash")

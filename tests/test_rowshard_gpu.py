@@ -191,10 +191,13 @@ def test_fused_rowshard_2ranks_equals_single_gpu_union_batch(tmp_path, update, e
     torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("merge", ["direct", "hash"])
 @pytest.mark.parametrize("update", ["sparse", "exact"])
-def test_fused_rowshard_4ranks_p2p_graphs(tmp_path, update):
+def test_fused_rowshard_4ranks_p2p_graphs(tmp_path, update, merge, monkeypatch):
     """4 ranks on one GPU: every table is split 4 ways and each all-to-all pushes to 3 peers (the
-    W>2 routing the 8-GPU node runs), through multi-step graphs."""
+    W>2 routing the 8-GPU node runs), through multi-step graphs; the owner merge by direct maps and
+    by the O(W·cap) hash table (ROCFM_MERGE=hash)."""
+    monkeypatch.setenv("ROCFM_MERGE", merge)
     out = str(tmp_path / "rs4.pt")
     steps = 10
     mp.start_processes(_worker, args=(4, _free_port(), update, out, "p2p", steps, 4), nprocs=4, join=True,
