@@ -51,8 +51,10 @@ struct FetchMultiParams {
   int32_t* ids;     // [S][Bp][F]
   float* vals;      // [S][Bp][F]
   float* labels;    // [S][Bp]
-  uint32_t* keys;   // [S][B*F] composite sort keys (nullable)
+  uint32_t* keys;   // [S][B*F] composite sort keys (nullable): step k's keys are k << id_bits | id
   int id_bits;
+  unsigned long long* keys64;  // [S][B*F] (nullable; instead of keys): k << id_bits | id as 64-bit
+                               // keys — vocabularies too wide for S << id_bits to fit 32 bits
   int shard_W;      // > 0: keys are owner-major row-shard keys (id % W)·Vs + id / W (shard.hip)
   uint32_t shard_Vs;
   int64_t* steps;   // [S] global_step of each prepared step
@@ -74,6 +76,11 @@ struct SortAuxParams {
   int n, S, chunk;
   int32_t* pos;           // [S·n] pos[batch · n + lookup] = sorted position within the batch
   int32_t* chunk_end;     // [S][ceil(n / chunk)] (nullable)
+  // 64-bit key sorts: skeys64 are the sorted keys; their ids (low id_bits) are written to
+  // skeys_out as plain 32-bit per-batch keys for the consumers (skeys is then unused)
+  const unsigned long long* skeys64;
+  uint32_t* skeys_out;
+  int id_bits;
 };
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream);
 

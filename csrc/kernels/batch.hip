@@ -78,14 +78,20 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
   int32_t* di = p.ids + (long long)k * p.Bp * p.F;
   float* dv = p.vals + (long long)k * p.Bp * p.F;
   uint32_t* dk = p.keys ? p.keys + (long long)k * n : nullptr;
-  const uint32_t kb = (uint32_t)k << p.id_bits;
+  const uint32_t kb = p.keys64 ? 0u : (uint32_t)k << p.id_bits;
+  unsigned long long* dk64 = p.keys64 ? p.keys64 + (long long)k * n : nullptr;
+  const unsigned long long kb64 = (unsigned long long)k << p.id_bits;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const int32_t id = guard_id(si[i], p.bad_ids, p.max_id);
     di[i] = id;
     dv[i] = sv[i];
-    if (dk) {
+    if (dk || dk64) {
       const uint32_t u = (uint32_t)id;
-      dk[i] = kb | (p.shard_W > 0 ? (u % (uint32_t)p.shard_W) * p.shard_Vs + u / (uint32_t)p.shard_W : u);
+      const uint32_t key = p.shard_W > 0 ? (u % (uint32_t)p.shard_W) * p.shard_Vs + u / (uint32_t)p.shard_W : u;
+      if (dk64)
+        dk64[i] = kb64 | key;
+      else
+        dk[i] = kb | key;
     }
   }
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.B; i += (long long)gridDim.x * 256)
@@ -107,18 +113,28 @@ __global__ __launch_bounds__(256) void sort_aux_kernel(const SortAuxParams p) {
   if (i < total) {
     const int k = (int)(i / p.n);
     p.pos[p.svals[i]] = (int32_t)(i - (long long)k * p.n);
+    if (p.skeys64) p.skeys_out[i] = (uint32_t)(p.skeys64[i] & ((1ull << p.id_bits) - 1ull));
   }
   if (p.chunk_end) {
     const int nch = (p.n + p.chunk - 1) / p.chunk;
     if (i < (long long)p.S * nch) {
       const int k = (int)(i / nch), c = (int)(i - (long long)k * nch);
-      const uint32_t* kb = p.skeys + (size_t)k * p.n;
       const int last = min((c + 1) * p.chunk, p.n) - 1;
-      const uint32_t key = kb[last];
       int lo = last + 1, hi = p.n;  // first position after `last` whose key differs (sorted)
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (kb[mid] == key) lo = mid + 1; else hi = mid;
+      if (p.skeys64) {  // (the 32-bit copies are being written by this same launch)
+        const unsigned long long* kb = p.skeys64 + (size_t)k * p.n;
+        const unsigned long long key = kb[last];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (kb[mid] == key) lo = mid + 1; else hi = mid;
+        }
+      } else {
+        const uint32_t* kb = p.skeys + (size_t)k * p.n;
+        const uint32_t key = kb[last];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (kb[mid] == key) lo = mid + 1; else hi = mid;
+        }
       }
       p.chunk_end[i] = lo;
     }
@@ -127,6 +143,8 @@ __global__ __launch_bounds__(256) void sort_aux_kernel(const SortAuxParams p) {
 
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.n > 0 && p.S > 0 && p.chunk > 0, "sort_aux: bad sizes");
+  ROCFM_REQUIRE(p.skeys64 == nullptr || (p.skeys_out != nullptr && p.id_bits >= 1 && p.id_bits <= 32),
+                "sort_aux: 64-bit keys need skeys_out and id_bits");
   const long long total = std::max<long long>((long long)p.S * p.n, (long long)p.S * ((p.n + p.chunk - 1) / p.chunk));
   hipLaunchKernelGGL(sort_aux_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
@@ -136,7 +154,8 @@ void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.pool_batches > 0 && p.S > 0, "fetch_multi: empty pool / S");
   ROCFM_REQUIRE(p.cur_dst != p.cur_src && p.step_dst != p.step_src, "fetch_multi: counters must differ");
   ROCFM_REQUIRE(p.keys == nullptr || ((unsigned long long)p.S << p.id_bits) <= (1ull << 32),
-                "fetch_multi: S << id_bits must fit in 32 bits");
+                "fetch_multi: S << id_bits must fit in 32 bits (use 64-bit keys)");
+  ROCFM_REQUIRE(p.keys64 == nullptr || p.id_bits <= 32, "fetch_multi: ids wider than 32 bits");
   const long long n = (long long)p.B * p.F;
   const int gx = (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 64));
   hipLaunchKernelGGL(fetch_multi_kernel, dim3(gx, p.S), dim3(256), 0, stream, p);

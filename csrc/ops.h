@@ -31,7 +31,10 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream);
 // sort.hip
 size_t sort_pairs_temp_bytes(int n, int end_bit);
 void sort_pairs_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_out,
-                     int n, int end_bit, hipStream_t stream);
+                     int n, int end_bit, hipStream_t stream, uint32_t first_val = 0);
+size_t sort_pairs64_temp_bytes(int n, int end_bit);
+void sort_pairs64_iota(void* temp, size_t temp_bytes, const uint64_t* keys_in, uint64_t* keys_out, uint32_t* vals_out,
+                       int n, int end_bit, hipStream_t stream);
 size_t sort_pairs_vals_temp_bytes(int n, int end_bit);
 void sort_pairs_vals(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                      const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit, hipStream_t stream);

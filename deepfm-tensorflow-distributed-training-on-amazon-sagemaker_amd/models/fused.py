@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -624,21 +625,26 @@ class FusedDeepFM:
     # kernel) and sorts all S·B·F lookups at once (composite key batch << id_bits | id), joined
     # at the graph's end.
     def _multi_S(self, Smax: int, shard: Optional[tuple] = None):
-        """(id bits, steps per graph): the composite sort key batch << id_bits | id is 32-bit,
-        so S is clamped to 2^(32 - id_bits)."""
+        """(id bits, steps per graph).  Graphs of S steps sort all S·B·F lookups at once on the
+        composite 32-bit key ``k << id_bits | id`` while S << id_bits fits (vocabularies up to
+        2^26 rows at S = 64); wider vocabularies (100M-1B rows) keep S and sort 64-bit composite
+        keys, whose ids the side chain then hands on as plain per-batch 32-bit keys
+        (``m_composite`` False)."""
         key_range = self.V if shard is None else shard[0] * shard[1]
         idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
-        return idbits, max(1, min(int(Smax), 1 << max(0, 32 - idbits)))
+        return idbits, max(1, int(Smax))
 
     def _build_multi(self, Smax: int, shard: Optional[tuple] = None) -> None:
         """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
         self._m_shard = shard
-        self.m_req = int(Smax)  # requested S (mS may be clamped below it by the key width)
+        self.m_req = int(Smax)
         idbits, Smax = self._multi_S(Smax, shard)
         sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
-        self.mS, self.m_idbits, self.m_bits = Smax, idbits, idbits + sbits
+        self.m_composite = (Smax << idbits) <= (1 << 32) and os.environ.get("ROCFM_SORT", "") != "wide"
+        self.mS, self.m_idbits = Smax, idbits
+        self.m_bits = idbits + sbits
         i32 = dict(dtype=torch.int32, device=dev)
         self.m_ids = torch.zeros(2, Smax, Bp, F, **i32)
         self.m_vals = torch.zeros(2, Smax, Bp, F, dtype=torch.float32, device=dev)
@@ -646,8 +652,13 @@ class FusedDeepFM:
         self.m_keys = torch.zeros(Smax * n, **i32)
         self.m_sk = torch.zeros(2, Smax * n, **i32)
         self.m_sv = torch.zeros(2, Smax * n, **i32)
-        self.m_temp = torch.zeros(max(H.sort_pairs_temp_bytes(Smax * n, self.m_bits), 16), dtype=torch.uint8,
-                                  device=dev)
+        if self.m_composite:
+            tb = H.sort_pairs_temp_bytes(Smax * n, self.m_bits)
+            self.m_keys64 = None
+        else:  # 64-bit keys in / out (the sorted ids land in m_sk via sort_aux)
+            tb = H.sort_pairs64_temp_bytes(Smax * n, self.m_bits)
+            self.m_keys64 = torch.zeros(2, Smax * n, dtype=torch.int64, device=dev)
+        self.m_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
         # each lookup's position in its batch's sorted order (the row kernel writes its gradient row
         # there) and the per-chunk run ends of the fused step tail (sort_aux, side chain)
         self.m_pos = torch.zeros(2, Smax * n, **i32)
@@ -661,7 +672,7 @@ class FusedDeepFM:
         self.m_params = [[self._step_param_set(self.m_ids[q, k], self.m_vals[q, k], self.m_labels[q, k],
                                                self.m_steps[q, k:].data_ptr(), self.m_lrt[q, k:].data_ptr(),
                                                self.m_sk[q, k * n:].data_ptr(), self.m_sv[q, k * n:].data_ptr(),
-                                               val_base=k * n, id_offset=k << idbits)
+                                               val_base=k * n, id_offset=(k << idbits) if self.m_composite else 0)
                           for k in range(Smax)] for q in range(2)]
         for q in range(2):
             for k in range(Smax):
@@ -688,6 +699,8 @@ class FusedDeepFM:
         f.ids, f.vals, f.labels = (self.m_ids[1 - q].data_ptr(), self.m_vals[1 - q].data_ptr(),
                                    self.m_labels[1 - q].data_ptr())
         f.keys, f.id_bits = self.m_keys.data_ptr(), self.m_idbits
+        if not self.m_composite:
+            f.keys, f.keys64 = 0, self.m_keys64[0].data_ptr()
         if getattr(self, "_m_shard", None) is not None:
             f.shard_W, f.shard_Vs = self._m_shard
         f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
@@ -699,13 +712,20 @@ class FusedDeepFM:
     def _prepare_multi(self, q: int, advance: int, stream) -> None:
         H = self.H
         H.fetch_multi(self._fetch_multi_params(q, advance), stream.cuda_stream)
-        H.sort_pairs_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys.data_ptr(),
-                          self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
-                          self.m_bits, stream.cuda_stream)
+        if self.m_composite:  # all S batches in one sort
+            H.sort_pairs_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys.data_ptr(),
+                              self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
+                              self.m_bits, stream.cuda_stream)
+        else:  # one sort of 64-bit composite keys
+            H.sort_pairs64_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys64[0].data_ptr(),
+                                self.m_keys64[1].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
+                                self.m_bits, stream.cuda_stream)
         a = H.SortAuxParams()
         a.skeys, a.svals = self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr()
         a.n, a.S, a.chunk = self.n_lookup, self.mS, self.m_chunk
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
+        if not self.m_composite:  # sorted 64-bit keys → plain per-batch ids in m_sk
+            a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
         H.sort_aux(a, stream.cuda_stream)
         if getattr(self, "_m_post", None) is not None:  # e.g. row-shard routing of the sorted batches
             self._m_post(1 - q, stream)
@@ -944,12 +964,12 @@ class FusedDeepFM:
             if (self.use_graph and self._primed and self._warm >= 2 and n >= S and self._i % 2 == 0
                     and not self._ring):
                 g = getattr(self, "_multi_graph", None)
-                if g is None or self._multi_S != S:
+                if g is None or self._pipe_S != S:
                     g = torch.cuda.CUDAGraph()
                     torch.cuda.synchronize(self.device)
                     with torch.cuda.graph(g):
                         self._enqueue_pipelined(S)
-                    self._multi_graph, self._multi_S = g, S
+                    self._multi_graph, self._pipe_S = g, S
                 g.replay()
                 self._i += S
                 n -= S

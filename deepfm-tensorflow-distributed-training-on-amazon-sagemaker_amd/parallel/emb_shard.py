@@ -773,7 +773,7 @@ class FusedRowShard:
                 rp = H.ShardRouteParams()
                 rp.skeys, rp.svals, rp.n = e.m_sk[q, k * n:].data_ptr(), e.m_sv[q, k * n:].data_ptr(), n
                 rp.W, rp.Vs, rp.cap = W, self.Vs, cap
-                rp.key_base, rp.val_base = k << e.m_idbits, k * n
+                rp.key_base, rp.val_base = (k << e.m_idbits) if e.m_composite else 0, k * n
                 rp.send_ids, rp.local_idx = self.ms_send[q, k].data_ptr(), self.ms_local[q, k].data_ptr()
                 rp.skeys_local, rp.counts = self.ms_skl[q, k].data_ptr(), self.ms_counts[q, k].data_ptr()
                 rp.overflow, rp.scratch = self.overflow.data_ptr(), self.ms_scratch.data_ptr()

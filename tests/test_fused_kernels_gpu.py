@@ -152,10 +152,14 @@ def test_device_auc_matches_streaming_auc():
     assert c == 5098 and abs(s - tot) < 1e-3
 
 
+@pytest.mark.parametrize("sort", ["composite", "wide"])
 @pytest.mark.parametrize("update", ["sparse", "exact"])
-def test_multi_step_graph_equals_per_step(update):
+def test_multi_step_graph_equals_per_step(update, sort, monkeypatch):
     """The multi-step pipeline (S steps per graph, one batched sort per graph, eager first graph,
-    tail graph of S' < S) trains bit-identically to per-step eager training."""
+    tail graph of S' < S) trains bit-identically to per-step eager training.  sort=wide: 64-bit
+    step|id keys — the path of vocabularies too wide for the 32-bit composite key (100M-1B rows),
+    forced here on a small one."""
+    monkeypatch.setenv("ROCFM_SORT", sort)
     spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[0.7, 0.8],
                      l2_reg=1e-3)
     hp = OptHParams(name="Adam", lr=2e-3)
@@ -170,6 +174,7 @@ def test_multi_step_graph_equals_per_step(update):
     a.attach_pool(ids, vals, labels)
     b.attach_pool(ids, vals, labels)
     a.train_steps(21, 8)  # 8 eager + 8 graph + 5 tail graph
+    assert a.m_composite == (sort == "composite")
     for _ in range(21):
         b.train_step()
     torch.cuda.synchronize()
