@@ -68,6 +68,13 @@ def parse():
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
                          "over the batch pool, 'safe' = batch_size*field_size (never overflows), or a number")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--input", default="pool", choices=["pool", "tfrecord"],
+                    help="pool: HBM-resident batch pool; tfrecord: synthetic Criteo-shape TFRecord files written "
+                         "before timing, fed through the C++ loader -> pinned ring -> HBM ring -> multi-step graphs "
+                         "(one GPU)")
+    ap.add_argument("--data_dir", default="", help="--input tfrecord: directory for the generated files (default: a "
+                                                   "temporary directory, removed afterwards)")
+    ap.add_argument("--loader_threads", type=int, default=16)
     ap.add_argument("--json_out", default="")
     return ap.parse_args()
 
@@ -128,6 +135,9 @@ def main():
     pool_ids = torch.stack([x[0] for x in pool])
     pool_vals = torch.stack([x[1] for x in pool])
     pool_labels = torch.stack([x[2] for x in pool])
+
+    if a.input == "tfrecord":
+        return bench_tfrecord(a, spec, hp, params, dev, rank)
 
     explicit_dp = a.parallelism in ("dp", "dense_dp")
     parallelism = a.parallelism
@@ -256,6 +266,99 @@ def main():
     if pg:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_tfrecord(a, spec, hp, params, dev, rank):
+    """Loader-fed end-to-end throughput on one GPU (the reference's tf.data chain is inside its
+    training loop: PS:147-165, HVD:128-159).  Files hold exactly W + K batches; the timed region
+    is the K steps' train_stream call — it starts the C++ decoders (skipping the W warm-up batches
+    undecoded) and ends when the last step has run, so pipeline fill and input stalls count."""
+    import shutil
+    import tempfile
+
+    import torch
+
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.data.tfrecord import TFRecordDataset
+    from rocfm.models.fused import FusedDeepFM
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--input tfrecord measures one GPU (use the Estimator / rocfm.cli for multi-GPU runs)")
+    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 16)
+    own = not a.data_dir
+    d = a.data_dir or tempfile.mkdtemp(prefix="rocfm_bench_")
+    os.makedirs(d, exist_ok=True)
+    nrec = (a.warmup + a.steps) * B
+    files, per = [], (nrec + 3) // 4
+    t0 = time.perf_counter()
+    for i in range(4):  # 4 files, like sharded S3 objects
+        p = os.path.join(d, f"tr{i}.tfrecords")
+        m = min(per, nrec - i * per)
+        if m <= 0:
+            break
+        if not (os.path.exists(p) and a.data_dir):
+            write_synthetic_tfrecord(p, m, a.feature_size, F, seed=a.seed + i)
+        files.append(p)
+    gen_s = time.perf_counter() - t0
+
+    def dataset():
+        return TFRecordDataset(files, F, B, a.feature_size, num_threads=a.loader_threads, verify_crc=True, hold=2)
+
+    # loader alone: decode every batch (CRC + Example parse into pinned memory), no GPU
+    t = time.perf_counter()
+    nb = sum(int(g[0].shape[0]) for g in dataset().groups(S))
+    loader_eps = nb * B / (time.perf_counter() - t)
+
+    eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
+                      compute_dtype=a.compute_dtype)
+    eng.train_stream(dataset().groups(S, hold=2, limit=a.warmup), S, hold=2)  # graphs + code objects
+    stall = [0.0]
+
+    def timed(it):
+        it = iter(it)
+        while True:
+            t1 = time.perf_counter()
+            x = next(it, None)
+            stall[0] += time.perf_counter() - t1
+            if x is None:
+                return
+            yield x
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = eng.train_stream(timed(dataset().groups(S, hold=2, skip=a.warmup, limit=a.steps)), S, hold=2)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.check()
+    if done != a.steps:
+        raise RuntimeError(f"trained {done} steps, expected {a.steps}")
+    value = B * a.steps / dt
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "examples/sec", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": round(value / EAGER_BASELINE[a.embedding_update], 3),
+        "dtype": a.compute_dtype,
+        "data": "synthetic Criteo-shape TFRecord files (39 fields, Zipf ids) through the C++ loader, random-init "
+                "weights",
+        "config": {"model": f"DeepFM Criteo-shape ({F} fields, {_human(a.feature_size)}-hash vocab, "
+                            f"k={a.embedding_size}, mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
+                   "global_batch": B, "seq_len": F, "parallelism": "dp1", "engine": "fused",
+                   "embedding_update": a.embedding_update, "input": "tfrecord", "steps_per_graph": S,
+                   "loader_threads": a.loader_threads},
+        "loader_alone_examples_per_sec": round(loader_eps, 1),
+        "input_stall_s": round(stall[0], 4),
+        "input_stall_fraction": round(stall[0] / dt, 4),
+        "data_gen_s": round(gen_s, 2),
+        "world_size": 1, "backend": None,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if own:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 if __name__ == "__main__":
