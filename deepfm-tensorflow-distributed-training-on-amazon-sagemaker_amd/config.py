@@ -107,6 +107,9 @@ class Config:
     seed: int = 1234
     save_checkpoints_steps: int = 0  # 0 → only at end (plus save_checkpoints_secs)
     save_checkpoints_secs: int = 600  # Estimator default cadence
+    hbm_cache: bool = True  # single GPU, >1 epoch, no shuffle: keep the decoded first epoch in HBM and
+    #                         train later epochs from it (the reference re-reads + re-parses every epoch)
+    hbm_cache_gb: float = 64.0  # budget for that cache (decoded epoch: B·(8F + 4) bytes per batch)
     ckpt_poll_steps: int = 200  # world > 1: steps between rank 0's broadcasts of the time-based save decision
     keep_checkpoint_max: int = 5
     eval_every_epoch: bool = True

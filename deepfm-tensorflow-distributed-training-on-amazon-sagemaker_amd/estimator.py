@@ -246,6 +246,17 @@ class Estimator:
             if faults:
                 faults.after_step(step)
 
+        # decoded-epoch HBM cache (single GPU, several epochs of the same files, no shuffle): epoch 1
+        # streams from the loader into an HBM ring sized for the whole epoch, epochs 2.. replay it
+        # from HBM (the reference's tf.data re-reads and re-parses every epoch, PS:147-165)
+        cache_nb = 0
+        if stream and num_epochs > 1 and cfg.hbm_cache and not cfg.perform_shuffle and skip_batches == 0 \
+                and not cfg.pipe_mode and limit is None and not max_steps:
+            nb = self._dataset(files, 1, training=True).num_batches()
+            if nb and nb * cfg.batch_size * (8 * cfg.field_size + 4) <= cfg.hbm_cache_gb * (1 << 30):
+                cache_nb = nb
+                batches = self._host_batches(self._dataset(files, 1, training=True).groups(S, hold=2))
+                batches = _timed(batches, timer)
         try:
             with trace_range("train"):
                 if stream:
@@ -268,7 +279,21 @@ class Estimator:
                             pend.append((first + n, *self.eng.loss_async()))
                         flush(False)
 
-                    self.eng.train_stream(batches, S, after_steps=after_graph, hold=2)
+                    self.eng.train_stream(batches, S, after_steps=after_graph, hold=2, ring_batches=cache_nb)
+                    if cache_nb:
+                        ids, vals, labels = self.eng.stream_ring()
+                        for _ in range(num_epochs - 1):
+                            g0 = self.global_step
+                            self.eng.attach_pool(ids[:cache_nb], vals[:cache_nb], labels[:cache_nb],
+                                                 start=(-g0) % cache_nb)
+                            left = cache_nb
+                            while left > 0:
+                                n = min(S, left)
+                                first = self.global_step
+                                self.eng.train_steps(n, S)
+                                after_graph(first, n)
+                                left -= n
+                        self._log({"event": "hbm_cache", "batches": cache_nb, "epochs_from_cache": num_epochs - 1})
                     flush(True)
                 elif self.engine_name == "fused":
                     it = self.eng.train_on(batches) if not hasattr(self.eng, "eng") else self._dp_train_on(batches)

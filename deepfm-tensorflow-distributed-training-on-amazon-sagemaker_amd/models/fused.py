@@ -847,7 +847,8 @@ class FusedDeepFM:
                 and getattr(self, "m_req", None) == steps_per_graph and self._m_primed:
             self._precapture_multi(self._m_graphs, ("m",), n, self._multi_body)
 
-    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1) -> int:
+    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
+                     ring_batches: int = 0) -> int:
         """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
 
         Batches are copied host → HBM on a copy stream into a device ring of 4·S batch slots, two
@@ -860,9 +861,12 @@ class FusedDeepFM:
         The source may recycle an item's host memory once it has been advanced ``hold`` more
         times; the copy of every such item is waited for first.  Returns the number of steps
         trained; ``after_steps(first_step, n_steps)`` runs after each graph launch.
+        ``ring_batches`` ≥ the number of batches streamed sizes the HBM ring to hold them all, so
+        that afterwards ``stream_ring()[i]`` is the i-th batch of this call (the decoded-epoch HBM
+        cache of the Estimator: later epochs train from it via attach_pool).
         """
         S = self._multi_S(int(steps_per_graph))[1]
-        R = 4 * S
+        R = max(4 * S, (int(ring_batches) + S - 1) // S * S)
         hold = max(1, int(hold))
         dev = self.device
         ring = getattr(self, "_stream_ring", None)
@@ -952,6 +956,10 @@ class FusedDeepFM:
             e0.synchronize()
         self._primed = False
         return done
+
+    def stream_ring(self):
+        """The HBM ring of the last train_stream call (ids, vals, labels)."""
+        return self._stream_ring
 
     def train_steps(self, n: int, steps_per_graph: int = 8) -> None:
         """``n`` optimisation steps from the attached pool; full step-pairs are replayed from one

@@ -99,3 +99,27 @@ def test_streamed_training_equals_per_step_and_resumes(data_dir, tmp_path):
     assert [r["global_step"] for r in train] == [16, 21] and all(r["loss"] == r["loss"] for r in train)
     for e in (a, b, c):
         e.close()
+
+
+def test_hbm_epoch_cache_equals_streaming(data_dir, tmp_path):
+    """hbm_cache: epoch 1 streams from the loader into an HBM ring sized for the epoch, epochs 2..
+    replay it from HBM through multi-step graphs — bit-identical to streaming every epoch (no
+    shuffle: every epoch presents the same batches in the same order, PS:147-165)."""
+    import json
+
+    from rocfm.estimator import Estimator
+
+    tr = [os.path.join(data_dir, "tr.tfrecords")]
+    mf = str(tmp_path / "metrics.jsonl")
+    a = Estimator(_cfg(data_dir, "", hbm_cache="true", metrics_file=mf))
+    b = Estimator(_cfg(data_dir, "", hbm_cache="false"))
+    ra, rb = a.train(tr, num_epochs=3), b.train(tr, num_epochs=3)
+    assert ra["steps"] == rb["steps"] == 3 * (8192 // 512)
+    sa, sb = a.eng.state_dict(), b.eng.state_dict()
+    bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
+    assert not bad, bad
+    logs = [json.loads(line) for line in open(mf)]
+    assert any(r.get("event") == "hbm_cache" and r["epochs_from_cache"] == 2 for r in logs)
+    assert [r["global_step"] for r in logs if r.get("event") == "train"][-1] == 48
+    for e in (a, b):
+        e.close()
