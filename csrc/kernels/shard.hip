@@ -69,9 +69,16 @@ __device__ __forceinline__ void load_tile(const ShardRouteParams& p, int i0, uin
   prev = (i0 > 0 && i0 <= p.n) ? p.skeys[i0 - 1] - p.key_base : kPad;
 }
 
+// Owner counts are reduced per workgroup in LDS first (one global atomic per owner present in the
+// tile): with every thread adding straight to p.counts[owner], the few owners of a small world
+// took ~10k same-address global atomics per step (34 µs at world 1; MI355X guide §atomics).
 __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams p) {
   __shared__ int s_w[kRWaves];
-  const int i0 = blockIdx.x * kRTile + threadIdx.x * kRI;
+  __shared__ int s_cnt[kMaxOwners];
+  const int t = threadIdx.x;
+  for (int o = t; o < p.W; o += kRT) s_cnt[o] = 0;
+  __syncthreads();
+  const int i0 = blockIdx.x * kRTile + t * kRI;
   uint32_t k[kRI], prev;
   load_tile(p, i0, k, prev);
   int heads = 0, cur_o = -1, cur_c = 0;
@@ -81,7 +88,7 @@ __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams
       ++heads;
       const int o = (int)(k[u] / p.Vs);
       if (o != cur_o) {
-        if (cur_c) atomicAdd(&p.counts[cur_o], cur_c);
+        if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
         cur_o = o;
         cur_c = 0;
       }
@@ -89,10 +96,12 @@ __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams
     }
     if (i0 + u < p.n) prev = k[u];
   }
-  if (cur_c) atomicAdd(&p.counts[cur_o], cur_c);
+  if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
   int total;
-  block_excl_scan(heads, s_w, total);
-  if (threadIdx.x == 0) p.scratch[blockIdx.x] = total;
+  block_excl_scan(heads, s_w, total);  // (its barriers also order the LDS count adds)
+  if (t == 0) p.scratch[blockIdx.x] = total;
+  for (int o = t; o < p.W; o += kRT)
+    if (s_cnt[o]) atomicAdd(&p.counts[o], s_cnt[o]);
 }
 
 __global__ __launch_bounds__(kRT) void shard_route_assign_kernel(ShardRouteParams p) {
