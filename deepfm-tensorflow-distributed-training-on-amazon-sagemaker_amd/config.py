@@ -117,6 +117,7 @@ class Config:
     use_hip_graph: bool = True
     profile_steps: str = ""  # "a:b" — wrap steps [a,b) with torch.profiler / roctx ranges
     metrics_file: str = ""  # JSONL metrics output
+    tensorboard: bool = True  # chief writes TF event files: model_dir (train) and model_dir/eval (utils/tensorboard.py)
     crc_check: bool = True  # verify TFRecord CRCs
     on_bad_record: str = "fail"  # fail | skip
     max_steps: int = 0  # 0 → run num_epochs

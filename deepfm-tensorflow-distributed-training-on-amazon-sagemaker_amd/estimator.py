@@ -71,6 +71,7 @@ class Estimator:
         if cfg.metrics_file and self.info.is_chief:
             os.makedirs(os.path.dirname(os.path.abspath(cfg.metrics_file)), exist_ok=True)
             self.metrics_fh = open(cfg.metrics_file, "a")
+        self._tb = {}  # TensorBoard writers by subdirectory ("" = train, "eval"), chief only
         if restore and self.model_dir:
             self.restore()
         # steps already trained by the job this estimator resumes (fast-forward on restart, below)
@@ -225,6 +226,8 @@ class Estimator:
             eps = (step - last_step) * cfg.batch_size * self.world / max(now - last_t, 1e-9)
             _, stall = timer.lap()
             last_t, last_step = now, step
+            self._summary("", step, {"loss": loss, "global_step/sec": eps / (cfg.batch_size * self.world),
+                                     "examples/sec": eps, "input_stall": stall})
             self._log({"event": "train", "global_step": step, "loss": loss, "examples_per_sec": eps,
                        "examples_per_sec_per_gpu": eps / self.world, "lr": self.hp.lr * self._lr_scale,
                        "input_stall": round(stall, 4)})
@@ -456,6 +459,7 @@ class Estimator:
             if self.world > 1:
                 P, Y = _gather_var(P), _gather_var(Y)
             res["auc_exact"] = exact_auc(Y, P) if len(P) else float("nan")
+        self._summary("eval", self.global_step, {k: v for k, v in res.items() if k not in ("global_step", "examples")})
         self._log({"event": "eval", **res})
         return res
 
@@ -571,8 +575,22 @@ class Estimator:
         if self.metrics_fh:
             self.metrics_fh.close()
             self.metrics_fh = None
+        for w in self._tb.values():
+            w.close()
+        self._tb = {}
 
     # ---- logging ------------------------------------------------------------------------------------
+    def _summary(self, sub: str, step: int, values: dict) -> None:
+        """Scalar summaries for TensorBoard (the Estimator's event files: model_dir, model_dir/eval)."""
+        if not (self.cfg.tensorboard and self.info.is_chief and self.model_dir):
+            return
+        w = self._tb.get(sub)
+        if w is None:
+            from .utils.tensorboard import EventWriter
+
+            w = self._tb[sub] = EventWriter(os.path.join(self.model_dir, sub) if sub else self.model_dir)
+        w.scalars(int(step), values)
+
     def _log(self, rec: dict) -> None:
         if not self.info.is_chief:
             return

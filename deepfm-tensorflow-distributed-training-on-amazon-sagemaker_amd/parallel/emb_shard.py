@@ -460,6 +460,13 @@ class FusedRowShard:
             for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
                 self.p2p_x[t.data_ptr()] = ex
             self.graph_collectives = use_graph  # push kernels are capturable whatever the backend
+        elif self.W == 1 and not self.force:
+            # one rank: every exchange is the identity, so the receive side IS the send side (rows
+            # and row gradients share one buffer each; the request list each step reads is that
+            # step's own send list, bound per step below) — no copies in the step
+            self.recv_ids = None
+            self.rows_in = self.rows_out
+            self.grad_back = self.grad_stage
         else:
             self.recv_ids = torch.full((M,), PAD, **i32)
             self.rows_in = torch.zeros(M, Kp, **f32)
@@ -498,16 +505,8 @@ class FusedRowShard:
         e, H = self.eng, self.H
         self.route = [self._route_params(e.slot_ids[q], self.rsv[q], self.send_ids[q], self.local_idx[q], self.skl[q],
                                          self.counts[q], self.n) for q in range(2)]
-        sv = H.ShardServeParams()
-        sv.ids, sv.m, sv.W, sv.rank, sv.Vs = self.recv_ids.data_ptr(), self.M, self.W, self.rank, self.Vs
-        sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
-        sv.bad = self.bad.data_ptr()
-        self.serve = sv
-        pv = H.ShardServeParams()
-        pv.ids, pv.m, pv.W, pv.rank, pv.Vs = self.recv_ids.data_ptr(), self.M, self.W, self.rank, self.Vs
-        pv.table, pv.Kp, pv.rows_out, pv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
-        pv.bad = self.bad.data_ptr()
-        self.pred_serve = pv
+        self.serve = [self._serve_params(self._recv_ids_for(self.send_ids[p])) for p in range(2)]
+        self.pred_serve = self._serve_params(self._recv_ids_for(self.pred_send))
         self.owner_params = []
         for p in range(2):
             rp = e.rows_params[p]
@@ -517,7 +516,7 @@ class FusedRowShard:
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
             lp.touched = 0  # writes the exchange stage, not the table's gradient rows
             op = H.MergeParams()  # owner: Σ over source ranks per local row → optimizer
-            op.keys, op.key_stride = self.recv_ids.data_ptr(), self.cap
+            op.keys, op.key_stride = self._recv_ids_for(self.send_ids[p]).data_ptr(), self.cap
             op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
@@ -542,6 +541,18 @@ class FusedRowShard:
         pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
         self.pred_route = self._route_params(e.pred_ids, self.pred_rsv, self.pred_send, self.pred_local,
                                              self.pred_skl, self.pred_counts, self.n)
+
+    def _recv_ids_for(self, send: torch.Tensor) -> torch.Tensor:
+        """The request list an owner reads after exchanging ``send`` (world 1: ``send`` itself)."""
+        return send if self.recv_ids is None else self.recv_ids
+
+    def _serve_params(self, ids: torch.Tensor):
+        e = self.eng
+        sv = self.H.ShardServeParams()
+        sv.ids, sv.m, sv.W, sv.rank, sv.Vs = ids.data_ptr(), self.M, self.W, self.rank, self.Vs
+        sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
+        sv.bad = self.bad.data_ptr()
+        return sv
 
     # ---- batch feeding (delegated) ------------------------------------------------------------
     def attach_pool(self, ids, vals, labels, start: int = 0):
@@ -591,7 +602,7 @@ class FusedRowShard:
         return side
 
     def _phase_serve(self, p: int) -> None:
-        self.H.shard_serve(self.serve, self.eng.stream_ptr)
+        self.H.shard_serve(self.serve[p], self.eng.stream_ptr)
 
     def _phase_compute(self, p: int, with_side: bool = True) -> None:
         e, H = self.eng, self.H
@@ -631,7 +642,10 @@ class FusedRowShard:
         g.replay()
 
     def _exchange(self, out, inp):
-        """Equal-split all-to-all of ``inp`` into ``out`` (X1-X3)."""
+        """Equal-split all-to-all of ``inp`` into ``out`` (X1-X3).  World 1 (no forced collectives):
+        the receive side aliases the send side, nothing to move."""
+        if out is None or out is inp or out.data_ptr() == inp.data_ptr():
+            return
         ex = self.p2p_x.get(out.data_ptr())
         if ex is not None:
             key = (out.data_ptr(), inp.data_ptr())
@@ -794,9 +808,10 @@ class FusedRowShard:
                           "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
+                mg.keys = self._recv_ids_for(self.ms_send[q, k]).data_ptr()
                 if ed is not None:
                     ed.grad_scale = 1.0
-                steps.append((rows, wp, ep, da, ed, mg))
+                steps.append((rows, wp, ep, da, ed, mg, self._serve_params(self._recv_ids_for(self.ms_send[q, k]))))
             self.ms_route.append(routes)
             self.ms_steps.append(steps)
 
@@ -813,9 +828,9 @@ class FusedRowShard:
         e, H = self.eng, self.H
         s = torch.cuda.current_stream(self.device).cuda_stream
         for k in range(S):
-            rows, wp, ep, da, ed, mg = self.ms_steps[q][k]
+            rows, wp, ep, da, ed, mg, sv = self.ms_steps[q][k]
             self._exchange(self.recv_ids, self.ms_send[q, k])                   # X1 requests
-            H.shard_serve(self.serve, s)
+            H.shard_serve(sv, s)
             self._exchange(self.rows_in, self.rows_out)                         # X2 rows
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request

@@ -137,3 +137,32 @@ def test_sagemaker_pipe_mode_channels(data_dir, tmp_path, monkeypatch):
     assert out["channels"]["eval"] == [str(base / "data" / "evaluation_0")]
     assert out["train"]["steps"] == 2 * (6000 // 256)
     assert out["eval"]["examples"] == (1500 // 256) * 256
+
+
+def test_tensorboard_event_files(data_dir, tmp_path):
+    """Estimator summaries: TF event files in model_dir (train) and model_dir/eval, readable back
+    (TFRecord framing with valid CRCs, Event/Summary protobuf encoding)."""
+    import glob
+
+    from rocfm.utils.tensorboard import encode_event, frame, read_scalars
+
+    md = str(tmp_path / "m")
+    est = Estimator(_cfg(data_dir, md))
+    est.train([os.path.join(data_dir, "tr.tfrecords")], num_epochs=1)
+    res = est.evaluate([os.path.join(data_dir, "va.tfrecords")])
+    est.close()
+    tr = glob.glob(os.path.join(md, "events.out.tfevents.*"))
+    ev = glob.glob(os.path.join(md, "eval", "events.out.tfevents.*"))
+    assert len(tr) == 1 and len(ev) == 1
+    s = read_scalars(tr[0])
+    losses = [(st, v) for st, tag, v in s if tag == "loss"]
+    assert [st for st, _ in losses] == list(range(5, 6000 // 256 + 1, 5))
+    assert all(np.isfinite(v) for _, v in losses)
+    assert {"global_step/sec", "examples/sec"} <= {tag for _, tag, _ in s}
+    e = {tag: v for _, tag, v in read_scalars(ev[0])}
+    assert abs(e["auc"] - res["auc"]) < 1e-6 and abs(e["loss"] - res["loss"]) < 1e-5
+    # byte-level encoding of one event (field numbers / wire types of tensorflow.Event)
+    b = encode_event(1.5, 7, {"x": 2.0})
+    assert b == (b"\x09" + np.float64(1.5).tobytes() + b"\x10\x07" + b"\x2a\x0a\x0a\x08\x0a\x01x\x15"
+                 + np.float32(2.0).tobytes())
+    assert len(frame(b)) == len(b) + 16
