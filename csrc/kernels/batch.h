@@ -81,6 +81,9 @@ struct SortAuxParams {
   const unsigned long long* skeys64;
   uint32_t* skeys_out;
   int id_bits;
+  // nullable: [S][ceil(n / chunk)] run heads per chunk (the sorted DP export's output bases,
+  // EmbUpdateParams::chunk_heads); chunk must be a multiple of 64 and at most 1024
+  int32_t* chunk_heads;
 };
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream);
 

@@ -141,6 +141,23 @@ __global__ __launch_bounds__(256) void sort_aux_kernel(const SortAuxParams p) {
   }
 }
 
+// One workgroup of `chunk` threads per (batch, chunk): run heads of the chunk (ballot counts).
+__global__ __launch_bounds__(1024) void chunk_heads_kernel(const SortAuxParams p, int nch) {
+  __shared__ int s_w[16];
+  const int k = blockIdx.y, c = blockIdx.x, t = threadIdx.x;
+  const uint32_t* kb = (p.skeys64 ? p.skeys_out : p.skeys) + (size_t)k * p.n;
+  const int i = c * p.chunk + t;
+  const bool head = i < p.n && (i == 0 || kb[i] != kb[i - 1]);
+  const unsigned long long m = __ballot(head);
+  if ((t & 63) == 0) s_w[t >> 6] = __popcll(m);
+  __syncthreads();
+  if (t == 0) {
+    int h = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) h += s_w[w];
+    p.chunk_heads[(size_t)k * nch + c] = h;
+  }
+}
+
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.n > 0 && p.S > 0 && p.chunk > 0, "sort_aux: bad sizes");
   ROCFM_REQUIRE(p.skeys64 == nullptr || (p.skeys_out != nullptr && p.id_bits >= 1 && p.id_bits <= 32),
@@ -148,6 +165,12 @@ void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
   const long long total = std::max<long long>((long long)p.S * p.n, (long long)p.S * ((p.n + p.chunk - 1) / p.chunk));
   hipLaunchKernelGGL(sort_aux_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
+  if (p.chunk_heads) {  // after sort_aux: the 64-bit path reads the plain ids it wrote
+    ROCFM_REQUIRE(p.chunk % 64 == 0 && p.chunk <= 1024, "sort_aux: chunk_heads needs chunk % 64 == 0, <= 1024");
+    const int nch = (p.n + p.chunk - 1) / p.chunk;
+    hipLaunchKernelGGL(chunk_heads_kernel, dim3(nch, p.S), dim3(p.chunk), 0, stream, p, nch);
+    ROCFM_HIP_CHECK(hipGetLastError());
+  }
 }
 
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {

@@ -16,6 +16,12 @@ __device__ __forceinline__ const float4* contrib_row4(const EmbUpdateParams& p, 
   return reinterpret_cast<const float4*>(r);
 }
 
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
@@ -42,12 +48,23 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   __shared__ uint32_t s_hkey[kChunk + 1];
   __shared__ int s_wcnt[kWaves];
   __shared__ int s_nh, s_last_end, s_out_base;
+  __shared__ int s_hb[2 * kWaves];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c0 = bid * kChunk;
   const int cend = min(c0 + kChunk, p.n);
   const int i = c0 + t;
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
+  // sorted export (mode 2 + chunk_heads): this chunk's output base and the batch's total, from the
+  // side chain's per-chunk head counts (loaded with the keys; reduced below with the head compaction)
+  int hb_before = 0, hb_total = 0;
+  if (p.mode == 2 && p.chunk_heads != nullptr) {
+    for (int c = t; c < p.nch; c += kChunk) {
+      const int h = p.chunk_heads[c];
+      hb_total += h;
+      hb_before += c < bid ? h : 0;
+    }
+  }
   ROCFM_STAMP(p.stamps, 0);
 
   // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
@@ -86,7 +103,25 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const unsigned long long m = __ballot(head);
   const int before = __popcll(m & ((1ull << lane) - 1ull));
   if (lane == 0) s_wcnt[wave] = __popcll(m);
+  const bool sorted_out = p.mode == 2 && p.chunk_heads != nullptr;
+  if (sorted_out) {
+    hb_before = wave_sum_i(hb_before);
+    hb_total = wave_sum_i(hb_total);
+    if (lane == 0) {
+      s_hb[wave] = hb_before;
+      s_hb[kWaves + wave] = hb_total;
+    }
+  }
   __syncthreads();
+  if (sorted_out && t == 0) {
+    int b = 0, tot = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      b += s_hb[w];
+      tot += s_hb[kWaves + w];
+    }
+    s_out_base = b;
+    if (bid == 0) *p.out_count = tot;
+  }
   {
     int base = 0;
     for (int w = 0; w < wave; ++w) base += s_wcnt[w];
@@ -135,7 +170,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       }
       pos += kChunk;
     }
-    if (t == 0 && p.mode == 2) s_out_base = atomicAdd(p.out_count, nh);
+    if (t == 0 && p.mode == 2 && !sorted_out) s_out_base = atomicAdd(p.out_count, nh);
   }
   __syncthreads();
   ROCFM_STAMP(p.stamps, 2);

@@ -35,6 +35,11 @@ struct EmbUpdateParams {
   int sorted_contrib;  // 1: contrib rows are already in sorted order (row i ↔ sorted entry i; svals unused)
   const int32_t* chunk_end;  // nullable: per workgroup chunk, end of the run holding its last entry
   uint32_t* touched;   // mode 1 (nullable): touched[row] = step + 1 for every row whose gradient it wrote
+  // mode 2 (nullable): run heads per workgroup chunk (sort_aux, side chain).  The export then
+  // places chunk c's rows at Σ heads of chunks < c — the list comes out in sorted key order and is
+  // deterministic — and workgroup 0 stores the total count (no atomics; out_count need not be zeroed)
+  const int32_t* chunk_heads;
+  int nch;  // chunks of this batch (entries of chunk_heads)
 };
 
 struct EmbDenseParams {

@@ -9,6 +9,13 @@
 //   merge_apply   : the representative entry (r == rep[key]) sums the rows of key over r..W−1 in
 //                   rank order (deterministic, no float atomics), applies lazy L2 + the row
 //                   optimizer (or writes a dense gradient row), and restores pos/rep.
+// Search mode (merge_search_apply; every source list ascending within its count, pads last — the
+// row-shard request lists and the sorted DP export): ONE launch and no maps at all.  Each entry
+// binary-searches its key in the other W−1 lists (all searches advance together, one round of
+// L2-resident loads per halving); an entry found in a lower rank's list is not the representative,
+// the representative sums the rows it found in rank order and applies the optimizer as above.  At
+// W = 1 no search is made.  The MLP optimizer (dense_apply over the gathered rank segments) rides
+// as extra workgroups of the same launch.
 // Hash mode (hash_slots > 0; O(W·cap) memory whatever the vocabulary — the 1B-row tables): a
 // linear-probing table of hash_slots ≥ 2·W·cap slots replaces the maps.  Every word carries the
 // step's tag T = global_step + 1 in its high half, so slots of earlier steps read as empty and
@@ -61,5 +68,7 @@ void launch_merge_apply(const MergeParams& p, hipStream_t stream);
 void launch_merge_init(const MergeParams& p, hipStream_t stream);  // pos = −1, rep = W
 struct DenseApplyParams;
 void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d, hipStream_t stream);
+// search mode; d (nullable): the MLP optimizer launched as extra workgroups
+void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream);
 
 }  // namespace rocfm

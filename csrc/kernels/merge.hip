@@ -14,6 +14,10 @@ constexpr int kMergeThreads = 256;
 constexpr int kApplyThreads = 64;
 constexpr int kMaxW = 64;
 
+__device__ __forceinline__ float4 f4add_m(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
 __device__ __forceinline__ bool entry_valid(const MergeParams& p, int r, int j, uint32_t key) {
   if (key == kPadKey) return false;
   if (p.counts && j >= p.counts[(size_t)r * p.count_stride]) return false;
@@ -246,6 +250,185 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_dense_kernel(Merg
   }
 }
 
+// ---- search mode ----------------------------------------------------------------------------
+// Source q's list and its valid length (counts, else the cap: pads sort last)
+__device__ __forceinline__ const uint32_t* list_of(const MergeParams& p, int q) { return p.keys + (size_t)q * p.key_stride; }
+__device__ __forceinline__ int len_of(const MergeParams& p, int q) {
+  return p.counts ? min(max(p.counts[(size_t)q * p.count_stride], 0), p.cap) : p.cap;
+}
+
+// Optimizer (mode 0) or dense-gradient row (mode 1) of one merged row: shared by the search apply
+template <int KP4>
+__device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t row, float4 (&w)[KP4], float4 (&a)[KP4],
+                                               float4 (&b)[KP4], const float4 (&acc)[KP4]) {
+  const size_t base = (size_t)row * KP4;
+  if (p.mode == 1) {
+    float4* dg = reinterpret_cast<float4*>(p.dense_grad) + base;
+#pragma unroll
+    for (int c = 0; c < KP4; ++c)
+      dg[c] = make_float4(acc[c].x * p.grad_scale, acc[c].y * p.grad_scale, acc[c].z * p.grad_scale,
+                          acc[c].w * p.grad_scale);
+    if (p.touched) p.touched[row] = (uint32_t)*p.step + 1u;
+    return;
+  }
+  const OptStep st = opt_step(p.opt, *p.step);
+  float4* e4 = reinterpret_cast<float4*>(p.emb) + base;
+  float4* a4 = p.s0 ? reinterpret_cast<float4*>(p.s0) + base : nullptr;
+  float4* b4 = p.s1 ? reinterpret_cast<float4*>(p.s1) + base : nullptr;
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) {
+    float* wc = &w[c].x;
+    float* ac = &a[c].x;
+    float* bc = &b[c].x;
+    const float* gc = &acc[c].x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (c * 4 + u >= p.K1) continue;
+      opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
+    }
+    e4[c] = w[c];
+    if (a4) a4[c] = a[c];
+    if (b4) b4[c] = b[c];
+  }
+}
+
+// WMAX = 8: the W−1 searches advance together (≈log2(cap) rounds of up to 7 independent loads);
+// larger worlds search the lists one after another.
+template <int KP4, int WMAX>
+__device__ __forceinline__ void merge_search_body(const MergeParams& p, const int i) {
+  if (i >= p.W * p.cap) return;
+  const int r = i / p.cap, j = i - r * p.cap;
+  if (j == 0 && p.overflow && p.counts && p.counts[(size_t)r * p.count_stride] > p.cap) *p.overflow = 1;
+  const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
+  if (!entry_valid(p, r, j, key)) return;
+  const uint32_t row = key / p.key_div;
+  const int W = p.W;
+  const size_t base = (size_t)row * KP4;
+  // the row's parameters and slots: issued before the searches (same as merge_apply)
+  float4 w[KP4], a[KP4], b[KP4];
+  const float4* e4r = reinterpret_cast<const float4*>(p.emb) + base;
+  const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
+  const float4* b4r = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb) + base;
+  if (p.mode == 0) {
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) {
+      w[c] = e4r[c];
+      a[c] = a4r[c];
+      b[c] = b4r[c];
+    }
+    if (!p.s0)
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!p.s1)
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) b[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 acc[KP4];
+  const float4* own = reinterpret_cast<const float4*>(p.rows + (size_t)r * p.row_stride + (size_t)j * p.Kp);
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) acc[c] = own[c];
+  if (W > 1) {
+    if constexpr (WMAX <= 8) {
+      int lo[WMAX], len[WMAX], at[WMAX];
+#pragma unroll
+      for (int q = 0; q < WMAX; ++q) {
+        lo[q] = 0;
+        at[q] = -1;
+        len[q] = (q < W && q != r) ? len_of(p, q) : 0;
+      }
+      for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < WMAX; ++q) {
+          if (len[q] <= 0) continue;
+          any = true;
+          const int half = len[q] >> 1;
+          const uint32_t v = list_of(p, q)[lo[q] + half];
+          if (v == key) {
+            at[q] = lo[q] + half;
+            len[q] = 0;
+          } else if (v < key) {
+            lo[q] += half + 1;
+            len[q] -= half + 1;
+          } else {
+            len[q] = half;
+          }
+        }
+        if (!any) break;
+      }
+#pragma unroll
+      for (int q = 0; q < WMAX; ++q)
+        if (q < r && at[q] >= 0) return;  // a lower rank holds the key: not the representative
+      // rank order, this entry's own row first (it is the lowest rank holding the key)
+      float4 v[WMAX][KP4];
+#pragma unroll
+      for (int q = 0; q < WMAX; ++q) {
+        const float4* src = reinterpret_cast<const float4*>(
+            p.rows + (at[q] >= 0 ? (size_t)q * p.row_stride + (size_t)at[q] * p.Kp : 0));
+#pragma unroll
+        for (int c = 0; c < KP4; ++c) v[q][c] = (q < W && q > r && at[q] >= 0) ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < WMAX; ++q) {
+        if (q >= W || q <= r || at[q] < 0) continue;
+#pragma unroll
+        for (int c = 0; c < KP4; ++c) acc[c] = f4add_m(acc[c], v[q][c]);
+      }
+    } else {
+      auto find = [&](int q) -> int {
+        const uint32_t* L = list_of(p, q);
+        int lo = 0, len = len_of(p, q);
+        while (len > 0) {
+          const int half = len >> 1;
+          const uint32_t v = L[lo + half];
+          if (v == key) return lo + half;
+          if (v < key) {
+            lo += half + 1;
+            len -= half + 1;
+          } else {
+            len = half;
+          }
+        }
+        return -1;
+      };
+      for (int q = 0; q < r; ++q)
+        if (find(q) >= 0) return;
+      for (int q = r + 1; q < W; ++q) {
+        const int at = find(q);
+        if (at < 0) continue;
+        const float4* src = reinterpret_cast<const float4*>(p.rows + (size_t)q * p.row_stride + (size_t)at * p.Kp);
+#pragma unroll
+        for (int c = 0; c < KP4; ++c) acc[c] = f4add_m(acc[c], src[c]);
+      }
+    }
+  }
+  merged_row_out<KP4>(p, row, w, a, b, acc);
+}
+
+template <int KP4, int WMAX>
+__global__ __launch_bounds__(kApplyThreads) void merge_search_apply_kernel(MergeParams p, DenseApplyParams d,
+                                                                           int n_apply, int n_dense) {
+  if ((int)blockIdx.x < n_apply) {
+    merge_search_body<KP4, WMAX>(p, blockIdx.x * kApplyThreads + threadIdx.x);
+  } else {
+    dense_apply_body<kApplyThreads>(d, blockIdx.x - n_apply, n_dense);
+  }
+}
+
+template <int KP4>
+void launch_search_t(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+  const int n_apply = p.cap > 0 ? cdiv(p.W * p.cap, kApplyThreads) : 0;
+  const int n_dense = d ? std::max(1, std::min(cdiv(d->n, kApplyThreads), 1024)) : 0;
+  DenseApplyParams dd{};
+  if (d) dd = *d;
+  if (n_apply + n_dense == 0) return;
+  const dim3 grid(n_apply + n_dense), block(kApplyThreads);
+  if (p.W <= 8)
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, 8>), grid, block, 0, stream, p, dd, n_apply, n_dense);
+  else
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p, dd, n_apply, n_dense);
+}
+
 template <int KP4>
 void launch_apply_t(const MergeParams& p, hipStream_t stream) {
   const dim3 grid(cdiv(p.W * p.cap, kApplyThreads)), block(kApplyThreads);
@@ -294,6 +477,26 @@ void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d,
   const int n_dense = std::max(1, std::min(cdiv(d.n, 256), 256));
   hipLaunchKernelGGL(merge_scatter_dense_kernel, dim3(n_scatter + n_dense), dim3(kMergeThreads), 0, stream, p, d,
                      n_scatter, n_dense);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+  ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge: 1 <= W <= 64");
+  ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
+  ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
+  ROCFM_REQUIRE(p.key_div >= 1 && p.keys && p.rows && p.step, "merge: keys / rows / step missing");
+  ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : p.emb != nullptr, "merge_search_apply: missing outputs");
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N)                    \
+  case N:                               \
+    launch_search_t<N>(p, d, stream);   \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("merge: unsupported Kp");
+  }
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

@@ -188,9 +188,10 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
 
 // Elementwise optimizer over the flat dense buffer (+ bf16 / swizzled weight refresh), block `bid`
 // of `nblocks` 256-thread blocks (grid-strided).
+template <int TPB = 256>
 __device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, const int bid, const int nblocks) {
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
-  for (int idx = bid * 256 + (int)threadIdx.x; idx < p.n; idx += nblocks * 256) {
+  for (int idx = bid * TPB + (int)threadIdx.x; idx < p.n; idx += nblocks * TPB) {
     float w = p.params[idx];
     if (p.apply) {
       float a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;

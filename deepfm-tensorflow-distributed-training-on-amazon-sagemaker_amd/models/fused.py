@@ -634,8 +634,10 @@ class FusedDeepFM:
         idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
         return idbits, max(1, int(Smax))
 
-    def _build_multi(self, Smax: int, shard: Optional[tuple] = None) -> None:
-        """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard)."""
+    def _build_multi(self, Smax: int, shard: Optional[tuple] = None, heads: bool = False) -> None:
+        """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard).
+        ``heads``: the side chain also counts run heads per tail chunk (``m_chd``; the sorted DP
+        export places each chunk's rows from them)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
         self._m_shard = shard
@@ -665,6 +667,7 @@ class FusedDeepFM:
         self.m_chunk = self.H.tail_chunk()
         self.m_nch = (n + self.m_chunk - 1) // self.m_chunk
         self.m_cend = torch.zeros(2, Smax * self.m_nch, **i32)
+        self.m_chd = torch.zeros(2, Smax * self.m_nch, **i32) if heads else None
         self.m_steps = torch.zeros(2, Smax, dtype=torch.int64, device=dev)
         self.m_lrt = torch.zeros(2, Smax, dtype=torch.float32, device=dev)
         self.m_cur = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -724,6 +727,8 @@ class FusedDeepFM:
         a.skeys, a.svals = self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr()
         a.n, a.S, a.chunk = self.n_lookup, self.mS, self.m_chunk
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
+        if self.m_chd is not None:
+            a.chunk_heads = self.m_chd[1 - q].data_ptr()
         if not self.m_composite:  # sorted 64-bit keys → plain per-batch ids in m_sk
             a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
         H.sort_aux(a, stream.cuda_stream)

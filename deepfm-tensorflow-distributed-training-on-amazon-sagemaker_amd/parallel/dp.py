@@ -415,7 +415,10 @@ class FusedDataParallel:
     #            → emb_dense_update
     def _build_multi_dp(self, Smax: int) -> None:
         e, H = self.eng, self.eng.H
-        e._build_multi(Smax)
+        # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
+        # needs no maps: one search-mode launch (merge.hip) after the exchange
+        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp()
+        e._build_multi(Smax, heads=self.m_sorted)
         e._m_pool = e.pool_ids
         S_, n = e.mS, e.n_lookup
         self.m_dp = []
@@ -441,6 +444,8 @@ class FusedDataParallel:
                 ex.out_rows = self.send[self.off_rows:].data_ptr()
                 ex.out_count = self.send[self.off_cnt:].data_ptr()
                 ex.out_cap = self.cap
+                if self.m_sorted:
+                    ex.chunk_heads, ex.nch = e.m_chd[q, k * e.m_nch:].data_ptr(), e.m_nch
                 mg = H.MergeParams()
                 src = self.merge_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
@@ -464,7 +469,11 @@ class FusedDataParallel:
             H.deepfm_rows(rows, s)  # (dp: also zeroes the export counter)
             e._tail(wp, ep, None, s)
             self._exchange()
-            if self.mode == "dp":
+            if self.mode == "dp" and self.m_sorted:
+                H.merge_search_apply(mg, da, s)  # row merge ‖ MLP optimizer, one launch
+                if ed is not None:
+                    H.emb_dense_update(ed, s)
+            elif self.mode == "dp":
                 H.merge_scatter_dense(mg, da, s)  # row scatter ‖ MLP optimizer, one launch
                 H.merge_apply(mg, s)
                 if ed is not None:

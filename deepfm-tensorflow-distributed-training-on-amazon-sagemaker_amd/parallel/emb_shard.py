@@ -15,9 +15,12 @@ of HBM).  Every step, synchronously:
             each lookup's received-row index as its id; the lookup gradients are reduced per
             received row (emb_update.hip mode 1)
     X3      all_to_all  row gradients back to owners   [W, cap, K+1] f32
-    update  owners sum each requested row's gradients over source ranks in rank order (direct-
-            addressed position maps, merge.hip — no sort), apply lazy L2 once and the row optimizer (or, ``embedding_update=exact``, the dense full-table
-            update of the shard — the reference's full L2, with no dense traffic at all)
+    update  owners sum each requested row's gradients over source ranks in rank order (one
+            launch, merge.hip search mode: every request list is ascending, so each entry finds
+            its row in the other lists by binary search — no maps, no sort), apply lazy L2 once
+            and the row optimizer (or, ``embedding_update=exact``, the dense full-table update of
+            the shard — the reference's full L2, with no dense traffic at all); the MLP optimizer
+            rides as extra workgroups of the same launch
     X4      all_reduce  MLP gradients (one flat bucket), then the dense optimizer
 
 The exchange buffers have a fixed per-owner capacity so that every collective has static shapes
@@ -472,11 +475,6 @@ class FusedRowShard:
             self.rows_in = torch.zeros(M, Kp, **f32)
             self.grad_back = torch.zeros(M, Kp, **f32)
         self._p2p_params = {}
-        # owner merge maps (merge.hip): position of each local row in every source's request list
-        # (direct addressing over the local rows, or a W·cap hash table for very large shards)
-        from .dp import MergeMaps
-
-        self.maps = MergeMaps(W, cap, Vs, dev)
         # prediction routing (own buffers: never races the pipelined training route)
         self.pred_rsv = torch.zeros(n, **i32)
         self.pred_send = torch.full((M,), PAD, **i32)
@@ -486,7 +484,6 @@ class FusedRowShard:
         self._graphs: Dict = {}
         self._warm = 0
         self._build()
-        H.merge_init(self.owner_params[0], e.stream_ptr)
 
     # ---- kernel parameter blocks ------------------------------------------------------------------
     def _route_params(self, ids, rsv, send, local, skl, counts, n):
@@ -521,7 +518,6 @@ class FusedRowShard:
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
             op.key_div, op.Vmap = self.W, self.Vs
-            self.maps.bind(op)
             op.emb = e.emb.data_ptr()
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
@@ -617,16 +613,9 @@ class FusedRowShard:
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
         s = e.stream_ptr
-        main = torch.cuda.current_stream(self.device)
-        aux = e.aux_stream  # MLP optimizer concurrently with the owner's row update
-        aux.wait_stream(main)
-        with torch.cuda.stream(aux):
-            H.dense_apply(e.dense_apply_params[p], aux.cuda_stream)
-        H.merge_scatter(self.owner_params[p], s)
-        H.merge_apply(self.owner_params[p], s)
+        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], s)  # owner merge ‖ MLP opt
         if self.embedding_update == "exact":
             H.emb_dense_update(e.emb_dense_params[p], s)
-        e._join(aux)
 
     def _run(self, key, fn, collectives: bool = False):
         if not self.use_graph or self._warm < 4:
@@ -804,8 +793,8 @@ class FusedRowShard:
                 mg = H.MergeParams()
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
-                          "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos"):
+                          "K1", "key_div", "Vmap", "emb", "s0", "s1", "l2", "grad_scale", "mode",
+                          "dense_grad", "touched"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 mg.keys = self._recv_ids_for(self.ms_send[q, k]).data_ptr()
@@ -836,8 +825,7 @@ class FusedRowShard:
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
             self._allreduce_mlp()                                               # X4 MLP grads
-            H.merge_scatter_dense(mg, da, s)                                    # owner scatter ‖ MLP opt
-            H.merge_apply(mg, s)
+            H.merge_search_apply(mg, da, s)                                     # owner merge ‖ MLP opt
             if ed is not None:
                 H.emb_dense_update(ed, s)
 
@@ -955,7 +943,6 @@ class FusedRowShard:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
-        self.maps.reset()  # the hash merge tags words with the step, which just moved
         self._graphs = {}
         self._warm = 0
 
