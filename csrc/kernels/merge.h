@@ -68,7 +68,10 @@ void launch_merge_apply(const MergeParams& p, hipStream_t stream);
 void launch_merge_init(const MergeParams& p, hipStream_t stream);  // pos = −1, rep = W
 struct DenseApplyParams;
 void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d, hipStream_t stream);
-// search mode; d (nullable): the MLP optimizer launched as extra workgroups
-void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream);
+// search mode; d (nullable): the MLP optimizer launched as extra workgroups; sv (nullable): a
+// row-shard serve (shard.h) as further workgroups
+struct ShardServeParams;
+void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
+                               hipStream_t stream);
 
 }  // namespace rocfm

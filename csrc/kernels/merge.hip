@@ -1,6 +1,7 @@
 // Multi-source row-gradient merge by direct addressing — see merge.h.
 #include "merge.h"
 #include "wgrad_body.h"
+#include "shard_body.h"
 
 #include <algorithm>
 
@@ -405,28 +406,41 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   merged_row_out<KP4>(p, row, w, a, b, acc);
 }
 
+// Roles by workgroup: [merge apply | MLP optimizer | serve of the NEXT step's requests (bounded-
+// staleness row-shard mode: it reads rows this launch may be updating, Hogwild-style like the
+// reference's asynchronous parameter server)]
 template <int KP4, int WMAX>
 __global__ __launch_bounds__(kApplyThreads) void merge_search_apply_kernel(MergeParams p, DenseApplyParams d,
-                                                                           int n_apply, int n_dense) {
-  if ((int)blockIdx.x < n_apply) {
-    merge_search_body<KP4, WMAX>(p, blockIdx.x * kApplyThreads + threadIdx.x);
+                                                                           ShardServeParams sv, int n_apply,
+                                                                           int n_dense) {
+  const int b = blockIdx.x;
+  if (b < n_apply) {
+    merge_search_body<KP4, WMAX>(p, b * kApplyThreads + threadIdx.x);
+  } else if (b < n_apply + n_dense) {
+    dense_apply_body<kApplyThreads>(d, b - n_apply, n_dense);
   } else {
-    dense_apply_body<kApplyThreads>(d, blockIdx.x - n_apply, n_dense);
+    shard_serve_body(sv, (long long)(b - n_apply - n_dense) * kApplyThreads + threadIdx.x);
   }
 }
 
 template <int KP4>
-void launch_search_t(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+void launch_search_t(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
+                     hipStream_t stream) {
   const int n_apply = p.cap > 0 ? cdiv(p.W * p.cap, kApplyThreads) : 0;
   const int n_dense = d ? std::max(1, std::min(cdiv(d->n, kApplyThreads), 1024)) : 0;
+  const long long n_sv = sv ? (long long)sv->m * (sv->Kp / 4) : 0;
+  const int n_serve = (int)((n_sv + kApplyThreads - 1) / kApplyThreads);
   DenseApplyParams dd{};
   if (d) dd = *d;
-  if (n_apply + n_dense == 0) return;
-  const dim3 grid(n_apply + n_dense), block(kApplyThreads);
+  ShardServeParams ss{};
+  if (sv) ss = *sv;
+  if (n_apply + n_dense + n_serve == 0) return;
+  const dim3 grid(n_apply + n_dense + n_serve), block(kApplyThreads);
   if (p.W <= 8)
-    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, 8>), grid, block, 0, stream, p, dd, n_apply, n_dense);
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, 8>), grid, block, 0, stream, p, dd, ss, n_apply, n_dense);
   else
-    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p, dd, n_apply, n_dense);
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p, dd, ss, n_apply,
+                       n_dense);
 }
 
 template <int KP4>
@@ -480,16 +494,19 @@ void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d,
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
+                               hipStream_t stream) {
   ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge: 1 <= W <= 64");
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
   ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
   ROCFM_REQUIRE(p.key_div >= 1 && p.keys && p.rows && p.step, "merge: keys / rows / step missing");
   ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : p.emb != nullptr, "merge_search_apply: missing outputs");
+  ROCFM_REQUIRE(sv == nullptr || (sv->Kp % 4 == 0 && sv->Kp > 0 && sv->ids && sv->table),
+                "merge_search_apply: bad serve params");
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N)                    \
   case N:                               \
-    launch_search_t<N>(p, d, stream);   \
+    launch_search_t<N>(p, d, sv, stream); \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
     ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)

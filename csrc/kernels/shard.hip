@@ -9,6 +9,7 @@
 //                and the same indices in sorted order (input of the local gradient reduction)
 //   shard_serve  owner: requested ids → table rows (forward) and local row keys (update)
 #include "shard.h"
+#include "shard_body.h"
 
 #include <algorithm>
 
@@ -167,23 +168,7 @@ __global__ __launch_bounds__(kRT) void shard_route_assign_kernel(ShardRouteParam
 }
 
 __global__ __launch_bounds__(256) void shard_serve_kernel(ShardServeParams p) {
-  const int KP4 = p.Kp >> 2;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)p.m * KP4) return;
-  const int r = (int)(i / KP4), c = (int)(i - (long long)r * KP4);
-  const uint32_t id = p.ids[r];
-  const bool pad = id == kPad;
-  const uint32_t lr = id / (uint32_t)p.W;
-  const bool ok = !pad && (int)(id % (uint32_t)p.W) == p.rank && lr < p.Vs;
-  if (!pad && !ok && p.bad) *p.bad = 1;
-  if (p.rows_out) {
-    // load row 0 for requests this owner does not serve and zero the value: `ok ? load : 0`
-    // compiled to a select between a global and a private address (flat access + scratch)
-    float4 v = reinterpret_cast<const float4*>(p.table)[(size_t)(ok ? lr : 0u) * KP4 + c];
-    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    reinterpret_cast<float4*>(p.rows_out)[(size_t)r * KP4 + c] = v;
-  }
-  if (c == 0 && p.lkeys) p.lkeys[r] = ok ? lr : p.Vs;
+  shard_serve_body(p, (long long)blockIdx.x * 256 + threadIdx.x);
 }
 
 }  // namespace

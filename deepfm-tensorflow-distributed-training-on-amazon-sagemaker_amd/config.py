@@ -124,6 +124,9 @@ class Config:
     dist_timeout_s: int = 600
     watchdog_s: int = 0  # >0: dump stacks and exit(3) when no step completes for this long (§5.3)
     exchange_capacity: int = 0  # rows per rank (dp) / per owner (rowshard) in the exchange buffers; 0 = B*F (safe)
+    # rowshard: 0 = synchronous; 1 = bounded staleness (the reference's async PS, PS:461-521): a step's
+    # rows are served during the previous step's owner update (Hogwild-style reads; not bitwise reproducible)
+    ps_staleness: int = 0
     dp_exchange: str = "auto"  # dp / rowshard exchange transport: auto | p2p (IPC push over xGMI, one node) | rccl
 
     # ------------------------------------------------------------------------------------
@@ -146,6 +149,10 @@ class Config:
             raise ValueError("feature_size must be > 0")
         if self.embedding_size <= 0:
             raise ValueError("embedding_size must be > 0")
+        if self.ps_staleness not in (0, 1):
+            raise ValueError("ps_staleness must be 0 or 1")
+        if self.ps_staleness and self.parallelism != "rowshard":
+            raise ValueError("ps_staleness applies to parallelism=rowshard (the parameter-server equivalent)")
         if len(self.keep_probs) != len(self.layers):
             raise ValueError(
                 f"len(dropout)={len(self.keep_probs)} must equal len(deep_layers)={len(self.layers)}")

@@ -388,9 +388,18 @@ class FusedRowShard:
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
                  capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
-                 exchange: Optional[str] = None):
+                 exchange: Optional[str] = None, staleness: int = 0):
         from ..models.fused import FusedDeepFM
 
+        if staleness not in (0, 1):
+            raise ValueError(f"row-shard staleness must be 0 (synchronous) or 1, got {staleness}")
+        # staleness 1 (the reference's asynchronous PS, bounded): the rows of step k+1 are served
+        # in the same launch as step k's owner update, so a row updated at step k may be read
+        # before, during or after its update (Hogwild-style, not bitwise reproducible — as with
+        # TF's async PS); the MLP stays synchronous.  Every multi-step graph's first step is
+        # served after the previous update (staleness 0 there).
+        self.staleness = int(staleness)
+        self._pre_served = False
         W, r = _world_rank()
         self.W, self.rank = W, r
         self.V = spec.feature_size
@@ -451,17 +460,24 @@ class FusedRowShard:
         from .p2p import open_exchanges
 
         self.P = e.layout.total
-        exs = open_exchanges([cap, cap * Kp, cap * Kp, self.P], dev, exchange)
+        exs = open_exchanges([cap, cap * Kp, cap * Kp, self.P] + ([cap] if self.staleness else []), dev, exchange)
         self.exchange = "p2p" if exs else "rccl"
         self.p2p_x = {}
+        self.recv_pair = None  # staleness 1: request lists of consecutive steps (parity)
         if exs:
-            self.x_ids, self.x_rows, self.x_grad, self.x_mlp = exs
+            self.x_ids, self.x_rows, self.x_grad, self.x_mlp = exs[:4]
+            self.x_all = list(exs)
             self.recv_ids = self.x_ids.recv_tensor(torch.int32, (M,))
             self.recv_ids.fill_(PAD)
             self.rows_in = self.x_rows.recv_tensor(torch.float32, (M, Kp))
             self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
             for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
                 self.p2p_x[t.data_ptr()] = ex
+            if self.staleness:
+                r2 = exs[4].recv_tensor(torch.int32, (M,))
+                r2.fill_(PAD)
+                self.p2p_x[r2.data_ptr()] = exs[4]
+                self.recv_pair = [self.recv_ids, r2]
             self.graph_collectives = use_graph  # push kernels are capturable whatever the backend
         elif self.W == 1 and not self.force:
             # one rank: every exchange is the identity, so the receive side IS the send side (rows
@@ -474,6 +490,8 @@ class FusedRowShard:
             self.recv_ids = torch.full((M,), PAD, **i32)
             self.rows_in = torch.zeros(M, Kp, **f32)
             self.grad_back = torch.zeros(M, Kp, **f32)
+            if self.staleness:
+                self.recv_pair = [self.recv_ids, torch.full((M,), PAD, **i32)]
         self._p2p_params = {}
         # prediction routing (own buffers: never races the pipelined training route)
         self.pred_rsv = torch.zeros(n, **i32)
@@ -502,7 +520,7 @@ class FusedRowShard:
         e, H = self.eng, self.H
         self.route = [self._route_params(e.slot_ids[q], self.rsv[q], self.send_ids[q], self.local_idx[q], self.skl[q],
                                          self.counts[q], self.n) for q in range(2)]
-        self.serve = [self._serve_params(self._recv_ids_for(self.send_ids[p])) for p in range(2)]
+        self.serve = [self._serve_params(self._recv_ids_for(self.send_ids[p], p)) for p in range(2)]
         self.pred_serve = self._serve_params(self._recv_ids_for(self.pred_send))
         self.owner_params = []
         for p in range(2):
@@ -513,7 +531,7 @@ class FusedRowShard:
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
             lp.touched = 0  # writes the exchange stage, not the table's gradient rows
             op = H.MergeParams()  # owner: Σ over source ranks per local row → optimizer
-            op.keys, op.key_stride = self._recv_ids_for(self.send_ids[p]).data_ptr(), self.cap
+            op.keys, op.key_stride = self._recv_ids_for(self.send_ids[p], p).data_ptr(), self.cap
             op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
@@ -538,9 +556,16 @@ class FusedRowShard:
         self.pred_route = self._route_params(e.pred_ids, self.pred_rsv, self.pred_send, self.pred_local,
                                              self.pred_skl, self.pred_counts, self.n)
 
-    def _recv_ids_for(self, send: torch.Tensor) -> torch.Tensor:
+    def _recv(self, parity: int = 0) -> Optional[torch.Tensor]:
+        """X1 receive buffer of a step of this parity (None: world 1, the send list is read)."""
+        if self.recv_ids is None:
+            return None
+        return self.recv_pair[parity] if self.recv_pair is not None else self.recv_ids
+
+    def _recv_ids_for(self, send: torch.Tensor, parity: int = 0) -> torch.Tensor:
         """The request list an owner reads after exchanging ``send`` (world 1: ``send`` itself)."""
-        return send if self.recv_ids is None else self.recv_ids
+        r = self._recv(parity)
+        return send if r is None else r
 
     def _serve_params(self, ids: torch.Tensor):
         e = self.eng
@@ -554,12 +579,14 @@ class FusedRowShard:
     def attach_pool(self, ids, vals, labels, start: int = 0):
         self.eng.attach_pool(ids, vals, labels, start)
         self._graphs = {}
+        self._pre_served = False
 
     def push_batch(self, ids, vals, labels):
         self.eng.push_batch(ids, vals, labels)
 
     def load_batch(self, ids, vals, labels=None):
         self.eng.load_batch(ids, vals, labels)
+        self._pre_served = False
 
     def set_lr_scale(self, s: float) -> None:
         e = self.eng
@@ -670,6 +697,9 @@ class FusedRowShard:
 
     def _step_body(self, p: int) -> None:
         e = self.eng
+        if self.staleness:
+            self._step_body_stale(p, serve_first=not self._pre_served)
+            return
         side = self._fork_next(p)  # next batch's fetch + route overlaps the whole step
         self._exchange(self.recv_ids, self.send_ids[p])                        # X1 requests
         self._phase_serve(p)
@@ -680,13 +710,38 @@ class FusedRowShard:
         self._phase_update(p)
         e._join(side)
 
+    def _step_body_stale(self, p: int, serve_first: bool) -> None:
+        """Staleness 1: this step's rows were served by the previous step's update launch (unless
+        ``serve_first``); the next batch is routed on the side chain during the compute and its
+        rows are served by this step's update launch."""
+        e, H = self.eng, self.H
+        if serve_first:
+            self._exchange(self._recv(p), self.send_ids[p])                     # X1 requests
+            self._phase_serve(p)
+            self._exchange(self.rows_in, self.rows_out)                         # X2 rows
+        self._phase_compute(p, with_side=True)  # joins the side chain: batch 1-p is routed
+        self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
+        self._allreduce_mlp()                                                   # X4 MLP grads
+        self._exchange(self._recv(1 - p), self.send_ids[1 - p])                 # X1 of the next step
+        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], e.stream_ptr, self.serve[1 - p])
+        if self.embedding_update == "exact":
+            H.emb_dense_update(e.emb_dense_params[p], e.stream_ptr)
+        self._exchange(self.rows_in, self.rows_out)                             # X2 of the next step
+
     def train_step(self) -> None:
         e = self.eng
         e._m_primed = False
         if not e._primed:
             self.prime()
         p = e._i % 2
-        if self.graph_collectives:  # one graph per step, collectives included
+        if self.staleness:
+            first = not self._pre_served
+            if self.graph_collectives:
+                self._run(("stale", p, first), lambda: self._step_body_stale(p, first), collectives=True)
+            else:
+                self._step_body_stale(p, first)
+            self._pre_served = True
+        elif self.graph_collectives:  # one graph per step, collectives included
             self._run(("step", p), lambda: self._step_body(p), collectives=True)
         else:
             self._exchange(self.recv_ids, self.send_ids[p])
@@ -716,6 +771,10 @@ class FusedRowShard:
         if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
             self._train_steps_multi(n, steps_per_graph)
             return
+        if self.staleness:
+            for _ in range(n):
+                self.train_step()
+            return
         S = max(2, steps_per_graph // 2 * 2)
         while n > 0:
             if (self.graph_collectives and self.use_graph and self._warm >= 4 and e._primed and n >= S
@@ -744,9 +803,9 @@ class FusedRowShard:
         torch.cuda.synchronize(self.device)
         self._graphs = {}
         if self.exchange == "p2p":
-            self.recv_ids = self.rows_in = self.grad_back = None  # views of the buffers freed below
+            self.recv_ids = self.rows_in = self.grad_back = self.recv_pair = None  # views of the buffers freed below
             self.p2p_x = {}
-            for ex in (self.x_ids, self.x_rows, self.x_grad, self.x_mlp):
+            for ex in self.x_all:
                 ex.close()
             self.exchange = "closed"
 
@@ -797,10 +856,11 @@ class FusedRowShard:
                           "dense_grad", "touched"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
-                mg.keys = self._recv_ids_for(self.ms_send[q, k]).data_ptr()
+                par = k % 2 if self.staleness else 0
+                mg.keys = self._recv_ids_for(self.ms_send[q, k], par).data_ptr()
                 if ed is not None:
                     ed.grad_scale = 1.0
-                steps.append((rows, wp, ep, da, ed, mg, self._serve_params(self._recv_ids_for(self.ms_send[q, k]))))
+                steps.append((rows, wp, ep, da, ed, mg, self._serve_params(self._recv_ids_for(self.ms_send[q, k], par))))
             self.ms_route.append(routes)
             self.ms_steps.append(steps)
 
@@ -816,15 +876,25 @@ class FusedRowShard:
         FusedDeepFM._launch_multi)."""
         e, H = self.eng, self.H
         s = torch.cuda.current_stream(self.device).cuda_stream
+        st = self.staleness
         for k in range(S):
             rows, wp, ep, da, ed, mg, sv = self.ms_steps[q][k]
-            self._exchange(self.recv_ids, self.ms_send[q, k])                   # X1 requests
-            H.shard_serve(sv, s)
-            self._exchange(self.rows_in, self.rows_out)                         # X2 rows
+            par = k % 2 if st else 0
+            if k == 0 or not st:  # (staleness 1: later steps were served by the previous update)
+                self._exchange(self._recv(par), self.ms_send[q, k])             # X1 requests
+                H.shard_serve(sv, s)
+                self._exchange(self.rows_in, self.rows_out)                     # X2 rows
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
             self._allreduce_mlp()                                               # X4 MLP grads
+            if st and k + 1 < S:  # owner merge ‖ MLP opt ‖ serve of step k+1
+                self._exchange(self._recv(1 - par), self.ms_send[q, k + 1])     # X1 of step k+1
+                H.merge_search_apply(mg, da, s, self.ms_steps[q][k + 1][6])
+                if ed is not None:
+                    H.emb_dense_update(ed, s)
+                self._exchange(self.rows_in, self.rows_out)                     # X2 of step k+1
+                continue
             H.merge_search_apply(mg, da, s)                                     # owner merge ‖ MLP opt
             if ed is not None:
                 H.emb_dense_update(ed, s)
@@ -842,6 +912,7 @@ class FusedRowShard:
             self._after_steps(e._i - S, e._i)
         torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
         e._primed = False
+        self._pre_served = False
 
     def train_on(self, batches):
         it = iter(batches)
@@ -870,13 +941,14 @@ class FusedRowShard:
                                f"rebuild with capacity >= {c} (or capacity=batch_size*field_size)")
         if bad:
             raise RuntimeError("row-shard routing error: a rank received ids it does not own")
-        if self.exchange == "p2p" and any(x.errored() for x in (self.x_ids, self.x_rows, self.x_grad, self.x_mlp)):
+        if self.exchange == "p2p" and any(x.errored() for x in self.x_all):
             raise RuntimeError("row-shard p2p exchange: a peer wait timed out (rank missing or stalled)")
 
     # ---- inference (collective) ------------------------------------------------------------------
     @torch.no_grad()
     def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
         e = self.eng
+        self._pre_served = False  # the prediction reuses the serve / row buffers
         nrows = int(ids.shape[0])
         nch = max(1, (nrows + e.B - 1) // e.B)
         if self.W > 1:
@@ -943,6 +1015,7 @@ class FusedRowShard:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
+        self._pre_served = False
         self._graphs = {}
         self._warm = 0
 
