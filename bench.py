@@ -68,6 +68,8 @@ def parse():
                     help="rows per rank (dp) / per owner (rowshard) in the exchange buffers: 'auto' = the exact max "
                          "over the batch pool, 'safe' = batch_size*field_size (never overflows), or a number")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--hot_rows", type=int, default=0,
+                    help="rowshard: replicate the N most frequent ids on every rank (gradients ride the MLP bucket)")
     ap.add_argument("--ps_staleness", type=int, default=0, choices=[0, 1],
                     help="rowshard: 1 = bounded-staleness (async-PS) row serving, 0 = synchronous")
     ap.add_argument("--input", default="pool", choices=["pool", "tfrecord"],
@@ -159,7 +161,7 @@ def main():
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
                                 use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype,
-                                exchange=a.dp_exchange, staleness=a.ps_staleness)
+                                exchange=a.dp_exchange, staleness=a.ps_staleness, hot_rows=a.hot_rows)
         elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 
@@ -252,6 +254,7 @@ def main():
             "embedding_update": a.embedding_update,
             "exchange_capacity": cap,
             "ps_staleness": a.ps_staleness if parallelism == "rowshard" else None,
+            "hot_rows": a.hot_rows if parallelism == "rowshard" else None,
             "exchange": getattr(eng, "exchange", None) if pg else None,
         },
         "world_size": dist.get_world_size() if pg else 1,

@@ -57,6 +57,8 @@ struct FetchMultiParams {
                                // keys — vocabularies too wide for S << id_bits to fit 32 bits
   int shard_W;      // > 0: keys are owner-major row-shard keys (id % W)·Vs + id / W (shard.hip)
   uint32_t shard_Vs;
+  const uint32_t* shard_hot;  // replicated ids (ascending; shard_key in shard.h), nullable
+  int shard_nhot;
   int64_t* steps;   // [S] global_step of each prepared step
   float* lrt;       // [S] lr_t of each prepared step
   float lr, beta1, beta2;

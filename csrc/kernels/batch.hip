@@ -7,6 +7,7 @@
 // the sort orders batch i+1 while step i trains) and never writes a word the concurrent step
 // reads: it reads cursor[p]/step[p] and writes cursor[1-p]/step[1-p].
 #include "batch.h"
+#include "shard.h"
 
 namespace rocfm {
 
@@ -87,7 +88,8 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
     dv[i] = sv[i];
     if (dk || dk64) {
       const uint32_t u = (uint32_t)id;
-      const uint32_t key = p.shard_W > 0 ? (u % (uint32_t)p.shard_W) * p.shard_Vs + u / (uint32_t)p.shard_W : u;
+      const uint32_t key =
+          p.shard_W > 0 ? shard_key(u, (uint32_t)p.shard_W, p.shard_Vs, p.shard_hot, p.shard_nhot) : u;
       if (dk64)
         dk64[i] = kb64 | key;
       else

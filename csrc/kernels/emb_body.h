@@ -256,6 +256,12 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
           if (u4 == 0) p.out_keys[slot] = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
         }
       } else if (p.mode == 1) {
+        const uint32_t rr = (uint32_t)(idx4[u] / KP4);
+        if (p.hot_out != nullptr && rr >= p.hot_base) {  // replicated row → the X4 bucket
+          reinterpret_cast<float4*>(p.hot_out)[(size_t)(rr - p.hot_base) * KP4 + u4] = g[u];
+          if (u4 == 0) p.hot_out[(size_t)p.n_hot * KP4 * 4 + (rr - p.hot_base)] = 1.f;
+          continue;
+        }
         reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];
         if (p.touched && u4 == 0) p.touched[idx4[u] / KP4] = (uint32_t)*p.step + 1u;
       } else {

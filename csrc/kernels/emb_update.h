@@ -40,6 +40,11 @@ struct EmbUpdateParams {
   // deterministic — and workgroup 0 stores the total count (no atomics; out_count need not be zeroed)
   const int32_t* chunk_heads;
   int nch;  // chunks of this batch (entries of chunk_heads)
+  // mode 1 (nullable): rows >= hot_base are replicated rows (row-shard hot replication); their sums
+  // go to hot_out[(row − hot_base)·Kp] and a 1 to hot_out[n_hot·Kp + row − hot_base] (the X4 bucket)
+  float* hot_out;
+  uint32_t hot_base;
+  int n_hot;
 };
 
 struct EmbDenseParams {

@@ -68,10 +68,27 @@ void launch_merge_apply(const MergeParams& p, hipStream_t stream);
 void launch_merge_init(const MergeParams& p, hipStream_t stream);  // pos = −1, rep = W
 struct DenseApplyParams;
 void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d, hipStream_t stream);
+// Row-shard hot-row replication: every rank applies the same update to its replica of the
+// replicated rows from the X4 bucket's hot part (per rank: [H·Kp gradient sums | H touched flags]).
+struct HotApplyParams {
+  float* rows;            // [H][Kp] replica (the received-rows buffer behind the W owner segments)
+  float* s0;              // [H][Kp] optimizer slots (nullable)
+  float* s1;
+  const float* grads;     // segment r at grads + r·seg_stride: [H·Kp | H]
+  int nseg;               // 1: already summed (all-reduce); W: rank segments summed in rank order
+  long long seg_stride;   // floats
+  float* zero;            // nullable: this rank's bucket part, cleared after it is read
+  int H, Kp, K1;
+  float l2, grad_scale;
+  OptParams opt;
+  const int64_t* step;
+  int dense;              // 1 (exact): every replicated row is updated (g = λ·θ when untouched)
+};
+
 // search mode; d (nullable): the MLP optimizer launched as extra workgroups; sv (nullable): a
-// row-shard serve (shard.h) as further workgroups
+// row-shard serve (shard.h) as further workgroups; hot (nullable): the replicated rows' update
 struct ShardServeParams;
 void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
-                               hipStream_t stream);
+                               const HotApplyParams* hot, hipStream_t stream);
 
 }  // namespace rocfm

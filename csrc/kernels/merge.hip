@@ -406,26 +406,68 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   merged_row_out<KP4>(p, row, w, a, b, acc);
 }
 
+// One thread per (replicated row, float4 column): Σ of the rank segments in rank order (the
+// owner merge's order, so replicated and owned rows take bit-identical updates), then the row
+// optimizer on the replica; the bucket part is cleared for the next step.
+template <int KP4>
+__device__ __forceinline__ void hot_apply_body(const HotApplyParams& h, const int i) {
+  if (i >= h.H * KP4) return;
+  const int r = i / KP4, c = i - r * KP4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float cnt = 0.f;
+  for (int q = 0; q < h.nseg; ++q) {
+    const float* seg = h.grads + (size_t)q * h.seg_stride;
+    acc = f4add_m(acc, reinterpret_cast<const float4*>(seg)[(size_t)r * KP4 + c]);
+    cnt += seg[(size_t)h.H * KP4 * 4 + r];
+  }
+  if (h.zero) {
+    reinterpret_cast<float4*>(h.zero)[(size_t)r * KP4 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c == 0) h.zero[(size_t)h.H * KP4 * 4 + r] = 0.f;
+  }
+  const bool has = cnt > 0.f;
+  if (!has && !h.dense) return;
+  const size_t at = (size_t)r * KP4 + c;
+  float4 w = reinterpret_cast<const float4*>(h.rows)[at];
+  float4 a = h.s0 ? reinterpret_cast<const float4*>(h.s0)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 b = h.s1 ? reinterpret_cast<const float4*>(h.s1)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const OptStep st = opt_step(h.opt, *h.step);
+  float* wc = &w.x;
+  float* ac = &a.x;
+  float* bc = &b.x;
+  const float* gc = &acc.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (c * 4 + u >= h.K1) continue;
+    const float g = has ? gc[u] * h.grad_scale : 0.f;
+    opt_apply(h.opt, st, wc[u], g + h.l2 * wc[u], ac[u], bc[u]);
+  }
+  reinterpret_cast<float4*>(h.rows)[at] = w;
+  if (h.s0) reinterpret_cast<float4*>(h.s0)[at] = a;
+  if (h.s1) reinterpret_cast<float4*>(h.s1)[at] = b;
+}
+
 // Roles by workgroup: [merge apply | MLP optimizer | serve of the NEXT step's requests (bounded-
 // staleness row-shard mode: it reads rows this launch may be updating, Hogwild-style like the
-// reference's asynchronous parameter server)]
+// reference's asynchronous parameter server) | replicated-row update]
 template <int KP4, int WMAX>
 __global__ __launch_bounds__(kApplyThreads) void merge_search_apply_kernel(MergeParams p, DenseApplyParams d,
-                                                                           ShardServeParams sv, int n_apply,
-                                                                           int n_dense) {
+                                                                           ShardServeParams sv, HotApplyParams hot,
+                                                                           int n_apply, int n_dense, int n_serve) {
   const int b = blockIdx.x;
   if (b < n_apply) {
     merge_search_body<KP4, WMAX>(p, b * kApplyThreads + threadIdx.x);
   } else if (b < n_apply + n_dense) {
     dense_apply_body<kApplyThreads>(d, b - n_apply, n_dense);
-  } else {
+  } else if (b < n_apply + n_dense + n_serve) {
     shard_serve_body(sv, (long long)(b - n_apply - n_dense) * kApplyThreads + threadIdx.x);
+  } else {
+    hot_apply_body<KP4>(hot, (b - n_apply - n_dense - n_serve) * kApplyThreads + threadIdx.x);
   }
 }
 
 template <int KP4>
 void launch_search_t(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
-                     hipStream_t stream) {
+                     const HotApplyParams* hot, hipStream_t stream) {
   const int n_apply = p.cap > 0 ? cdiv(p.W * p.cap, kApplyThreads) : 0;
   const int n_dense = d ? std::max(1, std::min(cdiv(d->n, kApplyThreads), 1024)) : 0;
   const long long n_sv = sv ? (long long)sv->m * (sv->Kp / 4) : 0;
@@ -434,13 +476,17 @@ void launch_search_t(const MergeParams& p, const DenseApplyParams* d, const Shar
   if (d) dd = *d;
   ShardServeParams ss{};
   if (sv) ss = *sv;
-  if (n_apply + n_dense + n_serve == 0) return;
-  const dim3 grid(n_apply + n_dense + n_serve), block(kApplyThreads);
+  HotApplyParams hh{};
+  if (hot) hh = *hot;
+  const int n_hot = hot ? cdiv(hot->H * KP4, kApplyThreads) : 0;
+  if (n_apply + n_dense + n_serve + n_hot == 0) return;
+  const dim3 grid(n_apply + n_dense + n_serve + n_hot), block(kApplyThreads);
   if (p.W <= 8)
-    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, 8>), grid, block, 0, stream, p, dd, ss, n_apply, n_dense);
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, 8>), grid, block, 0, stream, p, dd, ss, hh, n_apply, n_dense,
+                       n_serve);
   else
-    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p, dd, ss, n_apply,
-                       n_dense);
+    hipLaunchKernelGGL((merge_search_apply_kernel<KP4, kMaxW>), grid, block, 0, stream, p, dd, ss, hh, n_apply,
+                       n_dense, n_serve);
 }
 
 template <int KP4>
@@ -495,7 +541,7 @@ void launch_merge_scatter_dense(const MergeParams& p, const DenseApplyParams& d,
 }
 
 void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
-                               hipStream_t stream) {
+                               const HotApplyParams* hot, hipStream_t stream) {
   ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge: 1 <= W <= 64");
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
   ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
@@ -503,10 +549,13 @@ void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, 
   ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : p.emb != nullptr, "merge_search_apply: missing outputs");
   ROCFM_REQUIRE(sv == nullptr || (sv->Kp % 4 == 0 && sv->Kp > 0 && sv->ids && sv->table),
                 "merge_search_apply: bad serve params");
+  ROCFM_REQUIRE(hot == nullptr || (hot->Kp == p.Kp && hot->H > 0 && hot->rows && hot->grads && hot->step &&
+                                   hot->nseg >= 1 && hot->K1 <= hot->Kp),
+                "merge_search_apply: bad hot-row params");
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N)                    \
   case N:                               \
-    launch_search_t<N>(p, d, sv, stream); \
+    launch_search_t<N>(p, d, sv, hot, stream); \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
     ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)

@@ -14,7 +14,28 @@ struct ShardKeysParams {
   int W;
   uint32_t Vs;         // rows per shard (ceil(V / W))
   uint32_t* keys;      // [n] owner-major keys
+  const uint32_t* hot_ids;  // [n_hot] ascending replicated ("hot") ids (nullable)
+  int n_hot;
 };
+
+// Hot-row replication: the n_hot replicated ids form a virtual owner W (key W·Vs + slot) — sorted
+// after every real owner, never requested from anyone; their lookups read the local replica.
+__device__ __forceinline__ uint32_t shard_key(uint32_t id, uint32_t W, uint32_t Vs, const uint32_t* hot, int nhot) {
+  if (nhot > 0) {
+    int lo = 0, len = nhot;
+    while (len > 0) {
+      const int h = len >> 1;
+      if (hot[lo + h] < id) {
+        lo += h + 1;
+        len -= h + 1;
+      } else {
+        len = h;
+      }
+    }
+    if (lo < nhot && hot[lo] == id) return W * Vs + (uint32_t)lo;
+  }
+  return (id % W) * Vs + id / W;
+}
 
 // From the sorted (key', lookup) pairs of one batch: the unique ids each owner must serve, and for
 // every lookup the row of the received-rows buffer ([W][cap][Kp]) that will hold its embedding.
@@ -27,6 +48,7 @@ struct ShardRouteParams {
   int cap;                // per-owner capacity of the exchange buffers
   uint32_t* send_ids;     // [W][cap] global ids requested from each owner; 0xFFFFFFFF = padding
   int32_t* local_idx;     // [>= n] lookup order: row (o * cap + j) of the received-rows buffer
+                          //   (hot ids, virtual owner W: row W·cap + slot, the local replica)
   uint32_t* skeys_local;  // [n] sorted order: the same rows (input of the local gradient reduction)
   int32_t* counts;        // [W] unique ids per owner this batch (> cap means overflow)
   int32_t* overflow;      // sticky flag: set to 1 when any owner needs more than cap rows

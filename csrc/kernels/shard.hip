@@ -54,8 +54,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int& total) {
 __global__ __launch_bounds__(256) void shard_keys_kernel(ShardKeysParams p) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= p.n) return;
-  const uint32_t id = (uint32_t)p.ids[i];
-  p.keys[i] = (id % (uint32_t)p.W) * p.Vs + id / (uint32_t)p.W;
+  p.keys[i] = shard_key((uint32_t)p.ids[i], (uint32_t)p.W, p.Vs, p.hot_ids, p.n_hot);
 }
 
 // Multi-workgroup routing of the sorted (key', lookup) pairs (tile = 1024 entries per workgroup).
@@ -87,9 +86,9 @@ __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams
   for (int u = 0; u < kRI; ++u) {
     if (i0 + u < p.n && k[u] != prev) {
       ++heads;
-      const int o = (int)(k[u] / p.Vs);
+      const int o = min((int)(k[u] / p.Vs), p.W);  // W: replicated rows (not counted)
       if (o != cur_o) {
-        if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
+        if (cur_c && cur_o < p.W) atomicAdd(&s_cnt[cur_o], cur_c);
         cur_o = o;
         cur_c = 0;
       }
@@ -97,7 +96,7 @@ __global__ __launch_bounds__(kRT) void shard_route_count_kernel(ShardRouteParams
     }
     if (i0 + u < p.n) prev = k[u];
   }
-  if (cur_c) atomicAdd(&s_cnt[cur_o], cur_c);
+  if (cur_c && cur_o < p.W) atomicAdd(&s_cnt[cur_o], cur_c);
   int total;
   block_excl_scan(heads, s_w, total);  // (its barriers also order the LDS count adds)
   if (t == 0) p.scratch[blockIdx.x] = total;
@@ -153,6 +152,12 @@ __global__ __launch_bounds__(kRT) void shard_route_assign_kernel(ShardRouteParam
     prev = k[u];
     urun += head ? 1 : 0;
     const int o = (int)(k[u] / p.Vs);
+    if (o >= W) {  // replicated row: the local replica behind the W owner segments
+      const uint32_t lk = (uint32_t)W * (uint32_t)p.cap + (k[u] - (uint32_t)W * p.Vs);
+      p.skeys_local[i0 + u] = lk;
+      p.local_idx[v[u]] = (int32_t)lk;
+      continue;
+    }
     const int j = urun - s_first[o];
     const uint32_t lk = (uint32_t)o * (uint32_t)p.cap + (uint32_t)min(j, p.cap - 1);
     p.skeys_local[i0 + u] = lk;
@@ -174,14 +179,16 @@ __global__ __launch_bounds__(256) void shard_serve_kernel(ShardServeParams p) {
 }  // namespace
 
 void launch_shard_keys(const ShardKeysParams& p, hipStream_t stream) {
-  ROCFM_REQUIRE(p.W >= 1 && (unsigned long long)p.W * p.Vs < 0xFFFFFFFFull, "shard_keys: W*Vs must fit in 32 bits");
+  ROCFM_REQUIRE(p.W >= 1 && (unsigned long long)(p.W + (p.n_hot > 0)) * p.Vs < 0xFFFFFFFFull,
+                "shard_keys: (W + hot) * Vs must fit in 32 bits");
+  ROCFM_REQUIRE(p.n_hot == 0 || (p.hot_ids != nullptr && (uint32_t)p.n_hot <= p.Vs), "shard_keys: hot ids");
   if (p.n <= 0) return;
   hipLaunchKernelGGL(shard_keys_kernel, dim3(cdiv(p.n, 256)), dim3(256), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_shard_route(const ShardRouteParams& p, hipStream_t stream) {
-  ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxOwners, "shard_route: 1 <= world <= 1024");
+  ROCFM_REQUIRE(p.W >= 1 && p.W < kMaxOwners, "shard_route: 1 <= world < 1024");
   ROCFM_REQUIRE(p.cap >= 1, "shard_route: capacity must be positive");
   ROCFM_REQUIRE((unsigned long long)p.W * p.cap < (1ull << 31), "shard_route: W*cap overflows int32");
   ROCFM_REQUIRE(p.scratch != nullptr, "shard_route: scratch (>= route_scratch_ints(n)) required");

@@ -127,6 +127,9 @@ class Config:
     # rowshard: 0 = synchronous; 1 = bounded staleness (the reference's async PS, PS:461-521): a step's
     # rows are served during the previous step's owner update (Hogwild-style reads; not bitwise reproducible)
     ps_staleness: int = 0
+    # rowshard: replicate the N most frequent ids (rank 0's first batches) on every rank; their
+    # gradients ride the MLP all-reduce bucket (synchronous, same update as their owners would apply)
+    hot_rows: int = 0
     dp_exchange: str = "auto"  # dp / rowshard exchange transport: auto | p2p (IPC push over xGMI, one node) | rccl
 
     # ------------------------------------------------------------------------------------
@@ -149,6 +152,8 @@ class Config:
             raise ValueError("feature_size must be > 0")
         if self.embedding_size <= 0:
             raise ValueError("embedding_size must be > 0")
+        if self.hot_rows < 0 or (self.hot_rows and self.parallelism != "rowshard"):
+            raise ValueError("hot_rows (>= 0) applies to parallelism=rowshard")
         if self.ps_staleness not in (0, 1):
             raise ValueError("ps_staleness must be 0 or 1")
         if self.ps_staleness and self.parallelism != "rowshard":

@@ -101,7 +101,8 @@ class Estimator:
                 return FusedRowShard(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                      embedding_update=cfg.embedding_update, seed=cfg.seed,
                                      use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,
-                                     exchange=cfg.dp_exchange, staleness=cfg.ps_staleness)
+                                     exchange=cfg.dp_exchange, staleness=cfg.ps_staleness,
+                                     hot_rows=cfg.hot_rows)
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
                                  seed=cfg.seed)
         if self.engine_name == "fused":

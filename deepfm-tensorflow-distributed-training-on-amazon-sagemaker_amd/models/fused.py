@@ -493,8 +493,10 @@ class FusedDeepFM:
             f.lr = self.hp.lr * self.lr_scale
         self._graphs = [None, None]
         self._primed = False
-        if getattr(self, "mS", None) is not None:
-            self._build_multi(self.mS, getattr(self, "_m_shard", None))  # rebuild with the new lr
+        # the multi-step parameter blocks carry the lr: the next train_steps rebuilds them (through
+        # the wrapper that built them — DP / row-shard add their own blocks on top)
+        self._m_pool = None
+        self._m_primed = False
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -630,7 +632,7 @@ class FusedDeepFM:
         2^26 rows at S = 64); wider vocabularies (100M-1B rows) keep S and sort 64-bit composite
         keys, whose ids the side chain then hands on as plain per-batch 32-bit keys
         (``m_composite`` False)."""
-        key_range = self.V if shard is None else shard[0] * shard[1]
+        key_range = self.V if shard is None else (shard[0] + (len(shard) > 2)) * shard[1]  # + hot owner
         idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
         return idbits, max(1, int(Smax))
 
@@ -640,7 +642,7 @@ class FusedDeepFM:
         export places each chunk's rows from them)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
-        self._m_shard = shard
+        self._m_shard = shard  # (W, Vs) or (W, Vs, hot ids tensor)
         self.m_req = int(Smax)
         idbits, Smax = self._multi_S(Smax, shard)
         sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
@@ -705,7 +707,9 @@ class FusedDeepFM:
         if not self.m_composite:
             f.keys, f.keys64 = 0, self.m_keys64[0].data_ptr()
         if getattr(self, "_m_shard", None) is not None:
-            f.shard_W, f.shard_Vs = self._m_shard
+            f.shard_W, f.shard_Vs = self._m_shard[:2]
+            if len(self._m_shard) > 2:  # replicated (hot) ids: the virtual owner W
+                f.shard_hot, f.shard_nhot = self._m_shard[2].data_ptr(), self._m_shard[2].numel()
         f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
         f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
         f.opt_type = OPT_ID[self.hp.name]

@@ -388,7 +388,7 @@ class FusedRowShard:
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
                  capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
-                 exchange: Optional[str] = None, staleness: int = 0):
+                 exchange: Optional[str] = None, staleness: int = 0, hot_rows: int = 0):
         from ..models.fused import FusedDeepFM
 
         if staleness not in (0, 1):
@@ -400,6 +400,13 @@ class FusedRowShard:
         # served after the previous update (staleness 0 there).
         self.staleness = int(staleness)
         self._pre_served = False
+        # hot-row replication (SURVEY §2.6 hybrid): the hot_rows most frequent ids (chosen from rank
+        # 0's first batches, or set_hot_ids) are replicated on every rank — looked up locally, never
+        # routed; their per-rank gradient sums ride the X4 MLP bucket and every rank applies the
+        # same (synchronous, rank-order) update to its replica.  The owners' copies are refreshed
+        # from the replica whenever the table is read outside training (_flush_hot).
+        self.NH = max(0, int(hot_rows))
+        self.hot_ids = None  # [n_hot] ascending global ids (int32 storage of uint32), once chosen
         W, r = _world_rank()
         self.W, self.rank = W, r
         self.V = spec.feature_size
@@ -438,7 +445,7 @@ class FusedRowShard:
         self.M = M
         i32 = dict(dtype=torch.int32, device=dev)
         # ---- routing buffers (parity q = the step that will consume them) ----
-        self.route_bits = max(1, math.ceil(math.log2(max(W * Vs, 2))))
+        self.route_bits = max(1, math.ceil(math.log2(max((W + (self.NH > 0)) * Vs, 2))))
         self.rkeys = torch.zeros(n, **i32)
         self.rsk = torch.zeros(n, **i32)
         self.rsv = [torch.zeros(n, **i32) for _ in range(2)]
@@ -453,14 +460,21 @@ class FusedRowShard:
                                       device=dev)
         # ---- exchange buffers ----
         f32 = dict(dtype=torch.float32, device=dev)
-        self.rows_out = torch.zeros(M, Kp, **f32)
+        NH = self.NH
+        # rows_in = [W·cap received rows | NH replicated rows] (the row kernel's table)
+        self.rows_out = torch.zeros(M + (NH if W == 1 and not self.force else 0), Kp, **f32)
         self.grad_stage = torch.zeros(M, Kp, **f32)
         # X1-X3 all-to-all and X4 MLP all-reduce: one-shot push over IPC-mapped peer buffers on one
         # node (rocfm.parallel.p2p; the receive buffers ARE the peer-mapped slots), else RCCL
         from .p2p import open_exchanges
 
         self.P = e.layout.total
-        exs = open_exchanges([cap, cap * Kp, cap * Kp, self.P] + ([cap] if self.staleness else []), dev, exchange)
+        # X4 bucket: [MLP grads P | NH·Kp replicated-row gradient sums | NH touched flags]
+        self.PX = (self.P + NH * (Kp + 1) + 3) // 4 * 4
+        self.mlp_bucket = torch.zeros(self.PX, **f32)
+        e.dense_grads_flat = self.mlp_bucket[:self.P]
+        slots = [cap, cap * Kp, cap * Kp, self.PX] + ([cap] if self.staleness else [])
+        exs = open_exchanges(slots, dev, exchange, extra_floats=[0, NH * Kp] + [0] * (len(slots) - 2))
         self.exchange = "p2p" if exs else "rccl"
         self.p2p_x = {}
         self.recv_pair = None  # staleness 1: request lists of consecutive steps (parity)
@@ -469,7 +483,7 @@ class FusedRowShard:
             self.x_all = list(exs)
             self.recv_ids = self.x_ids.recv_tensor(torch.int32, (M,))
             self.recv_ids.fill_(PAD)
-            self.rows_in = self.x_rows.recv_tensor(torch.float32, (M, Kp))
+            self.rows_in = self.x_rows.recv_tensor(torch.float32, (M + NH, Kp))
             self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
             for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
                 self.p2p_x[t.data_ptr()] = ex
@@ -488,11 +502,16 @@ class FusedRowShard:
             self.grad_back = self.grad_stage
         else:
             self.recv_ids = torch.full((M,), PAD, **i32)
-            self.rows_in = torch.zeros(M, Kp, **f32)
+            self.rows_in = torch.zeros(M + NH, Kp, **f32)
             self.grad_back = torch.zeros(M, Kp, **f32)
             if self.staleness:
                 self.recv_pair = [self.recv_ids, torch.full((M,), PAD, **i32)]
         self._p2p_params = {}
+        self.rows_x = self.rows_in[:M]  # the X2 all-to-all part of rows_in
+        self.hot_rep = self.rows_in[M:]  # the replica
+        self.hot_slots = [torch.zeros(NH, Kp, **f32) for _ in e.emb_slots] if NH else []
+        self.hot_ids_dev = torch.full((max(NH, 1),), PAD, **i32)
+        self.n_hot = 0
         # prediction routing (own buffers: never races the pipelined training route)
         self.pred_rsv = torch.zeros(n, **i32)
         self.pred_send = torch.full((M,), PAD, **i32)
@@ -508,6 +527,7 @@ class FusedRowShard:
         H = self.H
         kp = H.ShardKeysParams()
         kp.ids, kp.n, kp.W, kp.Vs, kp.keys = ids.data_ptr(), n, self.W, self.Vs, self.rkeys.data_ptr()
+        kp.hot_ids, kp.n_hot = self.hot_ids_dev.data_ptr(), self.n_hot
         rp = H.ShardRouteParams()
         rp.skeys, rp.svals, rp.n = self.rsk.data_ptr(), rsv.data_ptr(), n
         rp.W, rp.Vs, rp.cap = self.W, self.Vs, self.cap
@@ -530,6 +550,7 @@ class FusedRowShard:
             lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
             lp.touched = 0  # writes the exchange stage, not the table's gradient rows
+            self._bind_hot_out(lp)
             op = H.MergeParams()  # owner: Σ over source ranks per local row → optimizer
             op.keys, op.key_stride = self._recv_ids_for(self.send_ids[p], p).data_ptr(), self.cap
             op.rows, op.row_stride = self.grad_back.data_ptr(), self.cap * e.Kp
@@ -555,6 +576,113 @@ class FusedRowShard:
         pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
         self.pred_route = self._route_params(e.pred_ids, self.pred_rsv, self.pred_send, self.pred_local,
                                              self.pred_skl, self.pred_counts, self.n)
+        self.pred_route[0].n_hot = 0  # predictions read the owners' (flushed) rows
+        self.hot_params = [self._hot_params(lp_, self.owner_params[p].opt, self.owner_params[p].step)
+                           for p, lp_ in enumerate(e.emb_params[:2])]
+
+    # ---- hot-row replication ----------------------------------------------------------------------
+    def _bind_hot_out(self, ep) -> None:
+        """The local reduction sends replicated rows' sums to the X4 bucket instead of grad_stage."""
+        if self.n_hot:
+            ep.hot_out, ep.hot_base, ep.n_hot = self.mlp_bucket[self.P:].data_ptr(), self.M, self.n_hot
+        else:
+            ep.hot_out, ep.n_hot = 0, 0
+
+    def _hot_params(self, ep, opt, step_ptr):
+        """Replica update block (merge_search_apply role) or None without replicated rows."""
+        if not self.n_hot:
+            return None
+        e, H = self.eng, self.H
+        h = H.HotApplyParams()
+        h.rows = self.hot_rep.data_ptr()
+        sl = self.hot_slots
+        h.s0 = sl[0].data_ptr() if len(sl) > 0 else 0
+        h.s1 = sl[1].data_ptr() if len(sl) > 1 else 0
+        hot_part = self.mlp_bucket[self.P:]
+        if self.exchange == "p2p":  # W rank segments, summed in rank order by the kernel
+            h.grads, h.nseg, h.seg_stride = self.x_mlp.recv_ptr + 4 * self.P, self.W, self.x_mlp.slot
+        else:  # all-reduced in place (or one rank)
+            h.grads, h.nseg, h.seg_stride = hot_part.data_ptr(), 1, 0
+        h.zero = hot_part.data_ptr()
+        h.H, h.Kp, h.K1 = self.n_hot, e.Kp, e.K1
+        h.l2, h.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
+        h.opt, h.step = opt, step_ptr
+        h.dense = 1 if self.embedding_update == "exact" else 0
+        return h
+
+    def set_hot_ids(self, ids) -> None:
+        """Replicate these global ids (≤ hot_rows; rank 0's list is used on every rank).  Collective.
+        The replica (and its optimizer slots) is loaded from the owners."""
+        if not self.NH:
+            raise ValueError("set_hot_ids needs hot_rows > 0 at construction")
+        self._flush_hot()
+        t = torch.full((self.NH + 1,), -1, dtype=torch.int64)
+        u = torch.unique(torch.as_tensor(ids, dtype=torch.int64).flatten().cpu())
+        u = u[(u >= 0) & (u < self.V)][: self.NH]
+        t[0] = len(u)
+        t[1:1 + len(u)] = u
+        if self.W > 1:
+            from .dist import broadcast_tensors
+
+            tt = t.to(self.device) if dist.get_backend() == "nccl" else t
+            broadcast_tensors([tt])
+            t = tt.cpu()
+        k = int(t[0])
+        self.hot_ids = t[1:1 + k].clone()
+        self.n_hot = k
+        self.hot_ids_dev.fill_(PAD)
+        self.hot_ids_dev[:k].copy_(self.hot_ids.to(torch.int32))
+        self._load_hot()
+        self._build()  # parameter blocks carry n_hot
+        self._graphs = {}
+        self._ms_S = None  # multi-step blocks are rebuilt with the hot ids
+        self._pre_served = False
+
+    def _choose_hot(self, ids: torch.Tensor) -> None:
+        """Pick the hot_rows most frequent ids of these batches (rank 0's choice wins)."""
+        u, c = torch.unique(ids.flatten().to(torch.int64), return_counts=True)
+        top = torch.topk(c, min(self.NH, u.numel())).indices
+        self.set_hot_ids(u[top].cpu())
+
+    def _owned_hot(self):
+        """(replica slots, local rows) of the replicated ids this rank owns."""
+        hid = self.hot_ids
+        mine = (hid % self.W) == self.rank
+        slot = torch.nonzero(mine).flatten()
+        return slot.to(self.device), (hid[mine] // self.W).to(self.device)
+
+    @torch.no_grad()
+    def _load_hot(self) -> None:
+        """Replica ← owners' rows (and slots): every rank adds the rows it owns, all-reduced."""
+        if not self.n_hot:
+            return
+        e = self.eng
+        slot, rows = self._owned_hot()
+        bufs = [self.hot_rep] + self.hot_slots
+        srcs = [e.emb] + list(e.emb_slots)
+        flat = torch.zeros(len(bufs), self.n_hot, e.Kp, dtype=torch.float32, device=self.device)
+        for i, src in enumerate(srcs):
+            flat[i].index_copy_(0, slot, src.index_select(0, rows))
+        if self.W > 1:
+            if dist.get_backend() == "nccl":
+                all_reduce_(flat)
+            else:
+                c = flat.cpu()
+                all_reduce_(c)
+                flat.copy_(c)
+        for i, b in enumerate(bufs):
+            b[: self.n_hot].copy_(flat[i])
+
+    @torch.no_grad()
+    def _flush_hot(self) -> None:
+        """Owners' rows (and slots) ← the replica, for the replicated ids this rank owns."""
+        if not self.n_hot:
+            return
+        e = self.eng
+        torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
+        slot, rows = self._owned_hot()
+        for dst, src in zip([e.emb] + list(e.emb_slots), [self.hot_rep] + self.hot_slots):
+            dst.index_copy_(0, rows, src.index_select(0, slot))
 
     def _recv(self, parity: int = 0) -> Optional[torch.Tensor]:
         """X1 receive buffer of a step of this parity (None: world 1, the send list is read)."""
@@ -577,6 +705,8 @@ class FusedRowShard:
 
     # ---- batch feeding (delegated) ------------------------------------------------------------
     def attach_pool(self, ids, vals, labels, start: int = 0):
+        if self.NH and self.hot_ids is None:
+            self._choose_hot(ids[: min(len(ids), 8)])
         self.eng.attach_pool(ids, vals, labels, start)
         self._graphs = {}
         self._pre_served = False
@@ -585,6 +715,8 @@ class FusedRowShard:
         self.eng.push_batch(ids, vals, labels)
 
     def load_batch(self, ids, vals, labels=None):
+        if self.NH and self.hot_ids is None:
+            self._choose_hot(ids)
         self.eng.load_batch(ids, vals, labels)
         self._pre_served = False
 
@@ -640,7 +772,8 @@ class FusedRowShard:
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
         s = e.stream_ptr
-        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], s)  # owner merge ‖ MLP opt
+        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], s, None,
+                             self.hot_params[p])  # owner merge ‖ MLP opt ‖ replicated rows
         if self.embedding_update == "exact":
             H.emb_dense_update(e.emb_dense_params[p], s)
 
@@ -690,10 +823,10 @@ class FusedRowShard:
         if self.exchange == "p2p":
             prm = self._p2p_params.get("mlp")
             if prm is None:
-                prm = self._p2p_params["mlp"] = self.x_mlp.params(e.dense_grads_flat.data_ptr(), self.P)
+                prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), self.PX)
             self.x_mlp.push(prm)
         elif self.W > 1 or self.force:
-            all_reduce_(e.dense_grads_flat)
+            all_reduce_(self.mlp_bucket)  # MLP grads + replicated-row sums, one collective
 
     def _step_body(self, p: int) -> None:
         e = self.eng
@@ -703,7 +836,7 @@ class FusedRowShard:
         side = self._fork_next(p)  # next batch's fetch + route overlaps the whole step
         self._exchange(self.recv_ids, self.send_ids[p])                        # X1 requests
         self._phase_serve(p)
-        self._exchange(self.rows_in, self.rows_out)                             # X2 rows
+        self._exchange(self.rows_x, self.rows_out[:self.M])                             # X2 rows
         self._phase_compute(p, with_side=False)
         self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
         self._allreduce_mlp()                                                   # X4 MLP grads
@@ -718,15 +851,16 @@ class FusedRowShard:
         if serve_first:
             self._exchange(self._recv(p), self.send_ids[p])                     # X1 requests
             self._phase_serve(p)
-            self._exchange(self.rows_in, self.rows_out)                         # X2 rows
+            self._exchange(self.rows_x, self.rows_out[:self.M])                         # X2 rows
         self._phase_compute(p, with_side=True)  # joins the side chain: batch 1-p is routed
         self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
         self._allreduce_mlp()                                                   # X4 MLP grads
         self._exchange(self._recv(1 - p), self.send_ids[1 - p])                 # X1 of the next step
-        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], e.stream_ptr, self.serve[1 - p])
+        H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], e.stream_ptr, self.serve[1 - p],
+                             self.hot_params[p])
         if self.embedding_update == "exact":
             H.emb_dense_update(e.emb_dense_params[p], e.stream_ptr)
-        self._exchange(self.rows_in, self.rows_out)                             # X2 of the next step
+        self._exchange(self.rows_x, self.rows_out[:self.M])                             # X2 of the next step
 
     def train_step(self) -> None:
         e = self.eng
@@ -746,7 +880,7 @@ class FusedRowShard:
         else:
             self._exchange(self.recv_ids, self.send_ids[p])
             self._run(("serve", p), lambda: self._phase_serve(p))
-            self._exchange(self.rows_in, self.rows_out)
+            self._exchange(self.rows_x, self.rows_out[:self.M])
             self._run(("compute", p), lambda: self._phase_compute(p))
             self._exchange(self.grad_back, self.grad_stage)
             self._allreduce_mlp()
@@ -817,7 +951,7 @@ class FusedRowShard:
     def _build_multi_rs(self, Smax: int) -> None:
         e, H = self.eng, self.H
         W, cap, n, F = self.W, self.cap, self.n, e.F
-        e._build_multi(Smax, shard=(W, self.Vs))
+        e._build_multi(Smax, shard=(W, self.Vs) + ((self.hot_ids_dev[: self.n_hot],) if self.n_hot else ()))
         e._m_pool = e.pool_ids
         S_ = e.mS
         dev = self.device
@@ -847,6 +981,7 @@ class FusedRowShard:
                 ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
                 ep.touched = 0
                 ep.grad_scale = 1.0
+                self._bind_hot_out(ep)
                 da.apply, da.grad_scale = 1, 1.0 / W
                 self._set_mlp_grads(da)
                 mg = H.MergeParams()
@@ -860,7 +995,8 @@ class FusedRowShard:
                 mg.keys = self._recv_ids_for(self.ms_send[q, k], par).data_ptr()
                 if ed is not None:
                     ed.grad_scale = 1.0
-                steps.append((rows, wp, ep, da, ed, mg, self._serve_params(self._recv_ids_for(self.ms_send[q, k], par))))
+                steps.append((rows, wp, ep, da, ed, mg, self._serve_params(self._recv_ids_for(self.ms_send[q, k], par)),
+                              self._hot_params(ep, mg.opt, mg.step)))
             self.ms_route.append(routes)
             self.ms_steps.append(steps)
 
@@ -878,24 +1014,24 @@ class FusedRowShard:
         s = torch.cuda.current_stream(self.device).cuda_stream
         st = self.staleness
         for k in range(S):
-            rows, wp, ep, da, ed, mg, sv = self.ms_steps[q][k]
+            rows, wp, ep, da, ed, mg, sv, hot = self.ms_steps[q][k]
             par = k % 2 if st else 0
             if k == 0 or not st:  # (staleness 1: later steps were served by the previous update)
                 self._exchange(self._recv(par), self.ms_send[q, k])             # X1 requests
                 H.shard_serve(sv, s)
-                self._exchange(self.rows_in, self.rows_out)                     # X2 rows
+                self._exchange(self.rows_x, self.rows_out[:self.M])                     # X2 rows
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
             self._allreduce_mlp()                                               # X4 MLP grads
             if st and k + 1 < S:  # owner merge ‖ MLP opt ‖ serve of step k+1
                 self._exchange(self._recv(1 - par), self.ms_send[q, k + 1])     # X1 of step k+1
-                H.merge_search_apply(mg, da, s, self.ms_steps[q][k + 1][6])
+                H.merge_search_apply(mg, da, s, self.ms_steps[q][k + 1][6], hot)
                 if ed is not None:
                     H.emb_dense_update(ed, s)
-                self._exchange(self.rows_in, self.rows_out)                     # X2 of step k+1
+                self._exchange(self.rows_x, self.rows_out[:self.M])                     # X2 of step k+1
                 continue
-            H.merge_search_apply(mg, da, s)                                     # owner merge ‖ MLP opt
+            H.merge_search_apply(mg, da, s, None, hot)                          # owner merge ‖ MLP opt ‖ hot
             if ed is not None:
                 H.emb_dense_update(ed, s)
 
@@ -948,6 +1084,7 @@ class FusedRowShard:
     @torch.no_grad()
     def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
         e = self.eng
+        self._flush_hot()  # predictions read the replicated rows from their owners
         self._pre_served = False  # the prediction reuses the serve / row buffers
         nrows = int(ids.shape[0])
         nch = max(1, (nrows + e.B - 1) // e.B)
@@ -971,7 +1108,7 @@ class FusedRowShard:
             self._route_launch(self.pred_route, m * e.F, torch.cuda.current_stream(self.device))
             self._exchange(self.recv_ids, self.pred_send)
             self.H.shard_serve(self.pred_serve, e.stream_ptr)
-            self._exchange(self.rows_in, self.rows_out)
+            self._exchange(self.rows_x, self.rows_out[:self.M])
             if m:
                 pp = e.pred_params
                 pp.B = m
@@ -986,6 +1123,7 @@ class FusedRowShard:
     # ---- bookkeeping ----------------------------------------------------------------------------
     def l2_value(self) -> float:
         e = self.eng
+        self._flush_hot()
         nb = 1024
         part = torch.zeros(nb, dtype=torch.float32, device=self.device)
         self.H.emb_sumsq(e.emb.data_ptr(), e.V * e.Kp // 4, e.Kp, e.K1, part.data_ptr(), nb, e.stream_ptr)
@@ -1007,6 +1145,7 @@ class FusedRowShard:
         return {k: rows for k in names}
 
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        self._flush_hot()
         sd = self.eng.state_dict()
         for k in self.row_sets():
             sd[k] = sd[k][: self.n_loc].clone()
@@ -1015,12 +1154,14 @@ class FusedRowShard:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
+        self._load_hot()
         self._pre_served = False
         self._graphs = {}
         self._warm = 0
 
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
         e = self.eng
+        self._flush_hot()
         out = e.parameters_tf()
         if self.W > 1:
             out["fm_w"] = _gather_table(e.emb[:, e.K].contiguous(), self.V, self.W).cpu()

@@ -83,7 +83,7 @@ class P2PExchange:
     """
 
     def __init__(self, slot_floats: int, device, group=None, kind: int = KIND_UNCACHED,
-                 spin_limit: int = 1 << 30):
+                 spin_limit: int = 1 << 30, extra_floats: int = 0):
         H = self.H = _hip()
         self.group = group
         self.W = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -92,6 +92,8 @@ class P2PExchange:
             raise ValueError(f"p2p exchange supports at most {H.p2p_max_world()} ranks, got {self.W}")
         self.device = torch.device(device)
         self.slot = (int(slot_floats) + 3) // 4 * 4
+        # local floats behind the W slots (never pushed; e.g. the row-shard hot-row replica)
+        self.extra = (int(extra_floats) + 3) // 4 * 4
         self.spin_limit = int(spin_limit)
         self.kind = kind
         self._own: List[int] = []
@@ -117,7 +119,7 @@ class P2PExchange:
             try:
                 if self.init_error is not None:
                     raise self.init_error
-                self.recv_ptr = H.p2p_malloc(self.W * self.slot * 4, kind)
+                self.recv_ptr = H.p2p_malloc((self.W * self.slot + self.extra) * 4, kind)
                 self._own.append(self.recv_ptr)
                 self.sig_ptr = H.p2p_malloc(max(256, 8 * self.W), kind)
                 self._own.append(self.sig_ptr)
@@ -189,8 +191,8 @@ class P2PExchange:
         if torch.empty(0, dtype=dtype).element_size() != 4:
             raise ValueError("recv_tensor supports 4-byte dtypes")
         n = int(math.prod(shape))
-        if n > self.W * self.slot:
-            raise ValueError(f"{n} elements exceed the {self.W}x{self.slot} receive slots")
+        if n > self.W * self.slot + self.extra:
+            raise ValueError(f"{n} elements exceed the {self.W}x{self.slot} receive slots (+{self.extra})")
         typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
 
         class _Raw:  # __cuda_array_interface__ v3 view of the uncached HIP allocation
@@ -253,7 +255,8 @@ def selftest(ex: P2PExchange, n_floats: int, rounds: int = 3) -> bool:
     return ok
 
 
-def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None) -> Optional[List[P2PExchange]]:
+def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None,
+                   extra_floats: Optional[List[int]] = None) -> Optional[List[P2PExchange]]:
     """One P2PExchange per slot size, or None for the RCCL path.
 
     ``choice`` (default: env ROCFM_DP_EXCHANGE, else ``auto``): ``rccl`` → None; ``p2p`` → the
@@ -270,7 +273,8 @@ def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None)
         if choice == "p2p":
             raise RuntimeError("exchange=p2p needs every rank on one node")
         return None
-    exs = [P2PExchange(n, device) for n in slot_floats]  # collective; failures land in init_error
+    extra = list(extra_floats or [0] * len(slot_floats))
+    exs = [P2PExchange(n, device, extra_floats=x) for n, x in zip(slot_floats, extra)]  # collective
     ok = True
     for ex, n in zip(exs, slot_floats):
         ok = selftest(ex, n) and ok  # every rank runs every self-test (each one is agreed)

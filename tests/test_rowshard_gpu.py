@@ -142,7 +142,7 @@ def test_fused_rowshard_world1_equals_single(update, graph):
     torch.testing.assert_close(p, pr, rtol=1e-4, atol=1e-5)
 
 
-def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0, staleness=0):
+def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0, staleness=0, hot=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -153,7 +153,7 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     spec, hp = _cfg()
     B = 64
     eng = FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), embedding_update=update,
-                        use_graph=spg > 0, exchange=exchange, staleness=staleness)
+                        use_graph=spg > 0, exchange=exchange, staleness=staleness, hot_rows=hot)
     assert eng.exchange == exchange, eng.exchange
     batches = _batches(world * B, steps, 11, disjoint=staleness > 0)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
@@ -170,6 +170,8 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     P = eng.parameters_tf()
     ids, vals, _ = _batches(100, 1, 5)[0]
     p, _ = eng.predict_batch(ids.cuda() if rank == 0 else ids[:0].cuda(), vals.cuda() if rank == 0 else vals[:0].cuda())
+    if hot:
+        assert eng.n_hot == hot
     if rank == 0:
         torch.save({"P": dict(P), "pred": p.cpu()}, out_path)
     eng.close()
@@ -302,3 +304,58 @@ def test_rowshard_staleness1_2ranks_p2p(tmp_path):
     exp = ref.parameters_tf()
     for k in exp:
         torch.testing.assert_close(got["P"][k], exp[k], rtol=2e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("update,mode", [("sparse", "eager"), ("sparse", "graph"), ("sparse", "multi"),
+                                         ("exact", "multi")])
+def test_rowshard_hot_rows_world1_equals_single(update, mode):
+    """Hot-row replication: the 64 most frequent ids live in the local replica (routed to the
+    virtual owner W, updated from the X4 bucket) — same result as the single-GPU engine; the
+    checkpoint / prediction see the replica through the owners' rows."""
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg()
+    n = 11
+    eng = FusedRowShard(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=update,
+                        use_graph=mode != "eager", hot_rows=64)
+    batches = _batches(128, n, 11)
+    eng.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
+                    torch.stack([b[2] for b in batches]).cuda())
+    assert eng.n_hot == 64
+    if mode == "multi":
+        eng.train_steps(n, 4)
+    else:
+        for _ in range(n):
+            eng.train_step()
+    torch.cuda.synchronize()
+    eng.check()
+    ref = _single(update, n)
+    got, exp = eng.parameters_tf(), ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got[k], exp[k], rtol=2e-3, atol=2e-5)
+    sd, sr = eng.state_dict(), ref.state_dict()
+    for k in [k for k in sr if k.startswith("fm_")]:  # tables and their optimizer slots
+        torch.testing.assert_close(sd[k], sr[k], rtol=2e-3, atol=2e-5)
+    ids, vals, _ = _batches(100, 1, 5)[0]
+    p, _ = eng.predict_batch(ids.cuda(), vals.cuda())
+    pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
+    torch.testing.assert_close(p, pr, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("exchange,spg", [("p2p", 4), ("rccl", 0)])
+def test_rowshard_hot_rows_2ranks(tmp_path, exchange, spg):
+    """Two ranks: replicated rows' sums travel in the X4 bucket (p2p rank segments summed in rank
+    order / the backend's all-reduce) ≡ the single-GPU engine on the union batch."""
+    out = str(tmp_path / "rs_hot.pt")
+    steps = 10
+    mp.start_processes(_worker, args=(2, _free_port(), "sparse", out, exchange, steps, spg, 0, 48), nprocs=2,
+                       join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    ref = _single("sparse", steps)
+    exp = ref.parameters_tf()
+    for k in exp:
+        torch.testing.assert_close(got["P"][k], exp[k], rtol=2e-3, atol=1e-4)
+    ids, vals, _ = _batches(100, 1, 5)[0]
+    pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
+    torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-5)
