@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"])
     ap.add_argument("--compute_dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: the MLP input layer's forward GEMM on fp8-e4m3 MFMA (dynamic scales)")
+    ap.add_argument("--table_dtype", default="f32", choices=["f32", "bf16"],
+                    help="embedding table storage (bf16: stochastic-rounded updates, f32 optimizer slots)")
     ap.add_argument("--embedding_update", default="sparse", choices=["sparse", "exact"])
     ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
@@ -160,19 +162,19 @@ def main():
             from rocfm.parallel.emb_shard import FusedRowShard
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
-                                use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype,
+                                use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype, table_dtype=a.table_dtype,
                                 exchange=a.dp_exchange, staleness=a.ps_staleness, hot_rows=a.hot_rows)
         elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 
             eng = FusedDataParallel(spec, hp, B, dev, params=params, embedding_update=a.embedding_update,
                                     mode=parallelism, seed=a.seed, use_graph=not a.no_graph, capacity=cap,
-                                    compute_dtype=a.compute_dtype, exchange=a.dp_exchange)
+                                    compute_dtype=a.compute_dtype, table_dtype=a.table_dtype, exchange=a.dp_exchange)
         else:
             from rocfm.models.fused import FusedDeepFM
 
             eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
-                              use_graph=not a.no_graph, compute_dtype=a.compute_dtype)
+                              use_graph=not a.no_graph, compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
 
         eng.attach_pool(pool_ids, pool_vals, pool_labels)
 
@@ -252,6 +254,7 @@ def main():
             "parallelism": f"{parallelism}{world}" if (world > 1 or a.parallelism != "auto") else "dp1",
             "engine": a.engine,
             "embedding_update": a.embedding_update,
+            "table_dtype": a.table_dtype,
             "exchange_capacity": cap,
             "ps_staleness": a.ps_staleness if parallelism == "rowshard" else None,
             "hot_rows": a.hot_rows if parallelism == "rowshard" else None,
@@ -316,7 +319,7 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
     loader_eps = nb * B / (time.perf_counter() - t)
 
     eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
-                      compute_dtype=a.compute_dtype)
+                      compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
     eng.train_stream(dataset().groups(S, hold=2, limit=a.warmup), S, hold=2)  # graphs + code objects
     stall = [0.0]
 

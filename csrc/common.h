@@ -67,6 +67,56 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// ---- embedding-table storage: f32 or bf16 rows ([V][Kp], one float4 column group = 16 B or 8 B) ----
+// bf16 tables are updated with stochastic rounding (unbiased: updates far below one bf16 ulp still
+// move the weight in expectation); the random bits hash the element index and the step, so the
+// result is reproducible.  Optimizer slots stay f32.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint16_t f2bf_sr(float f, uint32_t r16) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return f2bf(f);  // inf / NaN
+  u += r16 & 0xffffu;
+  return (uint16_t)(u >> 16);
+}
+template <bool BT>
+__device__ __forceinline__ float4 tbl_load4(const void* t, size_t i) {
+  if constexpr (BT) {
+    const uint2 h = reinterpret_cast<const uint2*>(t)[i];
+    return make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u), __uint_as_float(h.y << 16),
+                       __uint_as_float(h.y & 0xffff0000u));
+  } else {
+    return reinterpret_cast<const float4*>(t)[i];
+  }
+}
+template <bool BT>
+__device__ __forceinline__ void tbl_store4(void* t, size_t i, float4 v, uint32_t step) {
+  if constexpr (BT) {
+    const uint32_t r0 = mix32((uint32_t)i * 2u ^ (step * 0x9e3779b9u)), r1 = mix32((uint32_t)i * 2u + 1u ^ (step * 0x9e3779b9u));
+    uint2 h;
+    h.x = (uint32_t)f2bf_sr(v.x, r0) | ((uint32_t)f2bf_sr(v.y, r0 >> 16) << 16);
+    h.y = (uint32_t)f2bf_sr(v.z, r1) | ((uint32_t)f2bf_sr(v.w, r1 >> 16) << 16);
+    reinterpret_cast<uint2*>(t)[i] = h;
+  } else {
+    reinterpret_cast<float4*>(t)[i] = v;
+  }
+}
+__device__ __forceinline__ float4 tbl_load4_rt(const void* t, size_t i, bool bf) {
+  return bf ? tbl_load4<true>(t, i) : tbl_load4<false>(t, i);
+}
+__device__ __forceinline__ void tbl_store4_rt(void* t, size_t i, float4 v, uint32_t step, bool bf) {
+  if (bf)
+    tbl_store4<true>(t, i, v, step);
+  else
+    tbl_store4<false>(t, i, v, step);
+}
+
 // MFMA B-fragment swizzle of a row-major bf16 matrix [R][C] (R % 16 == 0, C % 32 == 0): the
 // 16-row × 32-column block (nt, u) is stored as 64 lanes × 8 contiguous elements in the order the
 // 16x16x32 B operand wants them (lane l: row 16·nt + (l & 15), columns 32·u + 8·(l >> 4) .. +7),

@@ -27,6 +27,7 @@ struct RowsParams {
   const float* vals;    // [B][F]
   const float* labels;  // [B]
   const float* emb;     // [V][Kp]: cols 0..K-1 = fm_v row, col K = fm_w, rest 0
+  int tbl_bf16;         // 1: emb holds bf16 rows (common.h tbl_load4)
   const float* fm_bias;
   const float* w_out;  // [dims[nl]] f32 (deep_out/weights)
   const float* b_out;  // [1]

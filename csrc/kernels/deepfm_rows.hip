@@ -216,7 +216,7 @@ struct CtShape {
 // prefetched fragments.  Branch-free static kernels wait only for what they consume.
 constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
 
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG>
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const int D0 = F * K, D0p = sh.dim(0);
   const uint32_t magicF = p.magicF;
   const int Bp = p.Bp;
-  const float4* emb4 = reinterpret_cast<const float4*>(p.emb);
+  const void* emb4 = p.emb;  // f32 or (BT) bf16 rows: tbl_load4
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   ROWS_STAMP(0);
   if (p.zero_word != nullptr && blockIdx.x == 0 && t == 0) *p.zero_word = 0;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       for (int u = 0; u < U; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitems - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
-        v[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+        v[u] = tbl_load4<BT>(emb4, (size_t)s_ids[rf] * KP4 + c4);
       }
       // every gathered row is consumed (scaled) in straight-line code before any branch, so the
       // four loads are waited for once; the branches below hold LDS stores only
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     for (int u = 0; u < UF; ++u) {
       const int idx = min(u * kRowThreads + t, nitemsF - 1);
       const int rf = idx / KP4, c4 = idx - rf * KP4;
-      rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+      rowsF[u] = tbl_load4<BT>(emb4, (size_t)s_ids[rf] * KP4 + c4);
     }
   }
   lds_barrier();
@@ -914,7 +914,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       for (int u = 0; u < UF; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitemsF - 1);
         const int rf = idx / KP4, c4 = idx - rf * KP4;
-        rowsF[u] = emb4[(size_t)s_ids[rf] * KP4 + c4];
+        rowsF[u] = tbl_load4<BT>(emb4, (size_t)s_ids[rf] * KP4 + c4);
       }
     }
     // all four items' gradient rows are computed in straight-line code (clamped items, LDS reads
@@ -1015,9 +1015,9 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
   return L;
 }
 
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG>
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT>
 static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
-  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG>;
+  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG, BT>;
   static bool attr_set = false;
   static int max_dyn = 0;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
@@ -1045,17 +1045,18 @@ static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
 
 // Static shapes: branch-free train / inference kernels; the diagnostic (stamps, ablations)
 // instantiation only for the benchmark shape's training kernel.
-template <int KP4, class SH>
+template <int KP4, class SH, bool BT>
 static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   if constexpr (SH::kStatic) {
     const bool diag = p.stamps != nullptr || p.ablate != 0;
     if (diag) {
-      if constexpr (SH::F == 39 && SH::K == 10 && SH::nl == 3) {
+      if constexpr (SH::F == 39 && SH::K == 10 && SH::nl == 3 && !BT) {
         ROCFM_REQUIRE(!p.fp8 && p.train, "deepfm_rows: diagnostics are built for the bf16 training kernel only");
-        launch_rows_impl<KP4, SH, false, kTrain, true>(p, stream);
+        launch_rows_impl<KP4, SH, false, kTrain, true, false>(p, stream);
         return;
       } else {
-        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 shape");
+        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 shape "
+                                    "and an f32 table");
       }
     }
     if (p.fp8) {
@@ -1063,19 +1064,27 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
         throw std::invalid_argument("deepfm_rows: compute_dtype=fp8 supports input layers up to 512 wide");
       } else {
         if (p.train)
-          launch_rows_impl<KP4, SH, true, kTrain, false>(p, stream);
+          launch_rows_impl<KP4, SH, true, kTrain, false, BT>(p, stream);
         else
-          launch_rows_impl<KP4, SH, true, kInfer, false>(p, stream);
+          launch_rows_impl<KP4, SH, true, kInfer, false, BT>(p, stream);
         return;
       }
     }
     if (p.train)
-      launch_rows_impl<KP4, SH, false, kTrain, false>(p, stream);
+      launch_rows_impl<KP4, SH, false, kTrain, false, BT>(p, stream);
     else
-      launch_rows_impl<KP4, SH, false, kInfer, false>(p, stream);
+      launch_rows_impl<KP4, SH, false, kInfer, false, BT>(p, stream);
     return;
   }
-  launch_rows_impl<KP4, SH, false, kDynamic, true>(p, stream);
+  launch_rows_impl<KP4, SH, false, kDynamic, true, BT>(p, stream);
+}
+
+template <int KP4, class SH>
+static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
+  if (p.tbl_bf16)
+    launch_rows_t<KP4, SH, true>(p, stream);
+  else
+    launch_rows_t<KP4, SH, false>(p, stream);
 }
 
 // Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
@@ -1089,7 +1098,7 @@ static bool try_static(const RowsParams& p, hipStream_t stream) {
   for (int l = 0; l < nl; ++l)
     if (!p.WTs[l] || !p.Wbs[l]) return false;  // the static kernels load the frag_swz weight copies
   constexpr int KP4 = (K + 1 + 3) / 4;
-  launch_rows_t<KP4, CtShape<F, K, D1, D2, D3>>(p, stream);
+  launch_rows_tb<KP4, CtShape<F, K, D1, D2, D3>>(p, stream);
   return true;
 }
 
@@ -1122,7 +1131,7 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N)                          \
   case N:                                     \
-    launch_rows_t<N, RtShape>(p, stream);     \
+    launch_rows_tb<N, RtShape>(p, stream);    \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
     ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)

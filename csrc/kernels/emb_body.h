@@ -39,7 +39,7 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
 // are summed by a wave-level segmented scan (shfl_up, fixed order); each run owned by the chunk
 // (its first entry lies here) adds its ≤4 wave pieces and, for the chunk's last run, the
 // continuation chunks; then one 16-lane group per run applies the optimizer to the table row.
-template <int KP4, int kChunk>
+template <int KP4, int kChunk, bool BT = false>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
   __shared__ float4 s_rows[kChunk * KP4];
@@ -238,7 +238,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       idx4[u] = row * KP4 + u4;
       if (p.mode == 0) {  // issue the row's parameter + slot loads now
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        w[u] = reinterpret_cast<const float4*>(p.emb)[idx4[u]];
+        w[u] = tbl_load4<BT>(p.emb, idx4[u]);
         a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;
         b[u] = p.s1 ? reinterpret_cast<const float4*>(p.s1)[idx4[u]] : z;
       }
@@ -274,7 +274,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
           if (u4 * 4 + c >= p.K1) continue;  // padding columns keep their (zero) values
           opt_apply(p.opt, st, wc[c], gc[c] + p.l2 * wc[c], ac[c], bc[c]);
         }
-        reinterpret_cast<float4*>(p.emb)[idx4[u]] = w[u];
+        tbl_store4<BT>(p.emb, idx4[u], w[u], p.step ? (uint32_t)*p.step : 0u);
         if (p.s0) reinterpret_cast<float4*>(p.s0)[idx4[u]] = a[u];
         if (p.s1) reinterpret_cast<float4*>(p.s1)[idx4[u]] = b[u];
       }

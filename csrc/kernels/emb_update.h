@@ -45,6 +45,7 @@ struct EmbUpdateParams {
   float* hot_out;
   uint32_t hot_base;
   int n_hot;
+  int tbl_bf16;  // 1: emb holds bf16 rows (stochastic-rounded updates, common.h)
 };
 
 struct EmbDenseParams {
@@ -62,10 +63,12 @@ struct EmbDenseParams {
   // (written by the mode-1 scatter / merge).  Other rows read no gradient row (g = λ·θ only) and
   // their dense_grad stays zero — the update never reads or clears the whole gradient table.
   const uint32_t* touched;
+  int tbl_bf16;  // 1: emb holds bf16 rows
 };
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream);
 void launch_emb_dense_update(EmbDenseParams p, hipStream_t stream);
-void launch_emb_sumsq(const float* emb, long long n4, int Kp, int K1, float* partial, int nblocks, hipStream_t stream);
+void launch_emb_sumsq(const float* emb, long long n4, int Kp, int K1, float* partial, int nblocks, hipStream_t stream,
+                      int tbl_bf16 = 0);
 
 }  // namespace rocfm

@@ -18,14 +18,18 @@
 
 namespace rocfm {
 
-template <int KP4>
+template <int KP4, bool BT>
 __global__ __launch_bounds__(kEmbChunk) void emb_rows_update_kernel(const EmbUpdateParams p) {
-  emb_rows_body<KP4, kEmbChunk>(p, blockIdx.x);
+  emb_rows_body<KP4, kEmbChunk, BT>(p, blockIdx.x);
 }
 
 template <int KP4>
 static void launch_rows_update_t(const EmbUpdateParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(emb_rows_update_kernel<KP4>, dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream, p);
+  if (p.tbl_bf16)
+    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, true>), dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream, p);
+  else
+    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, false>), dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream,
+                       p);
 }
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {
@@ -52,7 +56,8 @@ void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDenseParams p) {
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
-  float4* E = reinterpret_cast<float4*>(p.emb);
+  const bool bf = p.tbl_bf16 != 0;
+  const uint32_t stp = p.step ? (uint32_t)*p.step : 0u;
   float4* G = reinterpret_cast<float4*>(p.dense_grad);
   float4* A = reinterpret_cast<float4*>(p.s0);
   float4* Bv = reinterpret_cast<float4*>(p.s1);
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < p.n4; i += (long long)gridDim.x * 256) {
     const int c0 = (int)(i % kp4) * 4;
     const bool has_g = p.touched == nullptr || p.touched[i / kp4] == tag;
-    float4 w = E[i], g = make_float4(0, 0, 0, 0);
+    float4 w = tbl_load4_rt(p.emb, i, bf), g = make_float4(0, 0, 0, 0);
     if (has_g) g = G[i];
     float4 a = A ? A[i] : make_float4(0, 0, 0, 0), b = Bv ? Bv[i] : make_float4(0, 0, 0, 0);
     float* wp = &w.x;
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], gp[u] * p.grad_scale + p.l2 * wp[u], ap[u], bp[u]);
-    E[i] = w;
+    tbl_store4_rt(p.emb, i, w, stp, bf);
     if (has_g) G[i] = make_float4(0, 0, 0, 0);
     if (A) A[i] = a;
     if (Bv) Bv[i] = b;
@@ -90,14 +95,13 @@ void launch_emb_dense_update(EmbDenseParams p, hipStream_t stream) {
 // Writes one partial per workgroup; the host sums the partials (deterministic).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void emb_sumsq_kernel(const float* emb, long long n4, int Kp, int K1,
-                                                        float* partial) {
+                                                        float* partial, int bf) {
   __shared__ float s[4];
-  const float4* E = reinterpret_cast<const float4*>(emb);
   const int kp4 = Kp >> 2;
   float acc = 0.f;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     const int c0 = (int)(i % kp4) * 4;
-    const float4 w = E[i];
+    const float4 w = tbl_load4_rt(emb, i, bf != 0);
     acc += (c0 + 0 < K1 ? w.x * w.x : 0.f) + (c0 + 1 < K1 ? w.y * w.y : 0.f) + (c0 + 2 < K1 ? w.z * w.z : 0.f) +
            (c0 + 3 < K1 ? w.w * w.w : 0.f);
   }
@@ -108,8 +112,8 @@ __global__ __launch_bounds__(256) void emb_sumsq_kernel(const float* emb, long l
 }
 
 void launch_emb_sumsq(const float* emb, long long n4, int Kp, int K1, float* partial, int nblocks,
-                      hipStream_t stream) {
-  hipLaunchKernelGGL(emb_sumsq_kernel, dim3(nblocks), dim3(256), 0, stream, emb, n4, Kp, K1, partial);
+                      hipStream_t stream, int tbl_bf16) {
+  hipLaunchKernelGGL(emb_sumsq_kernel, dim3(nblocks), dim3(256), 0, stream, emb, n4, Kp, K1, partial, tbl_bf16);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

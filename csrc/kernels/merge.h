@@ -61,6 +61,7 @@ struct MergeParams {
   unsigned long long* hkeys;  // [hash_slots], zero-initialised once
   unsigned long long* hrep;   // [hash_slots]
   unsigned long long* hpos;   // [hash_slots][W]
+  int tbl_bf16;               // 1: emb holds bf16 rows (stochastic-rounded updates, common.h)
 };
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);

@@ -139,12 +139,11 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
   // Absent slots read the table instead and are zeroed after the load: a `ptr ? load : 0` here
   // became a select between a global and a private address (flat access + scratch).
   float4 w[KP4], a[KP4], b[KP4];
-  const float4* e4r = reinterpret_cast<const float4*>(p.emb) + base;
   const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
   const float4* b4r = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb) + base;
 #pragma unroll
   for (int c = 0; c < KP4; ++c) {
-    w[c] = e4r[c];
+    w[c] = tbl_load4_rt(p.emb, base + c, p.tbl_bf16 != 0);
     a[c] = a4r[c];
     b[c] = b4r[c];
   }
@@ -220,7 +219,6 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
     return;
   }
   const OptStep st = opt_step(p.opt, *p.step);
-  float4* e4 = reinterpret_cast<float4*>(p.emb) + base;
   float4* a4 = p.s0 ? reinterpret_cast<float4*>(p.s0) + base : nullptr;
   float4* b4 = p.s1 ? reinterpret_cast<float4*>(p.s1) + base : nullptr;
 #pragma unroll
@@ -234,7 +232,7 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
       if (c * 4 + u >= p.K1) continue;
       opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
     }
-    e4[c] = w[c];
+    tbl_store4_rt(p.emb, base + c, w[c], (uint32_t)*p.step, p.tbl_bf16 != 0);
     if (a4) a4[c] = a[c];
     if (b4) b4[c] = b[c];
   }
@@ -273,7 +271,6 @@ __device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t ro
     return;
   }
   const OptStep st = opt_step(p.opt, *p.step);
-  float4* e4 = reinterpret_cast<float4*>(p.emb) + base;
   float4* a4 = p.s0 ? reinterpret_cast<float4*>(p.s0) + base : nullptr;
   float4* b4 = p.s1 ? reinterpret_cast<float4*>(p.s1) + base : nullptr;
 #pragma unroll
@@ -287,7 +284,7 @@ __device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t ro
       if (c * 4 + u >= p.K1) continue;
       opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
     }
-    e4[c] = w[c];
+    tbl_store4_rt(p.emb, base + c, w[c], (uint32_t)*p.step, p.tbl_bf16 != 0);
     if (a4) a4[c] = a[c];
     if (b4) b4[c] = b[c];
   }
@@ -307,13 +304,12 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   const size_t base = (size_t)row * KP4;
   // the row's parameters and slots: issued before the searches (same as merge_apply)
   float4 w[KP4], a[KP4], b[KP4];
-  const float4* e4r = reinterpret_cast<const float4*>(p.emb) + base;
   const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
   const float4* b4r = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb) + base;
   if (p.mode == 0) {
 #pragma unroll
     for (int c = 0; c < KP4; ++c) {
-      w[c] = e4r[c];
+      w[c] = tbl_load4_rt(p.emb, base + c, p.tbl_bf16 != 0);
       a[c] = a4r[c];
       b[c] = b4r[c];
     }

@@ -68,6 +68,7 @@ struct ShardServeParams {
   float* rows_out;      // [m][Kp] (nullable: keys only)
   uint32_t* lkeys;      // [m] local row, Vs for padding (nullable: rows only)
   int32_t* bad;         // nullable: set to 1 if a request is not owned by this rank
+  int tbl_bf16;         // 1: table holds bf16 rows (rows_out stays f32)
 };
 
 void launch_shard_keys(const ShardKeysParams& p, hipStream_t stream);

@@ -18,7 +18,7 @@ __device__ __forceinline__ void shard_serve_body(const ShardServeParams& p, cons
   if (p.rows_out) {
     // load row 0 for requests this owner does not serve and zero the value: `ok ? load : 0`
     // compiled to a select between a global and a private address (flat access + scratch)
-    float4 v = reinterpret_cast<const float4*>(p.table)[(size_t)(ok ? lr : 0u) * KP4 + c];
+    float4 v = tbl_load4_rt(p.table, (size_t)(ok ? lr : 0u) * KP4 + c, p.tbl_bf16 != 0);
     if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
     reinterpret_cast<float4*>(p.rows_out)[(size_t)r * KP4 + c] = v;
   }

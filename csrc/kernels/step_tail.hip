@@ -14,12 +14,12 @@ constexpr int kTailThreads = 512;
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
-template <int KP4>
+template <int KP4, bool BT>
 __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                  const int n_emb) {
   const int bid = blockIdx.x;
   if (bid < n_emb)
-    emb_rows_body<KP4, kTailThreads>(e, bid);  // the longer role first: its workgroups dispatch first
+    emb_rows_body<KP4, kTailThreads, BT>(e, bid);  // the longer role first: its workgroups dispatch first
   else
     wgrad_body(w, bid - n_emb);
 }
@@ -32,9 +32,12 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   switch (e.Kp / 4) {
-#define ROCFM_KP4(N)                                                              \
-  case N:                                                                         \
-    hipLaunchKernelGGL(step_tail_kernel<N>, grid, block, 0, stream, w, e, n_emb); \
+#define ROCFM_KP4(N)                                                                         \
+  case N:                                                                                    \
+    if (e.tbl_bf16)                                                                          \
+      hipLaunchKernelGGL((step_tail_kernel<N, true>), grid, block, 0, stream, w, e, n_emb);  \
+    else                                                                                     \
+      hipLaunchKernelGGL((step_tail_kernel<N, false>), grid, block, 0, stream, w, e, n_emb); \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
     ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12)

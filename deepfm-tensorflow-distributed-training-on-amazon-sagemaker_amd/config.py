@@ -130,6 +130,7 @@ class Config:
     # rowshard: replicate the N most frequent ids (rank 0's first batches) on every rank; their
     # gradients ride the MLP all-reduce bucket (synchronous, same update as their owners would apply)
     hot_rows: int = 0
+    table_dtype: str = "f32"  # fused engines: f32 | bf16 embedding-table storage (f32 slots, stochastic rounding)
     dp_exchange: str = "auto"  # dp / rowshard exchange transport: auto | p2p (IPC push over xGMI, one node) | rccl
 
     # ------------------------------------------------------------------------------------
@@ -154,6 +155,8 @@ class Config:
             raise ValueError("embedding_size must be > 0")
         if self.hot_rows < 0 or (self.hot_rows and self.parallelism != "rowshard"):
             raise ValueError("hot_rows (>= 0) applies to parallelism=rowshard")
+        if self.table_dtype not in ("f32", "bf16"):
+            raise ValueError("table_dtype must be f32 or bf16")
         if self.ps_staleness not in (0, 1):
             raise ValueError("ps_staleness must be 0 or 1")
         if self.ps_staleness and self.parallelism != "rowshard":

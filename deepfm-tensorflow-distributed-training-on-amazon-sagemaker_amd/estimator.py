@@ -100,7 +100,7 @@ class Estimator:
             if self.engine_name == "fused":
                 return FusedRowShard(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                      embedding_update=cfg.embedding_update, seed=cfg.seed,
-                                     use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,
+                                     use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype,
                                      exchange=cfg.dp_exchange, staleness=cfg.ps_staleness,
                                      hot_rows=cfg.hot_rows)
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
@@ -112,12 +112,12 @@ class Estimator:
                 mode = "dense_dp" if cfg.parallelism == "dense_dp" else "dp"
                 return FusedDataParallel(self.spec, self.hp, cfg.batch_size, self.device, params=P,
                                          embedding_update=cfg.embedding_update, mode=mode, seed=cfg.seed,
-                                         use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype,
+                                         use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype,
                                          exchange=cfg.dp_exchange)
             from .models.fused import FusedDeepFM
 
             return FusedDeepFM(self.spec, self.hp, cfg.batch_size, self.device, embedding_update=cfg.embedding_update,
-                               seed=cfg.seed, params=P, use_graph=cfg.use_hip_graph, compute_dtype=cfg.compute_dtype)
+                               seed=cfg.seed, params=P, use_graph=cfg.use_hip_graph, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype)
         from .models.torch_engine import TorchDeepFM
 
         eng = TorchDeepFM(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,

@@ -112,7 +112,7 @@ class FusedDeepFM:
                  embedding_update: str = "sparse", seed: int = 1234,
                  params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
                  use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None,
-                 force_generic_kernels: bool = False, compute_dtype: str = "bf16"):
+                 force_generic_kernels: bool = False, compute_dtype: str = "bf16", table_dtype: str = "f32"):
         if len(spec.layers) > 6:
             raise ValueError("the fused engine supports at most 6 hidden layers")
         self.H = require_hip()
@@ -138,11 +138,18 @@ class FusedDeepFM:
         if compute_dtype not in ("bf16", "fp8"):
             raise ValueError(f"compute_dtype must be bf16 or fp8, got {compute_dtype!r}")
         self.compute_dtype = compute_dtype
+        # table_dtype bf16: fm_v / fm_w rows stored as bf16 (half the HBM and
+        # gather bytes; 1B rows = 24 GB instead of 48 GB), updated in f32 with stochastic rounding;
+        # optimizer slots and the exact-mode gradient table stay f32
+        if table_dtype not in ("f32", "bf16"):
+            raise ValueError(f"table_dtype must be f32 or bf16, got {table_dtype!r}")
+        self.table_dtype = table_dtype
+        self.tbl_bf16 = 1 if table_dtype == "bf16" else 0
         dev = self.device
         L = self.layout
 
         # ---- parameters + optimizer state ----------------------------------------------------
-        self.emb = torch.zeros(self.V, self.Kp, dtype=torch.float32, device=dev)
+        self.emb = torch.zeros(self.V, self.Kp, dtype=torch.bfloat16 if self.tbl_bf16 else torch.float32, device=dev)
         if params is not None:
             P = params
             self.emb[:, : self.K].copy_(P["fm_v"])
@@ -152,7 +159,9 @@ class FusedDeepFM:
             self._init_table_device(seed)
         self.dense = torch.zeros(L.total, dtype=torch.float32, device=dev)
         L.pack({k: v.to(dev) for k, v in P.items() if k not in ("fm_w", "fm_v")}, self.dense)
-        self.emb_slots = init_slots(hp, self.emb)
+        # f32 slots whatever the table dtype (an expanded scalar only carries shape / device)
+        self.emb_slots = [x.contiguous() for x in init_slots(
+            hp, torch.zeros((), dtype=torch.float32, device=dev).expand(self.V, self.Kp))]
         self.dense_slots = init_slots(hp, self.dense)
         # batch_norm: moving moments [layer][mean|var][column] (pads: mean 0, var 1) + the row
         # kernel's grid-reduction scratch (per-barrier partials, γ/β gradient sums, counters)
@@ -197,7 +206,7 @@ class FusedDeepFM:
         self.svals = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
         tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
         self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
-        self.dense_grad = (torch.zeros_like(self.emb) if embedding_update == "exact" else None)
+        self.dense_grad = (torch.zeros_like(self.emb, dtype=torch.float32) if embedding_update == "exact" else None)
         # exact mode: rows whose dense_grad holds this step's gradient carry touched[row] = step + 1,
         # so the dense update reads / clears gradient rows only there (None: read every row —
         # dense_dp, whose gradient table arrives all-reduced)
@@ -279,6 +288,7 @@ class FusedDeepFM:
         rp = H.RowsParams()
         rp.ids, rp.vals, rp.labels = ids.data_ptr(), vals.data_ptr(), labels.data_ptr()
         rp.emb = self.emb.data_ptr()
+        rp.tbl_bf16 = self.tbl_bf16
         rp.fm_bias = self.dense[L.off_fmb:].data_ptr()
         rp.w_out = self.dense[L.off_wout:].data_ptr()
         rp.b_out = self.dense[L.off_bout:].data_ptr()
@@ -354,6 +364,7 @@ class FusedDeepFM:
         ep.contrib = self.contrib.data_ptr()
         ep.K1, ep.Kp = self.K1, self.Kp
         ep.emb = self.emb.data_ptr()
+        ep.tbl_bf16 = self.tbl_bf16
         ep.s0, ep.s1 = self._slot_ptrs(self.emb_slots)
         ep.l2 = float(self.spec.l2_reg)
         ep.grad_scale = 1.0
@@ -368,6 +379,7 @@ class FusedDeepFM:
         if self.embedding_update == "exact":
             ed = H.EmbDenseParams()
             ed.emb = self.emb.data_ptr()
+            ed.tbl_bf16 = self.tbl_bf16
             ed.s0, ed.s1 = self._slot_ptrs(self.emb_slots)
             ed.dense_grad = self.dense_grad.data_ptr()
             ed.touched = self.touched.data_ptr() if self.touched is not None else 0
@@ -1041,7 +1053,7 @@ class FusedDeepFM:
         nb = 1024
         part = torch.zeros(nb, dtype=torch.float32, device=self.device)
         self.H.emb_sumsq(self.emb.data_ptr(), self.V * self.Kp // 4, self.Kp, self.K1, part.data_ptr(), nb,
-                         self.stream_ptr)
+                         self.stream_ptr, self.tbl_bf16)
         return float(self.spec.l2_reg * 0.5 * part.double().sum().item())
 
     def batch_loss(self, include_l2: bool = True) -> float:
@@ -1058,7 +1070,7 @@ class FusedDeepFM:
             nb = 1024
             part = torch.zeros(nb, dtype=torch.float32, device=self.device)
             self.H.emb_sumsq(self.emb.data_ptr(), self.V * self.Kp // 4, self.Kp, self.K1, part.data_ptr(), nb,
-                             self.stream_ptr)
+                             self.stream_ptr, self.tbl_bf16)
             v = v + self.spec.l2_reg * 0.5 * part.double().sum()
         host = torch.empty(1, dtype=torch.float64, pin_memory=True)
         host.copy_(v.view(1), non_blocking=True)
@@ -1080,7 +1092,7 @@ class FusedDeepFM:
         tf = self._tf_views(self.emb, self.dense)
         tf.update(self._bn_views())
         for k, v in tf.items():
-            sd[k] = v.detach().cpu().clone()
+            sd[k] = v.detach().float().cpu().clone()  # (a bf16 table is saved as f32: TF layout)
         names = slot_names(self.hp.name)
         for si, sn in enumerate(names):
             sv = self._tf_views(self.emb_slots[si], self.dense_slots[si])
@@ -1151,4 +1163,4 @@ class FusedDeepFM:
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
         tf = self._tf_views(self.emb, self.dense)
         tf.update(self._bn_views())
-        return OrderedDict((k, v.detach().cpu().clone()) for k, v in tf.items())
+        return OrderedDict((k, v.detach().float().cpu().clone()) for k, v in tf.items())

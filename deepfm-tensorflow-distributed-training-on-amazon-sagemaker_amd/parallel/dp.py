@@ -194,7 +194,7 @@ class FusedDataParallel:
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", mode: str = "dp", seed: int = 1234, use_graph: bool = True,
                  capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
-                 exchange: Optional[str] = None):
+                 exchange: Optional[str] = None, table_dtype: str = "f32"):
         from ..models.fused import FusedDeepFM
 
         self.world = _world()
@@ -207,7 +207,8 @@ class FusedDataParallel:
         self.exact = embedding_update == "exact"
         self.eng = FusedDeepFM(spec, hp, batch_size, device, embedding_update=embedding_update, seed=seed,
                                params=params, use_graph=False, fuse_dense_opt=False,
-                               dropout_seed=seed + 7919 * self.rank, compute_dtype=compute_dtype)
+                               dropout_seed=seed + 7919 * self.rank, compute_dtype=compute_dtype,
+                               table_dtype=table_dtype)
         e = self.eng
         self.use_graph = use_graph
         self.graph_collectives = use_graph and collectives_capturable()
@@ -287,7 +288,7 @@ class FusedDataParallel:
                 mp_.W, mp_.cap, mp_.Kp, mp_.K1 = self.world, cap, Kp, e.K1
                 mp_.key_div, mp_.Vmap = 1, e.V
                 self.maps.bind(mp_)
-                mp_.emb = e.emb.data_ptr()
+                mp_.emb, mp_.tbl_bf16 = e.emb.data_ptr(), e.tbl_bf16
                 mp_.s0, mp_.s1 = e._slot_ptrs(e.emb_slots)
                 mp_.l2, mp_.grad_scale = float(spec.l2_reg), 1.0 / self.world
                 mp_.opt, mp_.step = e._opt(p), e.steps[p:].data_ptr()
@@ -450,7 +451,7 @@ class FusedDataParallel:
                 src = self.merge_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "pos", "rep", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "overflow", "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos"):
+                          "overflow", "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos", "tbl_bf16"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 rows.zero_word = self.send[self.off_cnt:].data_ptr()

@@ -388,7 +388,8 @@ class FusedRowShard:
     def __init__(self, spec: ModelSpec, hp: OptHParams, batch_size: int, device, params=None,
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
                  capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
-                 exchange: Optional[str] = None, staleness: int = 0, hot_rows: int = 0):
+                 exchange: Optional[str] = None, staleness: int = 0, hot_rows: int = 0,
+                 table_dtype: str = "f32"):
         from ..models.fused import FusedDeepFM
 
         if staleness not in (0, 1):
@@ -418,7 +419,8 @@ class FusedRowShard:
         spec_loc = dataclasses.replace(spec, feature_size=Vs)
         self.eng = e = FusedDeepFM(spec_loc, hp, batch_size, dev, embedding_update=embedding_update, seed=seed,
                                    params=P, use_graph=False, fuse_dense_opt=False,
-                                   dropout_seed=seed + 7919 * r, compute_dtype=compute_dtype)
+                                   dropout_seed=seed + 7919 * r, compute_dtype=compute_dtype,
+                                   table_dtype=table_dtype)
         del P
         e.id_limit = self.V  # the id guard (ROCFM_CHECK_IDS) checks global ids, not local rows
         e._build_fetch()
@@ -546,6 +548,7 @@ class FusedRowShard:
         for p in range(2):
             rp = e.rows_params[p]
             rp.ids, rp.emb = self.local_idx[p].data_ptr(), self.rows_in.data_ptr()
+            rp.tbl_bf16 = 0  # the row kernel's table is the f32 received-rows buffer
             lp = e.emb_params[p]  # local: Σ lookup grads per received row → grad_stage
             lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
@@ -557,7 +560,7 @@ class FusedRowShard:
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
             op.key_div, op.Vmap = self.W, self.Vs
-            op.emb = e.emb.data_ptr()
+            op.emb, op.tbl_bf16 = e.emb.data_ptr(), e.tbl_bf16
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
             op.opt, op.step = e._opt(p), e.steps[p:].data_ptr()
@@ -574,6 +577,7 @@ class FusedRowShard:
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
         pp = e.pred_params
         pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
+        pp.tbl_bf16 = 0
         self.pred_route = self._route_params(e.pred_ids, self.pred_rsv, self.pred_send, self.pred_local,
                                              self.pred_skl, self.pred_counts, self.n)
         self.pred_route[0].n_hot = 0  # predictions read the owners' (flushed) rows
@@ -662,7 +666,7 @@ class FusedRowShard:
         srcs = [e.emb] + list(e.emb_slots)
         flat = torch.zeros(len(bufs), self.n_hot, e.Kp, dtype=torch.float32, device=self.device)
         for i, src in enumerate(srcs):
-            flat[i].index_copy_(0, slot, src.index_select(0, rows))
+            flat[i].index_copy_(0, slot, src.index_select(0, rows).float())
         if self.W > 1:
             if dist.get_backend() == "nccl":
                 all_reduce_(flat)
@@ -682,7 +686,7 @@ class FusedRowShard:
         torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
         slot, rows = self._owned_hot()
         for dst, src in zip([e.emb] + list(e.emb_slots), [self.hot_rep] + self.hot_slots):
-            dst.index_copy_(0, rows, src.index_select(0, slot))
+            dst.index_copy_(0, rows, src.index_select(0, slot).to(dst.dtype))
 
     def _recv(self, parity: int = 0) -> Optional[torch.Tensor]:
         """X1 receive buffer of a step of this parity (None: world 1, the send list is read)."""
@@ -701,6 +705,7 @@ class FusedRowShard:
         sv.ids, sv.m, sv.W, sv.rank, sv.Vs = ids.data_ptr(), self.M, self.W, self.rank, self.Vs
         sv.table, sv.Kp, sv.rows_out, sv.lkeys = e.emb.data_ptr(), e.Kp, self.rows_out.data_ptr(), 0
         sv.bad = self.bad.data_ptr()
+        sv.tbl_bf16 = e.tbl_bf16
         return sv
 
     # ---- batch feeding (delegated) ------------------------------------------------------------
@@ -976,6 +981,7 @@ class FusedRowShard:
                 routes.append(rp)
                 rows, wp, da, ep, ed = e.m_params[q][k]
                 rows.ids, rows.emb = self.ms_local[q, k].data_ptr(), self.rows_in.data_ptr()
+                rows.tbl_bf16 = 0
                 wp.grads = e.dense_grads_flat.data_ptr()
                 ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
                 ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
@@ -988,7 +994,7 @@ class FusedRowShard:
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "dense_grad", "touched"):
+                          "dense_grad", "touched", "tbl_bf16"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 par = k % 2 if self.staleness else 0
@@ -1126,7 +1132,7 @@ class FusedRowShard:
         self._flush_hot()
         nb = 1024
         part = torch.zeros(nb, dtype=torch.float32, device=self.device)
-        self.H.emb_sumsq(e.emb.data_ptr(), e.V * e.Kp // 4, e.Kp, e.K1, part.data_ptr(), nb, e.stream_ptr)
+        self.H.emb_sumsq(e.emb.data_ptr(), e.V * e.Kp // 4, e.Kp, e.K1, part.data_ptr(), nb, e.stream_ptr, e.tbl_bf16)
         t = part.double().sum().reshape(1)
         if self.W > 1:
             all_reduce_(t)
@@ -1164,8 +1170,8 @@ class FusedRowShard:
         self._flush_hot()
         out = e.parameters_tf()
         if self.W > 1:
-            out["fm_w"] = _gather_table(e.emb[:, e.K].contiguous(), self.V, self.W).cpu()
-            out["fm_v"] = _gather_table(e.emb[:, : e.K].contiguous(), self.V, self.W).cpu()
+            out["fm_w"] = _gather_table(e.emb[:, e.K].float().contiguous(), self.V, self.W).cpu()
+            out["fm_v"] = _gather_table(e.emb[:, : e.K].float().contiguous(), self.V, self.W).cpu()
         else:
             out["fm_w"], out["fm_v"] = out["fm_w"][: self.V], out["fm_v"][: self.V]
         return out
