@@ -23,6 +23,8 @@ feat_vals float32[None,F]; output prob).
 from __future__ import annotations
 
 import json
+import math
+import struct
 import os
 import re
 import shutil
@@ -201,6 +203,62 @@ def export_servable(servable_model_dir: str, params: Dict[str, torch.Tensor], mo
                   f, indent=1)
     os.replace(tmp, out)
     return out
+
+
+class StreamedServable:
+    """The same bundle as ``export_servable``, written incrementally: the dense variables at once,
+    the [V, ...] tables chunk by chunk at their final offsets (the row-sharded engine gathers one
+    row range at a time, so no rank ever holds a whole 1B-row table).  The safetensors header is
+    written first — the shapes are known — and the file is renamed into place on ``close``."""
+
+    def __init__(self, servable_model_dir: str, dense: Dict[str, torch.Tensor], table_shapes: Dict[str, tuple],
+                 model_config: dict):
+        ts = str(int(time.time()))
+        out = os.path.join(servable_model_dir, ts)
+        while os.path.exists(out):
+            ts = str(int(ts) + 1)
+            out = os.path.join(servable_model_dir, ts)
+        self.out, self.tmp = out, out + ".tmp"
+        self.config = model_config
+        os.makedirs(os.path.join(self.tmp, "variables"), exist_ok=True)
+        dense = {k: v.detach().contiguous().cpu().float() for k, v in dense.items()}
+        header, off = {}, 0
+        for k, v in dense.items():
+            n = v.numel() * 4
+            header[k] = {"dtype": "F32", "shape": list(v.shape), "data_offsets": [off, off + n]}
+            off += n
+        self.table_off = {}
+        for k, shp in table_shapes.items():
+            n = int(math.prod(shp)) * 4
+            header[k] = {"dtype": "F32", "shape": list(shp), "data_offsets": [off, off + n]}
+            self.table_off[k] = (off, int(math.prod(shp[1:])) if len(shp) > 1 else 1)
+            off += n
+        hb = json.dumps(header, separators=(",", ":")).encode()
+        hb += b" " * ((8 - len(hb) % 8) % 8)  # 8-byte aligned data start
+        self.data0 = 8 + len(hb)
+        self.path = os.path.join(self.tmp, "variables", "variables.safetensors")
+        self.fh = open(self.path, "wb")
+        self.fh.write(struct.pack("<Q", len(hb)) + hb)
+        for v in dense.values():
+            self.fh.write(v.numpy().tobytes())
+        self.fh.truncate(self.data0 + off)
+
+    def write_rows(self, name: str, row0: int, rows: torch.Tensor) -> None:
+        off, per = self.table_off[name]
+        self.fh.seek(self.data0 + off + row0 * per * 4)
+        self.fh.write(rows.detach().contiguous().cpu().float().numpy().tobytes())
+
+    def close(self) -> str:
+        self.fh.close()
+        sig = json.loads(json.dumps(SIGNATURE))
+        F = self.config.get("field_size")
+        for inp in sig["serving_default"]["inputs"].values():
+            inp["shape"] = [None, F]
+        with open(os.path.join(self.tmp, "model.json"), "w") as f:
+            json.dump({"format": "rocfm-servable-v1", "model": "DeepFM", "config": self.config, "signatures": sig},
+                      f, indent=1)
+        os.replace(self.tmp, self.out)
+        return self.out
 
 
 def load_servable(path: str):

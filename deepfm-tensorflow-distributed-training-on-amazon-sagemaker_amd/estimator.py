@@ -558,13 +558,28 @@ class Estimator:
         d = servable_model_dir or self.cfg.servable_model_dir
         if not d:
             return None
-        params = self.eng.parameters_tf()
-        if not self.info.is_chief:
-            return None
         cfgd = {"feature_size": self.cfg.feature_size, "field_size": self.cfg.field_size,
                 "embedding_size": self.cfg.embedding_size, "deep_layers": self.cfg.deep_layers,
                 "dropout": self.cfg.dropout, "batch_norm": self.cfg.batch_norm,
                 "batch_norm_decay": self.cfg.batch_norm_decay, "loss_type": self.cfg.loss_type}
+        if hasattr(self.eng, "iter_table_chunks"):
+            # row-sharded tables: streamed, one gathered row range at a time (no rank holds a
+            # whole table); the chief writes each range at its final offset
+            V, K = self.cfg.feature_size, self.cfg.embedding_size
+            w = ckpt.StreamedServable(d, self.eng.dense_parameters_tf(), {"fm_w": (V,), "fm_v": (V, K)}, cfgd) \
+                if self.info.is_chief else None
+            for a, fw, fv in self.eng.iter_table_chunks():  # collective
+                if w is not None:
+                    w.write_rows("fm_w", a, fw)
+                    w.write_rows("fm_v", a, fv)
+            if w is None:
+                return None
+            path = w.close()
+            self._log({"event": "export", "path": path})
+            return path
+        params = self.eng.parameters_tf()
+        if not self.info.is_chief:
+            return None
         path = ckpt.export_servable(d, params, cfgd)
         self._log({"event": "export", "path": path})
         return path

@@ -40,6 +40,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -164,6 +165,29 @@ def _gather_table(local: torch.Tensor, V: int, W: int) -> torch.Tensor:
     # buf[r*Vs + l] holds global id l*W + r
     full = buf.view(W, Vs, *local.shape[1:]).transpose(0, 1).reshape(W * Vs, *local.shape[1:])
     return full[:V].to(local.device)
+
+
+def iter_table_chunks(local: torch.Tensor, V: int, W: int, K: int, chunk_rows: Optional[int] = None):
+    """Collective, every rank: ``(row0, fm_w [n], fm_v [n, K])`` CPU f32 chunks of the global
+    tables in id order, from each rank's shard ``local`` [Vs, ≥K+1] (row l of rank r = id l·W + r;
+    column K = fm_w).  One row range is gathered at a time (≈chunk_rows·(K+1)·4 bytes), so a
+    1B-row table is exported without materialising it on any rank."""
+    chunk_rows = int(chunk_rows or os.environ.get("ROCFM_EXPORT_CHUNK_ROWS", 1 << 22))
+    step = max(W, chunk_rows // W * W)
+    for a in range(0, V, step):
+        b = min(V, a + step)
+        la, lb = a // W, (b + W - 1) // W
+        loc = local[la:lb, : K + 1].float().contiguous()
+        if W > 1:
+            dev_ok = dist.get_backend() == "nccl" or loc.device.type == "cpu"
+            src = loc if dev_ok else loc.cpu()
+            buf = torch.empty((W * (lb - la), K + 1), dtype=torch.float32, device=src.device)
+            dist.all_gather_into_tensor(buf, src) if dev_ok else dist.all_gather(list(buf.chunk(W)), src)
+            rows = buf.view(W, lb - la, K + 1).transpose(0, 1).reshape(-1, K + 1)[: b - a]
+        else:
+            rows = loc[: b - a]
+        rows = rows.cpu()
+        yield a, rows[:, K].contiguous(), rows[:, :K].contiguous()
 
 
 # ================================================================================================
@@ -345,6 +369,18 @@ class TorchRowShard:
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.base.load_state_dict(sd, strict=strict)
+
+    def dense_parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
+        """Every variable except the row-sharded tables (no collective)."""
+        out = self.base.parameters_tf()
+        out.pop("fm_w")
+        out.pop("fm_v")
+        return out
+
+    def iter_table_chunks(self, chunk_rows: Optional[int] = None):
+        """Collective: the full tables in id order, one gathered row range at a time."""
+        local = torch.cat([self.base.P["fm_v"], self.base.P["fm_w"].reshape(-1, 1)], 1)
+        yield from iter_table_chunks(local, self.V, self.W, self.spec.embedding_size, chunk_rows)
 
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
         """Full variables (collective: the tables are gathered from every rank)."""
@@ -1164,6 +1200,20 @@ class FusedRowShard:
         self._pre_served = False
         self._graphs = {}
         self._warm = 0
+
+    def dense_parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
+        """Every variable except the row-sharded tables (no collective)."""
+        e = self.eng
+        tf = e._tf_views(e.emb, e.dense)
+        tf.update(e._bn_views())
+        return OrderedDict((k, v.detach().float().cpu().clone()) for k, v in tf.items() if k not in ("fm_w", "fm_v"))
+
+    def iter_table_chunks(self, chunk_rows: Optional[int] = None):
+        """Collective: the full tables in id order, one gathered row range at a time (streamed
+        servable export: ``checkpoint.StreamedServable``)."""
+        self._flush_hot()
+        torch.cuda.synchronize(self.device)
+        yield from iter_table_chunks(self.eng.emb, self.V, self.W, self.eng.K, chunk_rows)
 
     def parameters_tf(self) -> "OrderedDict[str, torch.Tensor]":
         e = self.eng

@@ -38,8 +38,11 @@ def _worker(rank, world, port, data_dir, model_dir, par, out):
     ev = est.evaluate([os.path.join(data_dir, "va.tfrecords")])
     probs = est.predict([os.path.join(data_dir, "te.tfrecords")])
     full = est.eng.parameters_tf()
+    os.environ["ROCFM_EXPORT_CHUNK_ROWS"] = "300"  # row-shard export streams 7 gathered ranges
+    path = est.export(os.path.join(model_dir, "export"))
     if rank == 0:
-        torch.save({"tr": tr, "ev": ev, "probs": probs, "fm_v": full["fm_v"], "step": est.global_step}, out)
+        torch.save({"tr": tr, "ev": ev, "probs": probs, "fm_v": full["fm_v"], "step": est.global_step,
+                    "full": dict(full), "export": path}, out)
     est.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -67,6 +70,11 @@ def test_estimator_two_ranks(tmp_path, par):
     assert prefix and ckpt.checkpoint_step(prefix) == got["step"]
     sd = ckpt.load_checkpoint(prefix)  # both shards reassembled (row-shard) or the replicated table (dp)
     torch.testing.assert_close(sd["fm_v"], got["fm_v"])
+    # servable export (row-shard: streamed range by range into the bundle) ≡ the gathered variables
+    meta, params = ckpt.load_servable(got["export"])
+    assert set(params) == set(got["full"])
+    for k, v in got["full"].items():
+        torch.testing.assert_close(params[k], v.float())
     # a single-process estimator restores it
     from rocfm.config import parse_flags
     from rocfm.estimator import Estimator

@@ -168,6 +168,10 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     torch.cuda.synchronize()
     eng.check()
     P = eng.parameters_tf()
+    # the streamed export's row ranges reassemble the gathered tables
+    fw = torch.cat([c[1] for c in eng.iter_table_chunks(chunk_rows=700)])
+    fv = torch.cat([c[2] for c in eng.iter_table_chunks(chunk_rows=700)])
+    assert torch.equal(fw, P["fm_w"]) and torch.equal(fv, P["fm_v"])
     ids, vals, _ = _batches(100, 1, 5)[0]
     p, _ = eng.predict_batch(ids.cuda() if rank == 0 else ids[:0].cuda(), vals.cuda() if rank == 0 else vals[:0].cuda())
     if hot:
