@@ -105,8 +105,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParam
 // One thread per source entry; only representatives (lowest rank holding the key) do work.
 // WMAX = 8 (one node): every later source's position and row are loaded before any is summed.
 template <int KP4, int WMAX>
-__global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams p) {
-  const int i = blockIdx.x * kApplyThreads + threadIdx.x;
+__device__ __forceinline__ void merge_maps_body(const MergeParams& p, const int i) {
   if (i >= p.W * p.cap) return;
   const int r = i / p.cap, j = i - r * p.cap;
   const uint32_t key = p.keys[(size_t)r * p.key_stride + j];
@@ -236,6 +235,11 @@ __global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams 
     if (a4) a4[c] = a[c];
     if (b4) b4[c] = b[c];
   }
+}
+
+template <int KP4, int WMAX>
+__global__ __launch_bounds__(kApplyThreads) void merge_apply_kernel(MergeParams p) {
+  merge_maps_body<KP4, WMAX>(p, blockIdx.x * kApplyThreads + threadIdx.x);
 }
 
 // merge_scatter with the DP MLP optimizer (dense_apply over the gathered rank segments) as extra
@@ -451,7 +455,10 @@ __global__ __launch_bounds__(kApplyThreads) void merge_search_apply_kernel(Merge
                                                                            int n_apply, int n_dense, int n_serve) {
   const int b = blockIdx.x;
   if (b < n_apply) {
-    merge_search_body<KP4, WMAX>(p, b * kApplyThreads + threadIdx.x);
+    if (p.use_maps)  // maps filled by a merge_scatter launch (larger worlds)
+      merge_maps_body<KP4, WMAX>(p, b * kApplyThreads + threadIdx.x);
+    else
+      merge_search_body<KP4, WMAX>(p, b * kApplyThreads + threadIdx.x);
   } else if (b < n_apply + n_dense) {
     dense_apply_body<kApplyThreads>(d, b - n_apply, n_dense);
   } else if (b < n_apply + n_dense + n_serve) {
@@ -542,6 +549,7 @@ void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, 
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge: bad Kp");
   ROCFM_REQUIRE((long long)p.W * p.cap < (1ll << 31), "merge: W*cap overflows int32");
   ROCFM_REQUIRE(p.key_div >= 1 && p.keys && p.rows && p.step, "merge: keys / rows / step missing");
+  if (p.use_maps) check(p);  // maps mode: validated as merge_apply
   ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : p.emb != nullptr, "merge_search_apply: missing outputs");
   ROCFM_REQUIRE(sv == nullptr || (sv->Kp % 4 == 0 && sv->Kp > 0 && sv->ids && sv->table),
                 "merge_search_apply: bad serve params");

@@ -77,6 +77,10 @@ def _all_reduce(t: torch.Tensor) -> None:
     t.copy_(c)
 
 
+# Up to this many ranks the merge binary-searches the sorted source lists (one launch, no maps);
+# beyond it a scatter into position maps + apply is faster (tools/bench_merge.py on one MI355X,
+# 7.5k keys per rank: W=1 3.9 vs 8.9 µs, W=2 9.8 vs 10.0, W=4 12.8 vs 10.0, W=8 20.6 vs 13.7)
+SEARCH_MAX_W = 2
 MERGE_MAP_BUDGET = 512 << 20  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
 
 
@@ -418,7 +422,7 @@ class FusedDataParallel:
         e, H = self.eng, self.eng.H
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
-        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp()
+        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and self.world <= SEARCH_MAX_W
         e._build_multi(Smax, heads=self.m_sorted)
         e._m_pool = e.pool_ids
         S_, n = e.mS, e.n_lookup

@@ -15,9 +15,10 @@ of HBM).  Every step, synchronously:
             each lookup's received-row index as its id; the lookup gradients are reduced per
             received row (emb_update.hip mode 1)
     X3      all_to_all  row gradients back to owners   [W, cap, K+1] f32
-    update  owners sum each requested row's gradients over source ranks in rank order (one
-            launch, merge.hip search mode: every request list is ascending, so each entry finds
-            its row in the other lists by binary search — no maps, no sort), apply lazy L2 once
+    update  owners sum each requested row's gradients over source ranks in rank order (merge.hip:
+            up to dp.SEARCH_MAX_W ranks one launch — every request list is ascending, so each
+            entry finds its row in the other lists by binary search, no maps; larger worlds
+            scatter into position maps first, then apply), apply lazy L2 once
             and the row optimizer (or, ``embedding_update=exact``, the dense full-table update of
             the shard — the reference's full L2, with no dense traffic at all); the MLP optimizer
             rides as extra workgroups of the same launch
@@ -545,6 +546,12 @@ class FusedRowShard:
             if self.staleness:
                 self.recv_pair = [self.recv_ids, torch.full((M,), PAD, **i32)]
         self._p2p_params = {}
+        # owner merge: binary search in the sorted request lists (small worlds), or position maps
+        # filled by a scatter launch (direct addressing over the local rows, or a W·cap hash table
+        # for very large shards) — see dp.SEARCH_MAX_W
+        from .dp import SEARCH_MAX_W, MergeMaps
+
+        self.maps = MergeMaps(W, cap, Vs, dev) if W > SEARCH_MAX_W else None
         self.rows_x = self.rows_in[:M]  # the X2 all-to-all part of rows_in
         self.hot_rep = self.rows_in[M:]  # the replica
         self.hot_slots = [torch.zeros(NH, Kp, **f32) for _ in e.emb_slots] if NH else []
@@ -559,6 +566,8 @@ class FusedRowShard:
         self._graphs: Dict = {}
         self._warm = 0
         self._build()
+        if self.maps is not None:
+            H.merge_init(self.owner_params[0], e.stream_ptr)
 
     # ---- kernel parameter blocks ------------------------------------------------------------------
     def _route_params(self, ids, rsv, send, local, skl, counts, n):
@@ -596,6 +605,9 @@ class FusedRowShard:
             op.counts = 0
             op.W, op.cap, op.Kp, op.K1 = self.W, self.cap, e.Kp, e.K1
             op.key_div, op.Vmap = self.W, self.Vs
+            if self.maps is not None:
+                self.maps.bind(op)
+                op.use_maps = 1
             op.emb, op.tbl_bf16 = e.emb.data_ptr(), e.tbl_bf16
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
@@ -813,6 +825,8 @@ class FusedRowShard:
     def _phase_update(self, p: int) -> None:
         e, H = self.eng, self.H
         s = e.stream_ptr
+        if self.maps is not None:
+            H.merge_scatter(self.owner_params[p], s)
         H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], s, None,
                              self.hot_params[p])  # owner merge ‖ MLP opt ‖ replicated rows
         if self.embedding_update == "exact":
@@ -897,6 +911,8 @@ class FusedRowShard:
         self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
         self._allreduce_mlp()                                                   # X4 MLP grads
         self._exchange(self._recv(1 - p), self.send_ids[1 - p])                 # X1 of the next step
+        if self.maps is not None:
+            H.merge_scatter(self.owner_params[p], e.stream_ptr)
         H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], e.stream_ptr, self.serve[1 - p],
                              self.hot_params[p])
         if self.embedding_update == "exact":
@@ -1030,7 +1046,8 @@ class FusedRowShard:
                 src = self.owner_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "emb", "s0", "s1", "l2", "grad_scale", "mode",
-                          "dense_grad", "touched", "tbl_bf16"):
+                          "dense_grad", "touched", "tbl_bf16", "pos", "rep", "hash_slots", "hkeys", "hrep",
+                          "hpos", "use_maps"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 par = k % 2 if self.staleness else 0
@@ -1066,6 +1083,8 @@ class FusedRowShard:
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
             self._allreduce_mlp()                                               # X4 MLP grads
+            if self.maps is not None:
+                H.merge_scatter(mg, s)                                          # (larger worlds)
             if st and k + 1 < S:  # owner merge ‖ MLP opt ‖ serve of step k+1
                 self._exchange(self._recv(1 - par), self.ms_send[q, k + 1])     # X1 of step k+1
                 H.merge_search_apply(mg, da, s, self.ms_steps[q][k + 1][6], hot)
@@ -1197,6 +1216,8 @@ class FusedRowShard:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
         self._load_hot()
+        if self.maps is not None:
+            self.maps.reset()  # the hash merge tags words with the step, which just moved
         self._pre_served = False
         self._graphs = {}
         self._warm = 0

@@ -1,0 +1,81 @@
+"""Microbenchmark of the multi-rank row merge (merge.hip) at world sizes 1-8 on ONE GPU.
+
+W rank exports are synthesised from W synthetic Criteo-shape batches (unique ids of each batch,
+ascending — the sorted DP export), laid out like the gathered receive buffer; the two merges are
+timed on them with HIP events: the search mode (one launch, binary search in the other lists) and
+the map mode (scatter into W×V position maps, then apply).  Both write a dense gradient table
+(mode 1) so repeated launches leave the inputs unchanged.
+
+    python tools/bench_merge.py [--V 1000000] [--B 1024] [--iters 200]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rocfm.data.synthetic import SyntheticCriteo  # noqa: E402
+from rocfm.ops import require_hip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--V", type=int, default=1_000_000)
+    ap.add_argument("--B", type=int, default=1024)
+    ap.add_argument("--F", type=int, default=39)
+    ap.add_argument("--Kp", type=int, default=12)
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    H = require_hip()
+    dev = torch.device("cuda")
+    gen = SyntheticCriteo(a.V, a.F, seed=1)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for W in (1, 2, 4, 8):
+        lists = [torch.unique(gen.batch(a.B, dev, g)[0].flatten().to(torch.int64)) for _ in range(W)]
+        cap = (max(len(x) for x in lists) + 3) // 4 * 4
+        keys = torch.full((W, cap), 0xFFFFFFFF, dtype=torch.int64)
+        for r, x in enumerate(lists):
+            keys[r, : len(x)] = x.cpu()
+        keys32 = torch.from_numpy(keys.numpy().astype(np.uint32).view(np.int32)).to(dev)  # pads = 0xFFFFFFFF
+        counts = torch.tensor([len(x) for x in lists], dtype=torch.int32, device=dev)
+        rows = torch.randn(W, cap, a.Kp, device=dev)
+        dg = torch.zeros(a.V, a.Kp, device=dev)
+        touched = torch.zeros(a.V, dtype=torch.int32, device=dev)
+        step = torch.zeros(1, dtype=torch.int64, device=dev)
+        pos = torch.full((W * a.V,), -1, dtype=torch.int32, device=dev)
+        rep = torch.full((a.V,), W, dtype=torch.int32, device=dev)
+        p = H.MergeParams()
+        p.keys, p.key_stride = keys32.data_ptr(), cap
+        p.rows, p.row_stride = rows.data_ptr(), cap * a.Kp
+        p.counts, p.count_stride = counts.data_ptr(), 1
+        p.W, p.cap, p.Kp, p.K1 = W, cap, a.Kp, a.Kp - 1
+        p.key_div, p.Vmap = 1, a.V
+        p.pos, p.rep = pos.data_ptr(), rep.data_ptr()
+        p.mode, p.dense_grad, p.touched, p.step = 1, dg.data_ptr(), touched.data_ptr(), step.data_ptr()
+        p.emb = dg.data_ptr()  # merge_apply loads the table row in every mode (any valid [V][Kp] f32)
+        p.grad_scale = 1.0 / W
+        s = torch.cuda.current_stream().cuda_stream
+        res = {}
+        for name in ("search", "maps"):
+            def run():
+                if name == "search":
+                    H.merge_search_apply(p, None, s)
+                else:
+                    H.merge_scatter(p, s)
+                    H.merge_apply(p, s)
+            for _ in range(10):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            res[name] = e0.elapsed_time(e1) * 1000 / a.iters
+        print(f"W={W} cap={cap} entries={W * cap}: search {res['search']:.2f} us, maps {res['maps']:.2f} us")
+
+
+if __name__ == "__main__":
+    main()
