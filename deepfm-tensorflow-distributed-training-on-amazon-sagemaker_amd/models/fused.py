@@ -800,20 +800,29 @@ class FusedDeepFM:
                 graphs[key + (q, S, "side")], graphs[key + (q, S, "main")] = gs, gm
         if capture_only:
             return
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            if eager:
-                self._prepare_multi(q, S, side)
-            else:
-                gs.replay()
-        ev = torch.cuda.Event()
-        ev.record(side)
-        if self._m_side_ev is not None:
-            main.wait_event(self._m_side_ev)
         if eager:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._prepare_multi(q, S, side)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            if self._m_side_ev is not None:
+                main.wait_event(self._m_side_ev)
             body(q, S)
         else:
+            # main graph submitted first: its kernels start while the host is still submitting the
+            # side graph (a timed window otherwise begins with the side graph's whole submission);
+            # the side graph still waits only for the main work queued BEFORE this main graph
+            before = torch.cuda.Event()
+            before.record(main)
+            if self._m_side_ev is not None:
+                main.wait_event(self._m_side_ev)
             gm.replay()
+            side.wait_event(before)
+            with torch.cuda.stream(side):
+                gs.replay()
+            ev = torch.cuda.Event()
+            ev.record(side)
         self._m_side_ev = ev
         self._m_warm += 1
         self._mq ^= 1
