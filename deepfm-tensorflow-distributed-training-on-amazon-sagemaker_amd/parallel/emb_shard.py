@@ -693,8 +693,10 @@ class FusedRowShard:
     def _choose_hot(self, ids: torch.Tensor) -> None:
         """Pick the hot_rows most frequent ids of these batches (rank 0's choice wins)."""
         u, c = torch.unique(ids.flatten().to(torch.int64), return_counts=True)
-        top = torch.topk(c, min(self.NH, u.numel())).indices
-        self.set_hot_ids(u[top].cpu())
+        # count descending, ties to the lower id (stable sort over the ascending unique ids):
+        # the same hot set on every run
+        order = torch.argsort(c.cpu(), descending=True, stable=True)[: self.NH]
+        self.set_hot_ids(u.cpu()[order])
 
     def _owned_hot(self):
         """(replica slots, local rows) of the replicated ids this rank owns."""

@@ -346,7 +346,7 @@ def test_rowshard_hot_rows_world1_equals_single(update, mode):
     eng.check()
     ref = _single(update, n)
     got, exp = eng.parameters_tf(), ref.parameters_tf()
-    _assert_params_close(got, exp, 2e-5)
+    _assert_params_close(got, exp, 2e-5, frac_max=1e-2)
     sd, sr = eng.state_dict(), ref.state_dict()
     for k in [k for k in sr if k.startswith("fm_")]:  # tables and their optimizer slots
         torch.testing.assert_close(sd[k], sr[k], rtol=2e-3, atol=2e-5)
