@@ -64,9 +64,12 @@ constexpr int kWaves = kRowThreads / 64;
 // Bt + (nt*16 + (lane&15))*ldb + ks + 8*(lane>>4).  Every batch issues KU k-steps × NTW tiles of
 // 16-B loads before the first MFMA; out-of-range k-steps load a clamped (valid) address and are
 // zeroed on the VALUE (no per-load predication — cdna guide §5 trap (c)).
+// Bs (nullable): the same matrix in the frag_swz layout — every B fragment is then one 1 KiB
+// contiguous read instead of 16 strided row pieces (the runtime-shape kernel's weight traffic).
 template <int NTW, int KU>
 __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const uint16_t* Bt, int ldb, int ntiles,
-                                             int nt0, int step, int Kd, int lane, f32x4 (&acc)[NTW]) {
+                                             int nt0, int step, int Kd, int lane, f32x4 (&acc)[NTW],
+                                             const uint16_t* Bs = nullptr) {
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
@@ -74,8 +77,10 @@ __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const u
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
     const int nt = min(nt0 + step * j, ntiles - 1);
-    bp[j] = Bt + (size_t)(nt * 16 + (lane & 15)) * ldb + 8 * (lane >> 4);
+    bp[j] = Bs ? Bs + frag_at(nt, 0, ldb, lane) : Bt + (size_t)(nt * 16 + (lane & 15)) * ldb + 8 * (lane >> 4);
   }
+  // consecutive k-steps of one swizzled tile are 512 elements apart; of the row-major matrix, 32
+  const int kstride = Bs ? 512 / 32 : 1;
   const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int k0 = 0; k0 < Kd; k0 += 32 * KU) {
     bf16x8 a[KU], b[NTW][KU];
@@ -83,7 +88,7 @@ __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const u
     for (int u = 0; u < KU; ++u) {
       const int ks = min(k0 + 32 * u, Kd - 32);
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) b[j][u] = ld_frag(bp[j] + ks);
+      for (int j = 0; j < NTW; ++j) b[j][u] = ld_frag(bp[j] + (size_t)ks * kstride);
     }
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
@@ -555,7 +560,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         }
       } else {
         f32x4 accs[1];
-        rowtile_gemm<1, 16>(A, lda, p.WT[l], Din, ntiles, nt, kWaves, Din, lane, accs);
+        rowtile_gemm<1, 16>(A, lda, p.WT[l], Din, ntiles, nt, kWaves, Din, lane, accs, p.WTs[l]);
         acc = accs[0];
       }
       const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
@@ -856,7 +861,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         }
         (void)zero8;
       } else {
-        rowtile_gemm<NJ, 4>(dz_cur, ldz, p.Wb[li], Dout, ntiles, nt0, kWaves, Dout, lane, accs);
+        rowtile_gemm<NJ, 4>(dz_cur, ldz, p.Wb[li], Dout, ntiles, nt0, kWaves, Dout, lane, accs, p.Wbs[li]);
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
