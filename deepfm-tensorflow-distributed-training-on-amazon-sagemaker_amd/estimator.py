@@ -103,6 +103,8 @@ class Estimator:
                                      use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype,
                                      exchange=cfg.dp_exchange, staleness=cfg.ps_staleness,
                                      hot_rows=cfg.hot_rows)
+            if cfg.ps_staleness or cfg.hot_rows or cfg.table_dtype != "f32":
+                raise ValueError("ps_staleness / hot_rows / table_dtype=bf16 need the fused engine (a GPU)")
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
                                  seed=cfg.seed)
         if self.engine_name == "fused":
@@ -120,6 +122,8 @@ class Estimator:
                                seed=cfg.seed, params=P, use_graph=cfg.use_hip_graph, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype)
         from .models.torch_engine import TorchDeepFM
 
+        if cfg.table_dtype != "f32":
+            raise ValueError("table_dtype=bf16 needs the fused engine (a GPU)")
         eng = TorchDeepFM(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,
                           seed=cfg.seed, dropout_seed=cfg.seed + 7919 * self.info.rank)
         if self.world > 1:

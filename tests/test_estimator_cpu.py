@@ -166,3 +166,11 @@ def test_tensorboard_event_files(data_dir, tmp_path):
     assert b == (b"\x09" + np.float64(1.5).tobytes() + b"\x10\x07" + b"\x2a\x0a\x0a\x08\x0a\x01x\x15"
                  + np.float32(2.0).tobytes())
     assert len(frame(b)) == len(b) + 16
+
+
+def test_fused_only_options_fail_loudly_on_the_torch_engine(data_dir, tmp_path):
+    """Options only the fused engines implement are refused on the eager engine (not ignored)."""
+    for kw in ({"table_dtype": "bf16"}, {"parallelism": "rowshard", "hot_rows": 8},
+               {"parallelism": "rowshard", "ps_staleness": 1}):
+        with pytest.raises(ValueError):
+            Estimator(_cfg(data_dir, str(tmp_path / "m"), **kw))
