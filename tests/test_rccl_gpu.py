@@ -114,6 +114,17 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
     assert "falling back" not in log, log[-2000:]
 
 
+@pytest.mark.parametrize("extra", [[], ["--hot_rows", "256", "--ps_staleness", "1"]])
+def test_bench_rehearsal_4_ranks_rowshard(extra):
+    """The PS-equivalent bench at 4 ranks sharing the GPU: p2p all-to-alls, owner merge through
+    position maps (W > SEARCH_MAX_W), optionally replicated hot rows and bounded staleness."""
+    j, log = _bench(["--gpus", "4", "--parallelism", "rowshard", "--steps", "32", "--warmup", "8",
+                     "--steps_per_graph", "16"] + extra, {"ROCFM_BENCH_BACKEND": "gloo"})
+    assert j["n_gpus"] == 4 and j["config"]["parallelism"] == "rowshard4", j
+    assert j["config"]["exchange"] == "p2p", (j, log[-2000:])
+    assert j["value"] > 0 and "falling back" not in log, log[-2000:]
+
+
 @pytest.mark.parametrize("par", ["dp", "rowshard"])
 def test_bench_nccl_world1_forced_collectives(par):
     """The bench's RCCL path at world 1: nccl process group, collectives captured in the graphs."""
