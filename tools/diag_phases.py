@@ -35,7 +35,8 @@ def main():
     generic = os.environ.get("GENERIC", "0") == "1"  # runtime-shape row kernel (the only one with stamps
     #                                                   besides the 39x10 128-64-32 training kernel)
     dev = torch.device("cuda")
-    spec = ModelSpec(V, 39, K, [128, 64, 32], [0.5] * 3, l2_reg=1e-4)
+    layers = [int(x) for x in os.environ.get("LAYERS", "128,64,32").split(",")]
+    spec = ModelSpec(V, 39, K, layers, [0.5] * len(layers), l2_reg=1e-4)
     eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=False,
                       force_generic_kernels=generic)
     gen = SyntheticCriteo(V, 39, seed=1)
