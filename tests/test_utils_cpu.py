@@ -92,3 +92,24 @@ def test_id_guard(monkeypatch):
     check_ids(torch.tensor([[0, 5]]), 6)
     with pytest.raises(ValueError):
         check_ids(torch.tensor([[0, 6]]), 6)
+
+
+def test_rank_info_from_env(monkeypatch):
+    """torchrun env (RANK / WORLD_SIZE / LOCAL_*) and the SageMaker host list (SM_HOSTS,
+    SM_CURRENT_HOST — what the reference's dead set_dist_env read) → rank / host layout."""
+    from rocfm.parallel.dist import rank_info_from_env
+
+    monkeypatch.setenv("RANK", "5")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    monkeypatch.delenv("SM_HOSTS", raising=False)
+    r = rank_info_from_env()
+    assert (r.rank, r.world, r.local_rank, r.local_world, r.host_index, r.num_hosts) == (5, 8, 1, 4, 1, 2)
+    assert not r.is_chief and r.distributed
+    monkeypatch.setenv("SM_HOSTS", '["algo-1", "algo-2"]')
+    monkeypatch.setenv("SM_CURRENT_HOST", "algo-2")
+    r = rank_info_from_env()
+    assert r.num_hosts == 2 and r.host_index == 1
+    r = rank_info_from_env(worker_per_host=2)
+    assert r.local_world == 2
