@@ -29,6 +29,8 @@ def report(name, st, idx, labels):
 
 
 def main():
+    # MULTI=1: stamps from the multi-step graph path (step_tail's fused wgrad + embedding roles);
+    # default: the per-step path (separate mlp_wgrad / emb_rows_update launches)
     B = int(os.environ.get("B", "1024"))
     V = int(os.environ.get("V", "1000000"))
     K = int(os.environ.get("K", "10"))
@@ -37,7 +39,8 @@ def main():
     dev = torch.device("cuda")
     layers = [int(x) for x in os.environ.get("LAYERS", "128,64,32").split(",")]
     spec = ModelSpec(V, 39, K, layers, [0.5] * len(layers), l2_reg=1e-4)
-    eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=False,
+    multi = os.environ.get("MULTI", "0") == "1"  # the multi-step graph path (fused step_tail)
+    eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=multi,
                       force_generic_kernels=generic)
     gen = SyntheticCriteo(V, 39, seed=1)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -50,7 +53,7 @@ def main():
     nrows = eng.Bp // 16
     s_rows = torch.zeros(nrows * 16, dtype=torch.int64, device=dev)
     s_wg = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
-    s_emb = torch.zeros(((eng.n_lookup + 255) // 256) * 16, dtype=torch.int64, device=dev)
+    s_emb = torch.zeros(((eng.n_lookup + 255) // 256) * 16, dtype=torch.int64, device=dev)  # ≥ per-chunk slots
     for p in range(2):
         eng.rows_params[p].stamps = s_rows.data_ptr()
         eng.wgrad_params[p].stamps = s_wg.data_ptr()
@@ -58,9 +61,20 @@ def main():
     abl = int(os.environ.get("ABLATE", "0"))
     for p in range(2):
         eng.rows_params[p].ablate = abl
+    if multi:
+        eng.train_steps(8, 4)  # builds the multi-step parameter blocks
+        for q in range(2):
+            for k in range(eng.mS):
+                rows, wp, _, ep, _ = eng.m_params[q][k]
+                rows.stamps, wp.stamps, ep.stamps = s_rows.data_ptr(), s_wg.data_ptr(), s_emb.data_ptr()
+                rows.ablate = abl
+        eng._m_graphs = {}  # recapture with the stamp pointers
     for _ in range(3):
         s_rows.zero_(); s_wg.zero_(); s_emb.zero_()
-        eng.train_step()
+        if multi:
+            eng.train_steps(4, 4)
+        else:
+            eng.train_step()
         torch.cuda.synchronize()
     print("ablate", abl)
     report("deepfm_rows", s_rows.view(-1, 16).cpu(), [0, 1, 2, 3, 4, 5, 9, 10, 11, 12],
