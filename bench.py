@@ -262,6 +262,7 @@ def main():
             "ps_staleness": a.ps_staleness if parallelism == "rowshard" else None,
             "hot_rows": a.hot_rows if parallelism == "rowshard" else None,
             "exchange": getattr(eng, "exchange", None) if pg else None,
+            "fused_push": bool(getattr(eng, "fused_push", False)) if pg else None,
         },
         "world_size": dist.get_world_size() if pg else 1,
         "backend": (dist.get_backend() if pg else None),

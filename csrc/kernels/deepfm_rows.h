@@ -2,6 +2,7 @@
 #pragma once
 #include "../common.h"
 #include "optim.h"
+#include "push.h"
 
 namespace rocfm {
 
@@ -74,6 +75,7 @@ struct RowsParams {
   float* bn_grad;                     // [nl][2][bn_dmax]: Σ dy·x̂ (d γ), Σ dy (d β) of the batch
   unsigned* bn_sync;                  // [2] grid-barrier arrival / exit counters (0 between launches)
   int* bn_error;                      // set if a grid barrier timed out (the host check raises)
+  PushTarget push;                    // DP fused push (push.h): workgroup 0 signals "entered"
 };
 
 struct WgradParams {
@@ -102,6 +104,7 @@ struct WgradParams {
   const float* bn_grad;        // [nl][2][bn_dmax] (written by deepfm_rows)
   int bn_dmax;
   int off_gamma[kMaxHidden], off_beta[kMaxHidden];
+  PushTarget push;  // DP fused push (fuse_opt == 0): gradients go straight into the W receive slots
 };
 
 struct DenseApplyParams {

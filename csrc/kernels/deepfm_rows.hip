@@ -251,6 +251,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   ROWS_STAMP(0);
   if (p.zero_word != nullptr && blockIdx.x == 0 && t == 0) *p.zero_word = 0;
+  // DP fused push: the previous merge (last reader of this rank's receive slots) is done
+  if (p.push.W > 0 && blockIdx.x == 0 && t == 0) push_signal_ready(p.push);
 
   // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
   // The ids are the head of the kernel's latency chain (ids → gathered rows): their loads are

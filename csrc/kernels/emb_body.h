@@ -55,6 +55,13 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const int i = c0 + t;
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
+  // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
+  const bool push = p.mode == 2 && p.push.W > 0;
+  uint32_t push_n = 0, push_seen = 0;
+  if (push) {
+    push_n = push_exchange_no(p.push);
+    push_seen = push_ready_load(p.push, push_n);
+  }
   // sorted export (mode 2 + chunk_heads): this chunk's output base and the batch's total, from the
   // side chain's per-chunk head counts (loaded with the keys; reduced below with the head compaction)
   int hb_before = 0, hb_total = 0;
@@ -212,6 +219,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   //    continuation), then the optimizer on a float4 of the table row; every thread issues its
   //    table/slot loads for up to 4 items before using any.
   const int nitems = nh * KP4;
+  if (push) push_wait_ready(p.push, push_n, push_seen);
   for (int base = 0; base < nitems; base += kChunk * 4) {
     float4 w[4], a[4], b[4], g[4];
     uint32_t kk[4];
@@ -252,8 +260,17 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       if (p.mode == 2) {
         const int slot = s_out_base + r;
         if (slot < p.out_cap) {
-          reinterpret_cast<float4*>(p.out_rows)[(size_t)slot * KP4 + u4] = g[u];  // pad columns are 0
-          if (u4 == 0) p.out_keys[slot] = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
+          const uint32_t row_id = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
+          if (push) {  // this rank's slot in every receive buffer (xGMI stores under the tail)
+            for (int d = 0; d < p.push.W; ++d) {
+              float* b = p.push.slot[d];
+              reinterpret_cast<float4*>(b + p.push_off_rows)[(size_t)slot * KP4 + u4] = g[u];
+              if (u4 == 0) reinterpret_cast<uint32_t*>(b + p.push_off_keys)[slot] = row_id;
+            }
+          } else {
+            reinterpret_cast<float4*>(p.out_rows)[(size_t)slot * KP4 + u4] = g[u];  // pad columns are 0
+            if (u4 == 0) p.out_keys[slot] = row_id;
+          }
         }
       } else if (p.mode == 1) {
         const uint32_t rr = (uint32_t)(idx4[u] / KP4);
@@ -280,6 +297,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       }
     }
   }
+  if (push) push_drain();
   __syncthreads();
   ROCFM_STAMP(p.stamps, 4);
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include "../common.h"
 #include "optim.h"
+#include "push.h"
 
 namespace rocfm {
 
@@ -46,6 +47,10 @@ struct EmbUpdateParams {
   uint32_t hot_base;
   int n_hot;
   int tbl_bf16;  // 1: emb holds bf16 rows (stochastic-rounded updates, common.h)
+  // mode 2 with push.W > 0: keys / rows are stored into the W receive slots (push.h) at these
+  // float offsets instead of out_keys / out_rows; the count still goes to out_count (local)
+  PushTarget push;
+  int push_off_keys, push_off_rows;
 };
 
 struct EmbDenseParams {

@@ -6,6 +6,16 @@ namespace rocfm {
 
 namespace {
 
+// A gradient of the flat dense buffer: the local grads buffer, or (fused DP push) this rank's slot
+// in every receive buffer — the MLP gradients lead each slot, as they lead the send buffer.
+__device__ __forceinline__ void put_grad(const WgradParams& p, int idx, float g) {
+  if (p.push.W > 0) {
+    for (int d = 0; d < p.push.W; ++d) p.push.slot[d][idx] = g;
+  } else {
+    p.grads[idx] = g;
+  }
+}
+
 __device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, int idx, float g) {
   if (p.fuse_opt) {
     float w = p.params[idx], a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
@@ -14,7 +24,7 @@ __device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, in
     if (p.s0) p.s0[idx] = a;
     if (p.s1) p.s1[idx] = b;
   } else {
-    p.grads[idx] = g;
+    put_grad(p, idx, g);
   }
 }
 
@@ -38,6 +48,13 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
   const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int Bp = p.Bp;
+  // fused DP push: the peers' "entered" flags are read now, long before the stores that need them
+  const bool push = !p.fuse_opt && p.push.W > 0;
+  uint32_t push_n = 0, push_seen = 0;
+  if (push) {
+    push_n = push_exchange_no(p.push);
+    push_seen = push_ready_load(p.push, push_n);
+  }
   ROCFM_STAMP(p.stamps, 0);
 
   if (bid < n_tiles) {
@@ -86,8 +103,10 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
       idx[e] = p.offW[li] + (ti * 32 + il[e]) * Dout + to * 32 + ol[e];
     }
     if (!p.fuse_opt) {
+      if (push) push_wait_ready(p.push, push_n, push_seen);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) p.grads[idx[e]] = g[e];
+      for (int e = 0; e < 2; ++e) put_grad(p, idx[e], g[e]);
+      if (push) push_drain();
     } else {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -140,13 +159,16 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
     }
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
+    if (push) push_wait_ready(p.push, push_n, push_seen);
     if (sub == 0) emit(p, st, p.offb[li] + o, s * p.grad_scale);
+    if (push) push_drain();
     return;
   }
   // output layer: dW_out[c] = Σ_b h[c][b]·g[b]; d b_out = d fm_bias = Σ_b g[b]
   {
     const int Dn = p.dims[p.nl];
     const uint16_t* H = p.actT[p.nl];
+    if (push) push_wait_ready(p.push, push_n, push_seen);
     for (int c0 = 0; c0 < Dn; c0 += 32) {
       const int c = min(c0 + (t >> 4), Dn - 1);
       const uint16_t* row = H + (size_t)c * Bp;
@@ -182,6 +204,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
           emit(p, st, p.off_beta[l] + c, p.bn_grad[(size_t)(2 * l + 1) * p.bn_dmax + c] * p.grad_scale);
         }
     }
+    if (push) push_drain();
   }
 }
 

@@ -50,6 +50,9 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
                             embedding_update=update, mode=mode,
                             use_graph=spg > 0, exchange=exchange)
     assert eng.exchange == exchange or mode == "dense_dp", eng.exchange
+    # p2p dp: the tail's producers push into the peers' slots unless ROCFM_DP_PUSH=0
+    want_fused = exchange == "p2p" and mode == "dp" and os.environ.get("ROCFM_DP_PUSH", "1") != "0"
+    assert eng.fused_push == want_fused, (eng.fused_push, want_fused)
     batches = _batches(world * B, steps, 11)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
             for b in batches]
@@ -83,6 +86,14 @@ def test_fused_dp_world4_p2p_graphs(tmp_path, update):
     """4 ranks on one GPU: the p2p push fans out to 3 peers and the merge sums 4 rank lists (the
     W>2 paths the 8-GPU node runs), through multi-step graphs."""
     _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
+
+
+@pytest.mark.parametrize("world,spg", [(2, 0), (4, 4)])
+def test_fused_dp_p2p_unfused_push(tmp_path, monkeypatch, world, spg):
+    """ROCFM_DP_PUSH=0: the tail writes the local send buffer and the push launch copies all of it
+    (the path before producer-side pushing) ≡ the single-GPU union batch."""
+    monkeypatch.setenv("ROCFM_DP_PUSH", "0")
+    _check_dp_vs_single(tmp_path, world, "dp", "p2p", 11 if spg else 3, spg, "sparse")
 
 
 def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update):

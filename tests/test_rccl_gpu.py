@@ -108,7 +108,7 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
     j, log = _bench(["--gpus", "4", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
                     {"ROCFM_BENCH_BACKEND": "gloo"})
     assert j["n_gpus"] == 4 and j["world_size"] == 4 and j["backend"] == "gloo", j
-    assert j["config"]["exchange"] == "p2p", (j, log[-2000:])
+    assert j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is True, (j, log[-2000:])
     assert j["config"]["parallelism"] == "dp4" and j["config"]["global_batch"] == 4096, j
     assert j["value"] > 0 and j["rank_ms_per_step"]["max"] >= j["rank_ms_per_step"]["min"] > 0, j
     assert "falling back" not in log, log[-2000:]
