@@ -251,8 +251,6 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   ROWS_STAMP(0);
   if (p.zero_word != nullptr && blockIdx.x == 0 && t == 0) *p.zero_word = 0;
-  // DP fused push: the previous merge (last reader of this rank's receive slots) is done
-  if (p.push.W > 0 && blockIdx.x == 0 && t == 0) push_signal_ready(p.push);
 
   // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
   // The ids are the head of the kernel's latency chain (ids → gathered rows): their loads are
@@ -697,6 +695,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   }
   if (!train) return;
+  // fp8: s_amax now collects the per-row max |dz| of the input layer's output gradient (the A
+  // operand of the fp8 dgrad GEMM below); forward layer 0, its last reader, is done
+  if (FP8 && t < kRowTile) s_amax[t] = 0.f;
 
   // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E);
   // kLateBw0 shapes re-read them after the layer-0 backward GEMM (register budget)
@@ -810,6 +811,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const float h = bf2f(H[r * ldh + c]);
         v[i] = h > 0.f ? s_g[r] * wc * inv_keep : 0.f;
         dz_cur[r * ldz + c] = f2bf(v[i]);
+        if (FP8 && a == 1) atomicMax(reinterpret_cast<unsigned*>(s_amax) + r, __float_as_uint(fabsf(bf2f(f2bf(v[i])))));
       }
       *reinterpret_cast<uint2*>(p.dzT[a] + (size_t)c * Bp + row0 + rg * 4) =
           make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
@@ -846,6 +848,35 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
               for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
             }
           }
+        } else if (li == 0 && FP8) {
+          // fp8-e4m3 dgrad dh0 = dz·W0ᵀ: dz quantised per row (s_amax), W0ᵀ per output column d
+          // (this wave holds all of k = dims[1] of its tiles in registers); de-scaled after
+          float sb[NJ];
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            float wm = 0.f;
+            if (j < SH::NJB0H) {
+#pragma unroll
+              for (int u = 0; u < SH::KSB0; ++u) wm = absmax_bf16x8(bw0[j][u], wm);
+            }
+            wm = fmaxf(wm, __shfl_xor(wm, 16, 64));
+            wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
+            sb[j] = kFp8Max / fmaxf(wm, 1e-30f);
+          }
+          const float sa = kFp8Max / fmaxf(s_amax[lane & 15], 1e-30f);
+#pragma unroll
+          for (int u = 0; u < SH::KSB0; ++u) {
+            const long av = quant_fp8x8(ld_frag(ap + 32 * u), sa);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              if (j < SH::NJB0H && nt0 + kWaves * j < ntiles)
+                accs[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, quant_fp8x8(bw0[j][u], sb[j]), accs[j], 0, 0, 0);
+          }
+          const int rbq = (lane >> 4) * 4;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) accs[j][i] *= (fmaxf(s_amax[rbq + i], 1e-30f) / kFp8Max) * (1.f / sb[j]);
         } else if (li == 0) {
 #pragma unroll
           for (int u = 0; u < SH::KSB0; ++u) {
@@ -895,6 +926,15 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
             const float h = bf2f(H[(rb + i) * ldh + c]);
             v[i] = h > 0.f ? acc[i] * inv_keep : 0.f;
             dz_nxt[(rb + i) * ldz + c] = f2bf(v[i]);
+          }
+          if (FP8 && li == 1) {  // per-row max |bf16 dz| over this tile's 16 columns → s_amax
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float m = fabsf(bf2f(f2bf(v[i])));
+#pragma unroll
+              for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+              if ((lane & 15) == 0) atomicMax(reinterpret_cast<unsigned*>(s_amax) + rb + i, __float_as_uint(m));
+            }
           }
           *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
               make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
@@ -954,6 +994,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
   lds_barrier();
   ROWS_STAMP(12);
+  // DP fused push: the previous merge (last reader of this rank's receive slots) is done.  Raised
+  // by the last instructions of workgroup 0 (the exchange-counter load it needs would otherwise
+  // hold wave 0 for a memory round trip in front of the id loads); the peers' producers that
+  // read it store only at the end of their step tail.
+  if (p.push.W > 0 && blockIdx.x == 0 && t == 0) push_signal_ready(p.push);
   if constexpr (!SH::kStatic) {
     if (p.bn) bn_grid_exit(p);
   }

@@ -39,7 +39,9 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
 // are summed by a wave-level segmented scan (shfl_up, fixed order); each run owned by the chunk
 // (its first entry lies here) adds its ≤4 wave pieces and, for the chunk's last run, the
 // continuation chunks; then one 16-lane group per run applies the optimizer to the table row.
-template <int KP4, int kChunk, bool BT = false>
+// PUSH: the fused DP push variant (mode 2 with p.push set); a compile-time switch so the other
+// launches keep their memory-op stream (and waitcnt placement) free of the push's branches.
+template <int KP4, int kChunk, bool BT = false, bool PUSH = false>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
   __shared__ float4 s_rows[kChunk * KP4];
@@ -56,12 +58,9 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
   // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
-  const bool push = p.mode == 2 && p.push.W > 0;
-  uint32_t push_n = 0, push_seen = 0;
-  if (push) {
-    push_n = push_exchange_no(p.push);
-    push_seen = push_ready_load(p.push, push_n);
-  }
+  const bool push = PUSH && p.mode == 2 && p.push.W > 0;
+  PushSeen push_seen{};
+  if (PUSH) push_seen = push_ready_load(p.push);
   // sorted export (mode 2 + chunk_heads): this chunk's output base and the batch's total, from the
   // side chain's per-chunk head counts (loaded with the keys; reduced below with the head compaction)
   int hb_before = 0, hb_total = 0;
@@ -219,7 +218,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   //    continuation), then the optimizer on a float4 of the table row; every thread issues its
   //    table/slot loads for up to 4 items before using any.
   const int nitems = nh * KP4;
-  if (push) push_wait_ready(p.push, push_n, push_seen);
+  if (push) push_wait_ready(p.push, push_seen);
   for (int base = 0; base < nitems; base += kChunk * 4) {
     float4 w[4], a[4], b[4], g[4];
     uint32_t kk[4];

@@ -18,18 +18,25 @@
 
 namespace rocfm {
 
-template <int KP4, bool BT>
+template <int KP4, bool BT, bool PUSH>
 __global__ __launch_bounds__(kEmbChunk) void emb_rows_update_kernel(const EmbUpdateParams p) {
-  emb_rows_body<KP4, kEmbChunk, BT>(p, blockIdx.x);
+  emb_rows_body<KP4, kEmbChunk, BT, PUSH>(p, blockIdx.x);
 }
 
 template <int KP4>
 static void launch_rows_update_t(const EmbUpdateParams& p, hipStream_t stream) {
-  if (p.tbl_bf16)
-    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, true>), dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream, p);
-  else
-    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, false>), dim3(cdiv(p.n, kEmbChunk)), dim3(kEmbChunk), 0, stream,
-                       p);
+  const dim3 grid(cdiv(p.n, kEmbChunk)), block(kEmbChunk);
+  if (p.mode == 2 && p.push.W > 0) {  // fused DP push (export straight into the receive slots)
+    ROCFM_REQUIRE(p.push.W <= kPushMaxW, "emb_update: push world > 8");
+    if (p.tbl_bf16)
+      hipLaunchKernelGGL((emb_rows_update_kernel<KP4, true, true>), grid, block, 0, stream, p);
+    else
+      hipLaunchKernelGGL((emb_rows_update_kernel<KP4, false, true>), grid, block, 0, stream, p);
+  } else if (p.tbl_bf16) {
+    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, true, false>), grid, block, 0, stream, p);
+  } else {
+    hipLaunchKernelGGL((emb_rows_update_kernel<KP4, false, false>), grid, block, 0, stream, p);
+  }
 }
 
 void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {

@@ -14,11 +14,19 @@
 
 namespace rocfm {
 
-__global__ __launch_bounds__(kWgThreads) void mlp_wgrad_kernel(const WgradParams p) { wgrad_body(p, blockIdx.x); }
+template <bool PUSH>
+__global__ __launch_bounds__(kWgThreads) void mlp_wgrad_kernel(const WgradParams p) {
+  wgrad_body<PUSH>(p, blockIdx.x);
+}
 
 void launch_mlp_wgrad(WgradParams p, hipStream_t stream) {
   const int grid = wgrad_prepare(p);
-  hipLaunchKernelGGL(mlp_wgrad_kernel, dim3(grid), dim3(kWgThreads), 0, stream, p);
+  if (p.push.W > 0 && !p.fuse_opt) {  // fused DP push: gradients straight into the receive slots
+    ROCFM_REQUIRE(p.push.W <= kPushMaxW, "mlp_wgrad: push world > 8");
+    hipLaunchKernelGGL(mlp_wgrad_kernel<true>, dim3(grid), dim3(kWgThreads), 0, stream, p);
+  } else {
+    hipLaunchKernelGGL(mlp_wgrad_kernel<false>, dim3(grid), dim3(kWgThreads), 0, stream, p);
+  }
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

@@ -44,27 +44,35 @@ __device__ __forceinline__ void push_signal_ready(const PushTarget& t) {
     if (r != t.rank) __hip_atomic_store(t.peer_sig[r] + t.rank, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The smallest "entered" number over the peers, read without waiting (issued early by a producer).
-__device__ __forceinline__ uint32_t push_ready_load(const PushTarget& t, uint32_t n) {
-  uint32_t lo = n;
+// What a producer reads at its start (ctrl and every peer's "entered" flag) without waiting on any
+// of it: the values are only compared at its first store (push_wait_ready), so the loads fly under
+// the producer's own first round trip instead of holding the wave in front of it.
+struct PushSeen {
+  uint32_t done;               // exchanges completed (ctrl): this exchange is done + 1
+  uint32_t ready[kPushMaxW];   // ready[d]: last exchange rank d entered
+};
+
+__device__ __forceinline__ PushSeen push_ready_load(const PushTarget& t) {
+  PushSeen s;
+  s.done = __hip_atomic_load(t.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t* mine = t.peer_sig[t.rank];
-  for (int d = 0; d < t.W; ++d) {
-    if (d == t.rank) continue;
-    const uint32_t v = __hip_atomic_load(mine + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if ((int32_t)(v - lo) < 0) lo = v;
-  }
-  return lo;
+#pragma unroll
+  for (int d = 0; d < kPushMaxW; ++d)
+    s.ready[d] = (d < t.W && d != t.rank) ? __hip_atomic_load(mine + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : 0u;
+  return s;
 }
 
 // Before the first store into a peer's slot: every peer has entered exchange n (bounded wait).
 // Only a load → store order is needed (the peer's reads of the slot finished before it signalled):
 // the stores are issued after the flag values have returned and been compared, so the polls are
 // relaxed — an acquire fence here would invalidate this XCD's L2 under the tail's own loads.
-__device__ __forceinline__ void push_wait_ready(const PushTarget& t, uint32_t n, uint32_t seen) {
-  if ((int32_t)(seen - n) >= 0) return;
+__device__ __forceinline__ void push_wait_ready(const PushTarget& t, const PushSeen& s) {
+  const uint32_t n = s.done + 1u;
   const uint32_t* mine = t.peer_sig[t.rank];
-  for (int d = 0; d < t.W; ++d) {
-    if (d == t.rank) continue;
+#pragma unroll
+  for (int d = 0; d < kPushMaxW; ++d) {
+    if (d >= t.W || d == t.rank || (int32_t)(s.ready[d] - n) >= 0) continue;
     long long i = 0;
     while ((int32_t)(__hip_atomic_load(mine + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - n) < 0) {
       if (++i >= t.spin_limit) {

@@ -14,14 +14,23 @@ constexpr int kTailThreads = 512;
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
-template <int KP4, bool BT>
+template <int KP4, bool BT, bool PUSH>
 __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                  const int n_emb) {
   const int bid = blockIdx.x;
   if (bid < n_emb)
-    emb_rows_body<KP4, kTailThreads, BT>(e, bid);  // the longer role first: its workgroups dispatch first
+    emb_rows_body<KP4, kTailThreads, BT, PUSH>(e, bid);  // the longer role first: its workgroups dispatch first
   else
-    wgrad_body(w, bid - n_emb);
+    wgrad_body<PUSH>(w, bid - n_emb);
+}
+
+template <int KP4, bool PUSH>
+static void launch_tail_t(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
+                          hipStream_t stream) {
+  if (e.tbl_bf16)
+    hipLaunchKernelGGL((step_tail_kernel<KP4, true, PUSH>), grid, block, 0, stream, w, e, n_emb);
+  else
+    hipLaunchKernelGGL((step_tail_kernel<KP4, false, PUSH>), grid, block, 0, stream, w, e, n_emb);
 }
 
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
@@ -31,13 +40,16 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   const int n_wg = wgrad_prepare(w);
   const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
+  // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
+  const bool push = (e.push.W > 0 && e.mode == 2) || (w.push.W > 0 && !w.fuse_opt);
+  ROCFM_REQUIRE(!push || (e.push.W <= kPushMaxW && w.push.W <= kPushMaxW), "step_tail: push world > 8");
   switch (e.Kp / 4) {
-#define ROCFM_KP4(N)                                                                         \
-  case N:                                                                                    \
-    if (e.tbl_bf16)                                                                          \
-      hipLaunchKernelGGL((step_tail_kernel<N, true>), grid, block, 0, stream, w, e, n_emb);  \
-    else                                                                                     \
-      hipLaunchKernelGGL((step_tail_kernel<N, false>), grid, block, 0, stream, w, e, n_emb); \
+#define ROCFM_KP4(N)                                                   \
+  case N:                                                              \
+    if (push)                                                          \
+      launch_tail_t<N, true>(w, e, n_emb, grid, block, stream);        \
+    else                                                               \
+      launch_tail_t<N, false>(w, e, n_emb, grid, block, stream);       \
     break;
     ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
     ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12)

@@ -8,14 +8,16 @@ namespace {
 
 // A gradient of the flat dense buffer: the local grads buffer, or (fused DP push) this rank's slot
 // in every receive buffer — the MLP gradients lead each slot, as they lead the send buffer.
+template <bool PUSH>
 __device__ __forceinline__ void put_grad(const WgradParams& p, int idx, float g) {
-  if (p.push.W > 0) {
+  if (PUSH && p.push.W > 0) {
     for (int d = 0; d < p.push.W; ++d) p.push.slot[d][idx] = g;
   } else {
     p.grads[idx] = g;
   }
 }
 
+template <bool PUSH>
 __device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, int idx, float g) {
   if (p.fuse_opt) {
     float w = p.params[idx], a = p.s0 ? p.s0[idx] : 0.f, b = p.s1 ? p.s1[idx] : 0.f;
@@ -24,7 +26,7 @@ __device__ __forceinline__ void emit(const WgradParams& p, const OptStep& st, in
     if (p.s0) p.s0[idx] = a;
     if (p.s1) p.s1[idx] = b;
   } else {
-    put_grad(p, idx, g);
+    put_grad<PUSH>(p, idx, g);
   }
 }
 
@@ -41,6 +43,9 @@ __device__ __forceinline__ float dot_bf16x8_f32(uint4 v, const float* g) {
 
 constexpr int kWgThreads = 512;  // 8 waves: each takes 1/8 of the batch
 
+// PUSH: the fused DP push variant (gradients into the W receive slots, fuse_opt == 0); a
+// compile-time switch so single-GPU tails keep their code unchanged.
+template <bool PUSH = false>
 __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) {
   __shared__ __attribute__((aligned(16))) float s_red[(kWgThreads / 64) * 16 * 64];
   __shared__ uint16_t s_T[32 * 34];
@@ -49,12 +54,9 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int Bp = p.Bp;
   // fused DP push: the peers' "entered" flags are read now, long before the stores that need them
-  const bool push = !p.fuse_opt && p.push.W > 0;
-  uint32_t push_n = 0, push_seen = 0;
-  if (push) {
-    push_n = push_exchange_no(p.push);
-    push_seen = push_ready_load(p.push, push_n);
-  }
+  const bool push = PUSH && !p.fuse_opt && p.push.W > 0;
+  PushSeen push_seen{};
+  if (PUSH) push_seen = push_ready_load(p.push);
   ROCFM_STAMP(p.stamps, 0);
 
   if (bid < n_tiles) {
@@ -103,9 +105,9 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
       idx[e] = p.offW[li] + (ti * 32 + il[e]) * Dout + to * 32 + ol[e];
     }
     if (!p.fuse_opt) {
-      if (push) push_wait_ready(p.push, push_n, push_seen);
+      if (push) push_wait_ready(p.push, push_seen);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) put_grad(p, idx[e], g[e]);
+      for (int e = 0; e < 2; ++e) put_grad<PUSH>(p, idx[e], g[e]);
       if (push) push_drain();
     } else {
 #pragma unroll
@@ -159,8 +161,8 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
     }
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
-    if (push) push_wait_ready(p.push, push_n, push_seen);
-    if (sub == 0) emit(p, st, p.offb[li] + o, s * p.grad_scale);
+    if (push) push_wait_ready(p.push, push_seen);
+    if (sub == 0) emit<PUSH>(p, st, p.offb[li] + o, s * p.grad_scale);
     if (push) push_drain();
     return;
   }
@@ -168,7 +170,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
   {
     const int Dn = p.dims[p.nl];
     const uint16_t* H = p.actT[p.nl];
-    if (push) push_wait_ready(p.push, push_n, push_seen);
+    if (push) push_wait_ready(p.push, push_seen);
     for (int c0 = 0; c0 < Dn; c0 += 32) {
       const int c = min(c0 + (t >> 4), Dn - 1);
       const uint16_t* row = H + (size_t)c * Bp;
@@ -183,7 +185,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
       }
 #pragma unroll
       for (int d = 1; d < 16; d <<= 1) s += __shfl_xor(s, d, 64);
-      if (sub == 0 && c0 + (t >> 4) < Dn) emit(p, st, p.off_wout + c, s * p.grad_scale);
+      if (sub == 0 && c0 + (t >> 4) < Dn) emit<PUSH>(p, st, p.off_wout + c, s * p.grad_scale);
     }
     float s = 0.f;
     for (int b = t; b < Bp; b += kWgThreads) s += p.g[b];
@@ -194,14 +196,14 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
       float tot = 0.f;
       for (int w = 0; w < kWgThreads / 64; ++w) tot += s_red[w];
       tot *= p.grad_scale;
-      emit(p, st, p.off_bout, tot);
-      emit(p, st, p.off_fmb, tot);
+      emit<PUSH>(p, st, p.off_bout, tot);
+      emit<PUSH>(p, st, p.off_fmb, tot);
     }
     if (p.bn) {  // batch_norm γ / β: column sums already reduced over the batch by deepfm_rows
       for (int l = 0; l < p.nl; ++l)
         for (int c = t; c < p.dims[l + 1]; c += kWgThreads) {
-          emit(p, st, p.off_gamma[l] + c, p.bn_grad[(size_t)(2 * l) * p.bn_dmax + c] * p.grad_scale);
-          emit(p, st, p.off_beta[l] + c, p.bn_grad[(size_t)(2 * l + 1) * p.bn_dmax + c] * p.grad_scale);
+          emit<PUSH>(p, st, p.off_gamma[l] + c, p.bn_grad[(size_t)(2 * l) * p.bn_dmax + c] * p.grad_scale);
+          emit<PUSH>(p, st, p.off_beta[l] + c, p.bn_grad[(size_t)(2 * l + 1) * p.bn_dmax + c] * p.grad_scale);
         }
     }
     if (push) push_drain();

@@ -35,9 +35,9 @@ def _batches(B, n, seed):
     return [gen.batch(B, "cpu", g) for _ in range(n)]
 
 
-def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, update=None):
+def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, update=None, push="1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world))
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH=push)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from rocfm.models.deepfm import init_params
@@ -50,8 +50,8 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
                             embedding_update=update, mode=mode,
                             use_graph=spg > 0, exchange=exchange)
     assert eng.exchange == exchange or mode == "dense_dp", eng.exchange
-    # p2p dp: the tail's producers push into the peers' slots unless ROCFM_DP_PUSH=0
-    want_fused = exchange == "p2p" and mode == "dp" and os.environ.get("ROCFM_DP_PUSH", "1") != "0"
+    # p2p dp: the tail's producers push into the peers' slots when forced (ranks share this GPU)
+    want_fused = exchange == "p2p" and mode == "dp" and os.environ.get("ROCFM_DP_PUSH") == "1"
     assert eng.fused_push == want_fused, (eng.fused_push, want_fused)
     batches = _batches(world * B, steps, 11)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
@@ -89,16 +89,17 @@ def test_fused_dp_world4_p2p_graphs(tmp_path, update):
 
 
 @pytest.mark.parametrize("world,spg", [(2, 0), (4, 4)])
-def test_fused_dp_p2p_unfused_push(tmp_path, monkeypatch, world, spg):
+def test_fused_dp_p2p_unfused_push(tmp_path, world, spg):
     """ROCFM_DP_PUSH=0: the tail writes the local send buffer and the push launch copies all of it
     (the path before producer-side pushing) ≡ the single-GPU union batch."""
-    monkeypatch.setenv("ROCFM_DP_PUSH", "0")
-    _check_dp_vs_single(tmp_path, world, "dp", "p2p", 11 if spg else 3, spg, "sparse")
+    _check_dp_vs_single(tmp_path, world, "dp", "p2p", 11 if spg else 3, spg, "sparse", push="0")
 
 
-def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update):
+def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, push="1"):
+    # ranks share this GPU, where the fused push is off by default: the workers force it (small
+    # batches keep the spinning producers from starving a peer) unless the copy push is asked for
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_worker, args=(world, _free_port(), mode, out, exchange, steps, spg, update), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out, exchange, steps, spg, update, push), nprocs=world,
                        join=True, start_method="spawn")
     dp = torch.load(out, weights_only=True)
     from rocfm.models.deepfm import init_params

@@ -214,9 +214,10 @@ def test_train_stream_equals_per_step():
 
 
 def test_fp8_input_layer_matches_fp8_oracle():
-    """compute_dtype=fp8: the input layer's forward GEMM runs on fp8-e4m3 MFMA with per-row /
-    per-column scales; the step matches an oracle with the same quantisation (and differs from
-    the bf16 one by more than the comparison tolerance)."""
+    """compute_dtype=fp8: the input layer's forward GEMM and its dgrad (dz1·W0ᵀ, the embedding
+    gradient's MLP part) run on fp8-e4m3 MFMA with per-row / per-column scales; the step matches
+    an oracle with the same quantisation (and differs from the bf16 one by more than the
+    comparison tolerance)."""
     torch.manual_seed(0)
     dev = torch.device("cuda")
     V, F, K, B = 5000, 39, 10, 192
@@ -241,6 +242,15 @@ def test_fp8_input_layer_matches_fp8_oracle():
     for l in range(3):
         dW = before[f"Deep-part/mlp{l}/weights"] - after[f"Deep-part/mlp{l}/weights"]
         torch.testing.assert_close(dW, ref8["dW"][l], rtol=3e-2, atol=3e-5)
+    # embedding rows (GD, lazy L2): the fp8 dgrad's quantisation shows in their update
+    uniq, acc8 = R.emb_grad_reference(ids, ref8["contrib"])
+    _, acc16 = R.emb_grad_reference(ids, ref16["contrib"])
+    delta = (emb[:, : K + 1] - eng.emb.detach().cpu()[:, : K + 1])[uniq] - spec.l2_reg * emb[uniq, : K + 1]
+    # a 1-ulp bf16 difference in dz (f32 accumulation order) can flip one fp8 rounding (≈6 % of one
+    # product), hence the loose element tolerance; the second check separates fp8 from bf16 dgrad
+    # (measured: |Δ − fp8 oracle| 1.1e-4, |Δ − bf16 oracle| 8.8e-4, rows up to 0.24)
+    torch.testing.assert_close(delta, acc8, rtol=3e-2, atol=3e-4)
+    assert (delta - acc8).abs().max() < 0.3 * (acc16 - acc8).abs().max()
 
 
 def _rel(a, b):

@@ -108,10 +108,20 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
     j, log = _bench(["--gpus", "4", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
                     {"ROCFM_BENCH_BACKEND": "gloo"})
     assert j["n_gpus"] == 4 and j["world_size"] == 4 and j["backend"] == "gloo", j
-    assert j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is True, (j, log[-2000:])
+    # ranks sharing the GPU: the copy push (the fused one is the default with one GPU per rank)
+    assert j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is False, (j, log[-2000:])
     assert j["config"]["parallelism"] == "dp4" and j["config"]["global_batch"] == 4096, j
     assert j["value"] > 0 and j["rank_ms_per_step"]["max"] >= j["rank_ms_per_step"]["min"] > 0, j
     assert "falling back" not in log, log[-2000:]
+
+
+def test_bench_rehearsal_2_ranks_fused_push():
+    """The fused push (producers store into the peers' slots from the step tail) through bench.py
+    at the reference batch, 2 ranks sharing the GPU (forced: ROCFM_DP_PUSH=1)."""
+    j, log = _bench(["--gpus", "2", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
+                    {"ROCFM_BENCH_BACKEND": "gloo", "ROCFM_DP_PUSH": "1"})
+    assert j["n_gpus"] == 2 and j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is True, j
+    assert j["value"] > 0 and "falling back" not in log, log[-2000:]
 
 
 @pytest.mark.parametrize("extra", [[], ["--hot_rows", "256", "--ps_staleness", "1"]])
