@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--data_dir", default="", help="--input tfrecord: directory for the generated files (default: a "
                                                    "temporary directory, removed afterwards)")
     ap.add_argument("--loader_threads", type=int, default=16)
+    ap.add_argument("--loader_hold", type=int, default=2,
+                    help="--input tfrecord: decoded groups held ahead of the GPU (pinned ring of (hold+2)*S batches)")
     ap.add_argument("--json_out", default="")
     return ap.parse_args()
 
@@ -315,16 +317,18 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
     gen_s = time.perf_counter() - t0
 
     def dataset():
-        return TFRecordDataset(files, F, B, a.feature_size, num_threads=a.loader_threads, verify_crc=True, hold=2)
+        return TFRecordDataset(files, F, B, a.feature_size, num_threads=a.loader_threads, verify_crc=True,
+                               hold=a.loader_hold)
 
     # loader alone: decode every batch (CRC + Example parse into pinned memory), no GPU
     t = time.perf_counter()
-    nb = sum(int(g[0].shape[0]) for g in dataset().groups(S))
+    nb = sum(int(g[0].shape[0]) for g in dataset().groups(S, hold=a.loader_hold))
     loader_eps = nb * B / (time.perf_counter() - t)
 
     eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
                       compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
-    eng.train_stream(dataset().groups(S, hold=2, limit=a.warmup), S, hold=2)  # graphs + code objects
+    H = a.loader_hold
+    eng.train_stream(dataset().groups(S, hold=H, limit=a.warmup), S, hold=H)  # graphs + code objects
     stall = [0.0]
 
     def timed(it):
@@ -339,7 +343,7 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    done = eng.train_stream(timed(dataset().groups(S, hold=2, skip=a.warmup, limit=a.steps)), S, hold=2,
+    done = eng.train_stream(timed(dataset().groups(S, hold=H, skip=a.warmup, limit=a.steps)), S, hold=H,
                             ring_batches=a.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -370,7 +374,7 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
                             f"k={a.embedding_size}, mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
                    "global_batch": B, "seq_len": F, "parallelism": "dp1", "engine": "fused",
                    "embedding_update": a.embedding_update, "input": "tfrecord", "steps_per_graph": S,
-                   "loader_threads": a.loader_threads},
+                   "loader_threads": a.loader_threads, "loader_hold": a.loader_hold},
         "loader_alone_examples_per_sec": round(loader_eps, 1),
         "next_epoch_from_hbm_cache_examples_per_sec": round(cached_eps, 1),
         "input_stall_s": round(stall[0], 4),
