@@ -60,7 +60,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
   const bool push = PUSH && p.mode == 2 && p.push.W > 0;
   PushSeen push_seen{};
-  if (PUSH) push_seen = push_ready_load(p.push);
+  if (PUSH && p.push.W > 0) push_seen = push_ready_load(p.push);  // (the tail's other role may be the pusher)
   // sorted export (mode 2 + chunk_heads): this chunk's output base and the batch's total, from the
   // side chain's per-chunk head counts (loaded with the keys; reduced below with the head compaction)
   int hb_before = 0, hb_total = 0;

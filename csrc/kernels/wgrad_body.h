@@ -56,7 +56,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
   // fused DP push: the peers' "entered" flags are read now, long before the stores that need them
   const bool push = PUSH && !p.fuse_opt && p.push.W > 0;
   PushSeen push_seen{};
-  if (PUSH) push_seen = push_ready_load(p.push);
+  if (PUSH && p.push.W > 0) push_seen = push_ready_load(p.push);  // (the tail's other role may be the pusher)
   ROCFM_STAMP(p.stamps, 0);
 
   if (bid < n_tiles) {

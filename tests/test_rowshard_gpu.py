@@ -156,8 +156,10 @@ def test_fused_rowshard_world1_equals_single(update, graph):
 
 
 def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0, staleness=0, hot=0):
+    # ROCFM_DP_PUSH=1: the X4 producer push is forced on although the ranks share this GPU (small
+    # batches; the default keeps the copy push there)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world))
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from rocfm.models.deepfm import init_params
@@ -168,6 +170,7 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     eng = FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), embedding_update=update,
                         use_graph=spg > 0, exchange=exchange, staleness=staleness, hot_rows=hot)
     assert eng.exchange == exchange, eng.exchange
+    assert eng.fused_push == (exchange == "p2p" and hot == 0), eng.fused_push
     batches = _batches(world * B, steps, 11, disjoint=staleness > 0)
     pool = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
             for b in batches]
