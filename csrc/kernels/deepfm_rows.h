@@ -75,7 +75,8 @@ struct RowsParams {
   float* bn_grad;                     // [nl][2][bn_dmax]: Σ dy·x̂ (d γ), Σ dy (d β) of the batch
   unsigned* bn_sync;                  // [2] grid-barrier arrival / exit counters (0 between launches)
   int* bn_error;                      // set if a grid barrier timed out (the host check raises)
-  PushTarget push;                    // DP fused push (push.h): workgroup 0 signals "entered"
+  PushTarget push;                    // producer push (push.h): workgroup 0 signals "entered"
+  PushTarget push2;                   // a second exchange pushed by this step (row-shard X3)
 };
 
 struct WgradParams {

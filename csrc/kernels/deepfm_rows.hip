@@ -998,7 +998,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // by the last instructions of workgroup 0 (the exchange-counter load it needs would otherwise
   // hold wave 0 for a memory round trip in front of the id loads); the peers' producers that
   // read it store only at the end of their step tail.
-  if (p.push.W > 0 && blockIdx.x == 0 && t == 0) push_signal_ready(p.push);
+  if (blockIdx.x == 0 && t == 0) {
+    if (p.push.W > 0) push_signal_ready(p.push);
+    if (p.push2.W > 0) push_signal_ready(p.push2);
+  }
   if constexpr (!SH::kStatic) {
     if (p.bn) bn_grid_exit(p);
   }

@@ -58,7 +58,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
   // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
-  const bool push = PUSH && p.mode == 2 && p.push.W > 0;
+  const bool push = PUSH && p.push.W > 0 && (p.mode == 2 || (p.mode == 1 && p.push_seg > 0));
   PushSeen push_seen{};
   if (PUSH && p.push.W > 0) push_seen = push_ready_load(p.push);  // (the tail's other role may be the pusher)
   // sorted export (mode 2 + chunk_heads): this chunk's output base and the batch's total, from the
@@ -276,6 +276,11 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         if (p.hot_out != nullptr && rr >= p.hot_base) {  // replicated row → the X4 bucket
           reinterpret_cast<float4*>(p.hot_out)[(size_t)(rr - p.hot_base) * KP4 + u4] = g[u];
           if (u4 == 0) p.hot_out[(size_t)p.n_hot * KP4 * 4 + (rr - p.hot_base)] = 1.f;
+          continue;
+        }
+        if (push) {  // row-shard X3: straight into the owner's receive slot
+          const uint32_t d = rr / (uint32_t)p.push_seg, j = rr - d * (uint32_t)p.push_seg;
+          reinterpret_cast<float4*>(p.push.slot[d])[(size_t)j * KP4 + u4] = g[u];
           continue;
         }
         reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];

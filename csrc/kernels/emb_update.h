@@ -48,9 +48,12 @@ struct EmbUpdateParams {
   int n_hot;
   int tbl_bf16;  // 1: emb holds bf16 rows (stochastic-rounded updates, common.h)
   // mode 2 with push.W > 0: keys / rows are stored into the W receive slots (push.h) at these
-  // float offsets instead of out_keys / out_rows; the count still goes to out_count (local)
+  // float offsets instead of out_keys / out_rows; the count still goes to out_count (local).
+  // mode 1 with push.W > 0 and push_seg > 0 (row-shard X3): gradient row rr goes to destination
+  // rr / push_seg, row rr % push_seg of its slot, instead of dense_grad[rr]
   PushTarget push;
   int push_off_keys, push_off_rows;
+  int push_seg;
 };
 
 struct EmbDenseParams {

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kEmbChunk) void emb_rows_update_kernel(const EmbUpd
 template <int KP4>
 static void launch_rows_update_t(const EmbUpdateParams& p, hipStream_t stream) {
   const dim3 grid(cdiv(p.n, kEmbChunk)), block(kEmbChunk);
-  if (p.mode == 2 && p.push.W > 0) {  // fused DP push (export straight into the receive slots)
+  if (p.push.W > 0 && (p.mode == 2 || (p.mode == 1 && p.push_seg > 0))) {  // producer push (push.h)
     ROCFM_REQUIRE(p.push.W <= kPushMaxW, "emb_update: push world > 8");
     if (p.tbl_bf16)
       hipLaunchKernelGGL((emb_rows_update_kernel<KP4, true, true>), grid, block, 0, stream, p);

@@ -41,7 +41,7 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
-  const bool push = (e.push.W > 0 && e.mode == 2) || (w.push.W > 0 && !w.fuse_opt);
+  const bool push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);
   ROCFM_REQUIRE(!push || (e.push.W <= kPushMaxW && w.push.W <= kPushMaxW), "step_tail: push world > 8");
   switch (e.Kp / 4) {
 #define ROCFM_KP4(N)                                                   \
