@@ -127,7 +127,10 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
         dz[nl] = bf16(torch.where(h[nl] > 0, g[:, None] * w_out[None, :] / keeps[nl - 1], torch.zeros_like(h[nl])))
     dh0 = None
     for a in range(nl, 0, -1):
-        dh = dz[a] @ bf16(layers[a - 1]["W"]).t()
+        if fp8 and a == 1:  # the input layer's dgrad on fp8 MFMA (dz per row, W0ᵀ per column)
+            dh = fp8_rowcol_matmul(dz[a], bf16(layers[0]["W"]).t())
+        else:
+            dh = dz[a] @ bf16(layers[a - 1]["W"]).t()
         if a - 1 >= 1:
             if bn is not None:
                 dz[a - 1] = bn_back(a - 2, undrop(a - 2, dh))
@@ -156,7 +159,8 @@ FP8_MAX = 448.0  # largest finite float8 e4m3fn
 
 def fp8_rowcol_matmul(A: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """A·W with A quantised to fp8-e4m3 per row and W per column (scale = 448 / max|·|), f32
-    accumulate, de-scaled — the fused kernel's compute_dtype=fp8 input-layer GEMM."""
+    accumulate, de-scaled — the fused kernel's compute_dtype=fp8 input-layer GEMMs (forward
+    h0·W0, and the dgrad dz1·W0ᵀ)."""
     sa = FP8_MAX / A.abs().amax(1, keepdim=True).clamp_min(1e-30)
     sb = FP8_MAX / W.abs().amax(0, keepdim=True).clamp_min(1e-30)
     Aq = (A * sa).to(torch.float8_e4m3fn).float()

@@ -244,9 +244,10 @@ class FusedDataParallel:
             cap = (int(capacity or e.n_lookup) + 3) // 4 * 4  # keeps every row 16-B aligned
             self.cap = cap
             Kp = e.Kp
-            # send buffer (f32 words): [MLP grads P | count (int32) + pad 3 | keys cap (int32) | rows cap*Kp]
-            self.off_cnt = P
-            self.off_keys = P + 4
+            # send buffer (f32 words): [MLP grads P | pad to 4 | count (int32) + pad 3 | keys cap (int32) |
+            # rows cap*Kp]  (every part from the count on 16-B aligned)
+            self.off_cnt = (P + 3) // 4 * 4
+            self.off_keys = self.off_cnt + 4
             self.off_rows = self.off_keys + cap
             self.S = (self.off_rows + cap * Kp + 3) // 4 * 4  # float4 payload (p2p push)
             self.send = torch.zeros(self.S, dtype=torch.float32, device=e.device)
@@ -254,12 +255,24 @@ class FusedDataParallel:
 
             exs = open_exchanges([self.S], self.device, exchange)  # transport: p2p push or RCCL
             self.p2p = exs[0] if exs else None
+            # fused push (p2p only): the tail's producers store the MLP gradients and the exported
+            # rows straight into every rank's receive slot, so the xGMI transfer overlaps the tail;
+            # the push launch then carries only the row count + hand-off (ROCFM_DP_PUSH, see
+            # p2p.producer_push_enabled)
+            self.push_target = None  # fused_push below
             if self.p2p is not None:  # rank slots live in the uncached, peer-mapped receive buffer
                 self.exchange = "p2p"
                 self.graph_collectives = use_graph  # the push kernel is capturable whatever the backend
                 self.recv = None
                 self._recv_ptr = self.p2p.recv_ptr
-                self.p2p_params = self.p2p.params(self.send.data_ptr(), self.S)
+                from .p2p import producer_push_enabled
+
+                if producer_push_enabled(self.p2p):
+                    self.push_target = self.p2p.push_target()
+                    self.p2p_params = self.p2p.params(self.send[self.off_cnt:].data_ptr(), 4,
+                                                      dst_offset_floats=self.off_cnt)
+                else:
+                    self.p2p_params = self.p2p.params(self.send.data_ptr(), self.S)
             else:  # one rank: the gathered list IS the send buffer (no copy)
                 self.recv = (torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
                              if self.world > 1 or self.force else self.send)
@@ -283,6 +296,7 @@ class FusedDataParallel:
                 ex.out_rows = self.send[self.off_rows:].data_ptr()
                 ex.out_count = self.send[self.off_cnt:].data_ptr()
                 ex.out_cap = cap
+                self._set_push(e.rows_params[p], e.wgrad_params[p], ex)
                 self.export_params.append(ex)
                 mp_ = H.MergeParams()  # merge the gathered lists: Σ over ranks per id → row optimizer
                 mp_.keys = self._recv_ptr + 4 * self.off_keys
@@ -310,6 +324,21 @@ class FusedDataParallel:
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
         self._graphs = {}
         self._warm = 0
+
+    @property
+    def fused_push(self) -> bool:
+        """True when the tail's producers push into the peers' receive slots themselves."""
+        return getattr(self, "push_target", None) is not None
+
+    def _set_push(self, rows, wp, ex) -> None:
+        """Point one step's producers at the receive slots (fused push; no-op otherwise)."""
+        t = getattr(self, "push_target", None)
+        if t is None:
+            return
+        rows.push = t  # workgroup 0 of the row kernel signals "entered"
+        wp.push = t
+        ex.push = t
+        ex.push_off_keys, ex.push_off_rows = self.off_keys, self.off_rows
 
     # ---- batch feeding (delegated) ------------------------------------------------------------
     def attach_pool(self, ids, vals, labels, start: int = 0):
@@ -347,7 +376,7 @@ class FusedDataParallel:
         return side
 
     def _exchange(self):
-        if self.p2p is not None:
+        if self.p2p is not None:  # fused push: only the row count + the data hand-off are left
             self.p2p.push(self.p2p_params)
             return
         if self.world == 1 and not self.force:  # one rank: recv aliases send (dp) / the bucket is the sum
@@ -451,6 +480,7 @@ class FusedDataParallel:
                 ex.out_cap = self.cap
                 if self.m_sorted:
                     ex.chunk_heads, ex.nch = e.m_chd[q, k * e.m_nch:].data_ptr(), e.m_nch
+                self._set_push(rows, wp, ex)
                 mg = H.MergeParams()
                 src = self.merge_params[0]
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",

@@ -515,6 +515,7 @@ class FusedRowShard:
         slots = [cap, cap * Kp, cap * Kp, self.PX] + ([cap] if self.staleness else [])
         exs = open_exchanges(slots, dev, exchange, extra_floats=[0, NH * Kp] + [0] * (len(slots) - 2))
         self.exchange = "p2p" if exs else "rccl"
+        self.mlp_push = self.grad_push = None  # X4 / X3 producer-side push targets (below)
         self.p2p_x = {}
         self.recv_pair = None  # staleness 1: request lists of consecutive steps (parity)
         if exs:
@@ -532,6 +533,18 @@ class FusedRowShard:
                 self.p2p_x[r2.data_ptr()] = exs[4]
                 self.recv_pair = [self.recv_ids, r2]
             self.graph_collectives = use_graph  # push kernels are capturable whatever the backend
+            # X4 pushed by its producer (csrc/kernels/push.h): the wgrad workgroups store the MLP
+            # gradients straight into every rank's X4 slot from inside the step tail, and the X4
+            # launch only hands the data off.  Same switch as the DP push
+            # (p2p.producer_push_enabled); replicated hot rows keep the copy (their sums ride the
+            # same bucket from the embedding role).
+            from .p2p import producer_push_enabled
+
+            if NH == 0 and producer_push_enabled(self.x_mlp):
+                self.mlp_push = self.x_mlp.push_target()
+                # X3 likewise: the embedding role stores each requested row's gradient sum straight
+                # into its owner's slot (row o·cap + j → owner o, row j)
+                self.grad_push = self.x_grad.push_target()
         elif self.W == 1 and not self.force:
             # one rank: every exchange is the identity, so the receive side IS the send side (rows
             # and row gradients share one buffer each; the request list each step reads is that
@@ -623,6 +636,7 @@ class FusedRowShard:
             da.apply, da.grad_scale = 1, 1.0 / self.W
             self._set_mlp_grads(da)
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
+            self._set_push(rp, e.wgrad_params[p], lp)
         pp = e.pred_params
         pp.ids, pp.emb = self.pred_local.data_ptr(), self.rows_in.data_ptr()
         pp.tbl_bf16 = 0
@@ -858,7 +872,10 @@ class FusedRowShard:
             prm = self._p2p_params.get(key)
             if prm is None:
                 chunk = out.numel() // self.W
-                prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
+                if self.grad_push is not None and ex is self.x_grad:  # X3 already in the slots
+                    prm = self._p2p_params[key] = ex.params(inp.data_ptr(), 0)
+                else:
+                    prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
             ex.push(prm)
         elif self.W > 1 or self.force:
             all_to_all_equal(out, inp)
@@ -874,13 +891,29 @@ class FusedRowShard:
         else:
             da.grads, da.nseg = e.dense_grads_flat.data_ptr(), 1
 
+    @property
+    def fused_push(self) -> bool:
+        """True when the step tail's wgrad workgroups push X4 into the peers' slots themselves."""
+        return self.mlp_push is not None
+
+    def _set_push(self, rows, wp, ep) -> None:
+        """X4 / X3 producer push: the row kernel raises "entered" for both (their consumer, the
+        previous update launch, is done), the wgrad role stores X4 and the embedding role X3."""
+        if self.mlp_push is not None:
+            rows.push = self.mlp_push
+            wp.push = self.mlp_push
+        if self.grad_push is not None:
+            rows.push2 = self.grad_push
+            ep.push, ep.push_seg = self.grad_push, self.cap
+
     def _allreduce_mlp(self) -> None:
         """X4: the MLP gradients of every rank (p2p all-gather; the sum happens in dense_apply)."""
         e = self.eng
         if self.exchange == "p2p":
             prm = self._p2p_params.get("mlp")
-            if prm is None:
-                prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), self.PX)
+            if prm is None:  # fused push: the payload is already in the slots, only the hand-off
+                n = 0 if self.mlp_push is not None else self.PX
+                prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), n)
             self.x_mlp.push(prm)
         elif self.W > 1 or self.force:
             all_reduce_(self.mlp_bucket)  # MLP grads + replicated-row sums, one collective
@@ -1037,6 +1070,7 @@ class FusedRowShard:
                 rows.ids, rows.emb = self.ms_local[q, k].data_ptr(), self.rows_in.data_ptr()
                 rows.tbl_bf16 = 0
                 wp.grads = e.dense_grads_flat.data_ptr()
+                self._set_push(rows, wp, ep)
                 ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
                 ep.mode, ep.dense_grad, ep.id_offset, ep.max_key = 1, self.grad_stage.data_ptr(), 0, 0
                 ep.touched = 0

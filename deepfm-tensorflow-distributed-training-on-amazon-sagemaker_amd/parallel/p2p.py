@@ -103,9 +103,13 @@ class P2PExchange:
         # every rank takes part in every collective below even if a step fails on it, so that a
         # local failure becomes an agreed fallback (selftest) instead of a hang
         mine = None
+        # ranks sharing one GPU (rehearsals on a one-GPU box): producer-side pushing is unsafe there
+        # (a rank's spinning producers can occupy the CUs its lagging peer needs to raise its flag)
+        self.shared_device = False
         if self.W > 1:  # peer-access check first (a failure becomes an agreed RCCL fallback below)
             keys: List = [None] * self.W
             dist.all_gather_object(keys, _pci_key(self.device), group=group)
+            self.shared_device = len(set(keys)) < self.W
             try:
                 why = peer_access_problem(self.device, keys, self.rank)
             except Exception as exc:  # property queries failing: leave the verdict to the self-test
@@ -149,18 +153,20 @@ class P2PExchange:
             dist.barrier(group=group)  # every rank's buffers are zeroed and mapped before any push
 
     def params(self, src_ptr: int, n_floats: int, src_stride_floats: int = 0, chunks: Optional[int] = None,
-               spin_limit: Optional[int] = None):
-        if n_floats % 4 or src_stride_floats % 4 or src_ptr % 16:
+               spin_limit: Optional[int] = None, dst_offset_floats: int = 0):
+        """Push parameters.  ``dst_offset_floats``: the payload lands that far into each slot (a
+        fused-push exchange publishes only the part its producers did not store themselves)."""
+        if n_floats % 4 or src_stride_floats % 4 or src_ptr % 16 or dst_offset_floats % 4:
             raise ValueError("p2p payloads must be whole, 16-byte aligned float4 runs")
-        if n_floats > self.slot:
-            raise ValueError(f"payload of {n_floats} floats exceeds the {self.slot}-float slot")
+        if n_floats + dst_offset_floats > self.slot:
+            raise ValueError(f"payload of {n_floats} floats at {dst_offset_floats} exceeds the {self.slot}-float slot")
         p = self.H.P2PParams()
         p.src = src_ptr
         p.n4 = n_floats // 4
         p.src_stride4 = src_stride_floats // 4
         p.slot4 = self.slot // 4
         for r, (a, b) in enumerate(self.peers):
-            p.set_peer(r, a, b)
+            p.set_peer(r, a + 4 * dst_offset_floats, b)
         p.ctrl = self.ctrl.data_ptr()
         p.error = self.error.data_ptr()
         p.W, p.rank = self.W, self.rank
@@ -168,6 +174,20 @@ class P2PExchange:
         p.chunks = int(chunks or max(1, min(64, math.ceil(n_floats * 4 / 16384))))
         p.spin_limit = int(spin_limit or self.spin_limit)
         return p
+
+    def push_target(self):
+        """Producer-side push into this exchange (csrc/kernels/push.h): this rank's slot in every
+        rank's receive buffer, the peers' flag blocks, the exchange counter and error flag."""
+        if self.W > self.H.push_max_world():
+            raise ValueError(f"fused push supports at most {self.H.push_max_world()} ranks, got {self.W}")
+        t = self.H.PushTarget()
+        t.W, t.rank = self.W, self.rank
+        for d, (recv, sig) in enumerate(self.peers):
+            t.set_dest(d, recv + self.rank * self.slot * 4, sig)
+        t.ctrl = self.ctrl.data_ptr()
+        t.error = self.error.data_ptr()
+        t.spin_limit = self.spin_limit
+        return t
 
     def push(self, p, stream: Optional[int] = None) -> None:
         if stream is None:
@@ -203,6 +223,14 @@ class P2PExchange:
                                         "version": 3, "strides": None}
         return torch.as_tensor(raw, device=self.device).view(*shape)
 
+    def clear(self) -> None:
+        """Zero this rank's W receive slots (e.g. the self-test's patterns) and wait until every
+        rank has done so, so no peer's next push can land before the clear.  Collective."""
+        self.recv_tensor(torch.float32, (self.W * self.slot,)).zero_()
+        torch.cuda.synchronize(self.device)
+        if self.W > 1 and dist.is_initialized():
+            dist.barrier(group=self.group)
+
     def errored(self) -> bool:
         return bool(int(self.error.item()))
 
@@ -222,6 +250,20 @@ class P2PExchange:
             for a in self._own:
                 self.H.p2p_free(a)
         self._own, self._opened = [], []
+
+
+def producer_push_enabled(ex) -> bool:
+    """Whether an exchange's producers push into the peers' slots themselves (csrc/kernels/push.h).
+    ``ROCFM_DP_PUSH``: ``auto`` (default) — yes, unless ranks share a GPU (one-box rehearsals: a
+    rank's spinning producers could hold the CUs a lagging peer needs to raise its flag); ``1`` —
+    force (small test batches on a shared GPU); ``0`` — never (the push launch copies the bucket).
+    At most ``push_max_world()`` ranks (one node)."""
+    mode = os.environ.get("ROCFM_DP_PUSH", "auto").lower()
+    if mode not in ("auto", "0", "1"):
+        raise ValueError(f"ROCFM_DP_PUSH must be auto, 0 or 1, got {mode!r}")
+    if ex.W > ex.H.push_max_world():
+        return False
+    return mode == "1" or (mode == "auto" and not ex.shared_device)
 
 
 def selftest(ex: P2PExchange, n_floats: int, rounds: int = 3) -> bool:
@@ -279,6 +321,10 @@ def open_exchanges(slot_floats: List[int], device, choice: Optional[str] = None,
     for ex, n in zip(exs, slot_floats):
         ok = selftest(ex, n) and ok  # every rank runs every self-test (each one is agreed)
     if ok:
+        # slots start zeroed: a fused-push producer (rocfm.parallel.dp) never writes the padding
+        # words of its slot, which the MLP optimizer still reads
+        for ex in exs:
+            ex.clear()
         log.info("exchange: p2p push over IPC-mapped peer buffers (%d ranks, self-test passed)", world)
         return exs
     err = next((ex.init_error for ex in exs if ex.init_error is not None), None)
