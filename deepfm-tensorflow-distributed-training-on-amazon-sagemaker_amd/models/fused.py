@@ -818,6 +818,8 @@ class FusedDeepFM:
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
             gm.replay()
+            if getattr(self, "_m_serial_side", False):  # (see FusedRowShard: exact + replicated rows)
+                side.wait_stream(main)
             side.wait_event(before)
             with torch.cuda.stream(side):
                 gs.replay()

@@ -1100,6 +1100,11 @@ class FusedRowShard:
                 H.shard_route(rp, stream.cuda_stream)
 
         e._m_post = route_all
+        # replicated rows: the side chain of graph N (next batches' fetch, sort, route) runs AFTER
+        # main graph N instead of beside it.  Beside it, 4 identical exact-mode runs of ≥ 2 graphs
+        # were not bitwise equal (one graph, or this serialisation, were) and a sparse-mode run
+        # missed the single-GPU result once; the shared state is still to be found (README)
+        e._m_serial_side = self.NH > 0
         self._ms_S = Smax
 
     def _enqueue_multi_rs(self, q: int, S: int) -> None:
