@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--loader_hold", type=int, default=2,
                     help="--input tfrecord: decoded groups held ahead of the GPU (pinned ring of (hold+2)*S batches)")
     ap.add_argument("--json_out", default="")
+    ap.add_argument("--no_secondary", action="store_true",
+                    help="one GPU: skip the secondary windows (exact-mode and TFRecord-fed rates) reported "
+                         "next to the headline")
     return ap.parse_args()
 
 
@@ -212,6 +215,9 @@ def main():
     if a.steps_per_graph <= 0:
         a.steps_per_graph = max(2, min(64, a.steps))
     run(a.warmup)
+    shadow = getattr(eng, "shadow", None)
+    while shadow is not None and shadow.active:  # p2p self-validation window: always untimed
+        eng.train_step()
     if hasattr(eng, "precapture"):
         eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region
     torch.cuda.synchronize()
@@ -230,8 +236,13 @@ def main():
     if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, dt_min = float(t[0].item()), -float(t[1].item())
-    if hasattr(eng, "check"):
-        eng.check()  # sticky device flags (exchange overflow, p2p peer timeout, BN barrier): fail loudly
+    replicas_ok = None
+    if hasattr(eng, "verify_replicas"):
+        eng.check(replicas=False)  # sticky device flags (exchange overflow, p2p peer timeout): fail loudly
+        # collective digest of every replicated tensor: a fast but wrong multi-GPU run shows here
+        replicas_ok = bool(eng.verify_replicas()) if world > 1 else None
+    elif hasattr(eng, "check"):
+        eng.check()  # sticky device flags (BN barrier, id guard): fail loudly
     ms = dt / a.steps * 1e3
     value = B * world * a.steps / dt
     base = EAGER_BASELINE.get(a.embedding_update)
@@ -269,21 +280,76 @@ def main():
         "world_size": dist.get_world_size() if pg else 1,
         "backend": (dist.get_backend() if pg else None),
         "rank_ms_per_step": {"max": round(ms, 4), "min": round(dt_min / a.steps * 1e3, 4)},
+        # self-validation (rocfm.parallel.validate): replicas bit-identical across ranks after the
+        # timed steps; the p2p exchange's first steps checked bitwise against the collective
+        "replicas_consistent": replicas_ok,
+        "shadow_exchange": (shadow.status if shadow is not None else None),
     }
+    if hasattr(eng, "close"):
+        eng.close()  # graphs holding RCCL collectives must go before the process group
+    if (not pg and a.engine == "fused" and a.parallelism == "auto" and not a.no_secondary
+            and a.feature_size <= 20_000_000):
+        del eng, run
+        out.update(secondary_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels)))
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if hasattr(eng, "close"):
-        eng.close()  # graphs holding RCCL collectives must go before the process group
     if pg:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def secondary_windows(a, spec, hp, params, dev, pool):
+    """One GPU, same config and window length as the headline: (1) the reference-faithful
+    ``embedding_update=exact`` step (dense full-table L2 + Adam over every row, PS:277-278, 307) and
+    (2) the loader-fed rate (synthetic Criteo-shape TFRecord files → C++ loader → HBM ring →
+    multi-step graphs), so both are driver-observed, not only builder-run."""
+    import gc
+
+    import torch
+
+    from rocfm.models.fused import FusedDeepFM
+
+    out = {}
+    eng = FusedDeepFM(spec, hp, a.batch_size, dev, embedding_update="exact", params=params, seed=a.seed,
+                      compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
+    eng.attach_pool(*pool)
+    S = a.steps_per_graph
+    eng.train_steps(a.warmup, S)
+    eng.precapture(a.steps, S)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.train_steps(a.steps, S)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.check()
+    out["exact_examples_per_sec"] = round(a.batch_size * a.steps / dt, 1)
+    out["exact_ms_per_step"] = round(dt / a.steps * 1e3, 4)
+    del eng
+    gc.collect()
+    torch.cuda.empty_cache()
+    t = measure_tfrecord(a, spec, hp, params, dev)
+    out["tfrecord_examples_per_sec"] = t["value"]
+    out["tfrecord_ms_per_step"] = t["ms_per_step"]
+    out["tfrecord_input_stall_fraction"] = t["input_stall_fraction"]
+    out["tfrecord_loader_alone_examples_per_sec"] = t["loader_alone_examples_per_sec"]
+    return out
+
+
 def bench_tfrecord(a, spec, hp, params, dev, rank):
+    out = measure_tfrecord(a, spec, hp, params, dev)
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+
+
+def measure_tfrecord(a, spec, hp, params, dev):
     """Loader-fed end-to-end throughput on one GPU (the reference's tf.data chain is inside its
     training loop: PS:147-165, HVD:128-159).  Files hold exactly W + K batches; the timed region
     is the K steps' train_stream call — it starts the C++ decoders (skipping the W warm-up batches
@@ -382,14 +448,9 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
         "data_gen_s": round(gen_s, 2),
         "world_size": 1, "backend": None,
     }
-    if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
     if own:
         shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 if __name__ == "__main__":

@@ -77,6 +77,7 @@ struct RowsParams {
   int* bn_error;                      // set if a grid barrier timed out (the host check raises)
   PushTarget push;                    // producer push (push.h): workgroup 0 signals "entered"
   PushTarget push2;                   // a second exchange pushed by this step (row-shard X3)
+  int row_tile;                       // examples per workgroup: 16 (0 = default) or 8 (static shapes)
 };
 
 struct WgradParams {

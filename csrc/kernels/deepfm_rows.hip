@@ -202,6 +202,14 @@ struct CtShape {
   static_assert(GU <= 12, "CtShape: at most 12 gathered rows per thread");
 };
 
+template <class SH, int RT, int KP4>
+__device__ constexpr int gather_units() {
+  if constexpr (SH::kStatic)
+    return (RT * SH::F * KP4 + kRowThreads - 1) / kRowThreads;
+  else
+    return SH::GU;
+}
+
 }  // namespace
 
 // Diagnostic phase stamps kept in LDS and written out once at the end, so that recording them
@@ -221,8 +229,13 @@ struct CtShape {
 // prefetched fragments.  Branch-free static kernels wait only for what they consume.
 constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
 
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT>
+// RT: examples per workgroup (16, or 8 for twice the workgroups on a 256-CU chip).  The LDS tiles
+// and MFMA M tiles stay 16 rows; with RT = 8 rows 8..15 are zero padding whose outputs are
+// discarded (no global store touches them), so the arithmetic of every valid row is unchanged.
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
+  static_assert(RT == 16 || RT == 8, "rows per workgroup: 16 or 8");
+  static_assert(RT == 16 || SH::kStatic, "8-row workgroups: compile-time shapes only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
   const SH sh(p);
@@ -239,10 +252,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   float* s_prm = reinterpret_cast<float*>(smem + L.prm);
 
   constexpr int Kp = KP4 * 4;
+  // gathered table rows per thread (phases A, F): the whole tile's rows in one batch (static shapes)
+  constexpr int kGU = gather_units<SH, RT, KP4>();
   const bool train = MODE == kDynamic ? (p.train != 0) : (MODE == kTrain);
   const int ablate = DIAG ? p.ablate : 0;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int row0 = blockIdx.x * kRowTile;
+  const int row0 = blockIdx.x * RT;
   const int F = sh.F, K = sh.K, NL = sh.nl;
   const int D0 = F * K, D0p = sh.dim(0);
   const uint32_t magicF = p.magicF;
@@ -259,12 +274,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if constexpr (SH::kStatic) {
     // every load unconditional (clamped index, value selected afterwards): no exec branches in
     // the memory-op stream (see MODE above); the kernarg pointers are read up front
-    constexpr int kItems = (kRowTile * SH::F + kRowThreads - 1) / kRowThreads;
+    constexpr int kItems = (RT * SH::F + kRowThreads - 1) / kRowThreads;
     const int32_t* ids_g = p.ids;
     const float* vals_g = p.vals;
     const int32_t* pos_g = p.contrib_pos ? p.contrib_pos : p.ids;  // any valid [B][F] int32 buffer
     const bool has_pos = p.contrib_pos != nullptr;
-    const int nvalid = max(0, min(kRowTile, p.B - row0)) * F;  // valid lookups of this tile
+    const int nvalid = max(0, min(RT, p.B - row0)) * F;  // valid lookups of this tile
     const int last = max(p.B * F - 1, 0);                        // clamp target: a valid lookup
     int32_t idr[kItems];
     float vlr[kItems];
@@ -281,7 +296,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
     for (int l = 0; l < SH::nl; ++l) br[l] = p.bias[l][min(t, sh.dim(l + 1) - 1)];
     const float wo = p.w_out[min(t, sh.dim(SH::nl) - 1)];
-    const float lab = p.labels[min(row0 + (t & (kRowTile - 1)), max(p.B - 1, 0))];
+    const float lab = p.labels[min(row0 + (t & (RT - 1)), max(p.B - 1, 0))];
     const float bo = *p.b_out, fb = *p.fm_bias;
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
@@ -289,7 +304,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
-      if (i < kRowTile * F) {
+      if (i < RT * F) {
         const bool valid = i < nvalid;
         s_ids[i] = valid ? idr[u] : 0;
         s_vals[i] = valid ? vlr[u] : 0.f;
@@ -304,9 +319,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       s_prm[L.prm_bout] = bo;
       s_prm[L.prm_fmb] = fb;
     }
-    if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? lab : 0.f;
+    if (t < kRowTile) s_prm[L.prm_lab + t] = (t < RT && row0 + t < p.B) ? lab : 0.f;
   } else {
-    for (int i = t; i < kRowTile * F; i += kRowThreads) {
+    for (int i = t; i < RT * F; i += kRowThreads) {
       const bool valid = row0 + fdiv(i, magicF) < p.B;
       s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
       s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
@@ -320,7 +335,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       s_prm[L.prm_bout] = *p.b_out;
       s_prm[L.prm_fmb] = *p.fm_bias;
     }
-    if (t < kRowTile) s_prm[L.prm_lab + t] = (row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
+    if (t < kRowTile) s_prm[L.prm_lab + t] = (t < RT && row0 + t < p.B) ? p.labels[row0 + t] : 0.f;
   }
   const uint32_t step = p.step ? (uint32_t)(*p.step) : 0u;
   lds_barrier();
@@ -330,8 +345,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   {
     uint16_t* h0 = reinterpret_cast<uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
-    const int nitems = kRowTile * F * KP4;
-    constexpr int U = SH::GU;  // static shapes: the whole tile's rows in one batch
+    const int nitems = RT * F * KP4;
+    constexpr int U = kGU;  // static shapes: the whole tile's rows in one batch
     for (int base = 0; base < nitems; base += kRowThreads * U) {
       float4 v[U];
 #pragma unroll
@@ -372,9 +387,15 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         }
       }
     }
-    for (int i = t; i < kRowTile * (D0p - D0); i += kRowThreads) {
+    for (int i = t; i < RT * (D0p - D0); i += kRowThreads) {
       const int r = i / (D0p - D0), c = D0 + i - r * (D0p - D0);
       h0[r * lda + c] = 0;
+    }
+    if constexpr (RT < kRowTile) {  // padding rows of the MFMA tile: zero (finite) operands
+      for (int i = t; i < (kRowTile - RT) * (lda / 8); i += kRowThreads) {
+        const int r = RT + i / (lda / 8), c8 = i - (r - RT) * (lda / 8);
+        *reinterpret_cast<uint4*>(h0 + r * lda + 8 * c8) = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   }
   lds_barrier();
@@ -387,7 +408,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   }
 
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
-  if (!(ablate & 2)) {
+  if (!(ablate & 2) && (t >> 5) < RT) {  // (wave-uniform: two rows per wave)
     const int r = t >> 5, q = t & 31;
     float cterm = 0.f, yw = 0.f, amx = 0.f;
     // G = ⌊32/K⌋ lanes per embedding column split the F fields (field f → group f mod G); the
@@ -445,8 +466,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if (train && !(ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
-    for (int it = t; it < D0p * 2; it += kRowThreads) {
-      const int c = it >> 1, h = it & 1;
+    for (int it = t; it < D0p * (RT / 8); it += kRowThreads) {
+      const int c = RT == 8 ? it : it >> 1, h = RT == 8 ? 0 : it & 1;
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -589,11 +610,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       for (int i = 0; i < 4; ++i) {
         float a = fmaxf(acc[i] + bc, 0.f);
         if (drop) a = keep_from_bits(pick4(bits, i), keep) ? a * inv_keep : 0.f;
-        if (row0 + rb + i >= p.B) a = 0.f;
+        if (rb + i >= RT || row0 + rb + i >= p.B) a = 0.f;
         hv[i] = a;
         O[(rb + i) * ldo + c] = f2bf(a);
       }
-      if (train)
+      if (train && rb < RT)
         *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
     }
@@ -672,7 +693,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     s += __shfl_xor(s, 2, 64);
     if (q == 0) {
       const int gr = row0 + r;
-      const bool valid = gr < p.B;
+      const bool valid = r < RT && gr < p.B;
       const float y = s_ylin[r] + s + s_prm[L.prm_bout];
       const float tl = s_prm[L.prm_lab + r];
       const float pr = 1.f / (1.f + __expf(-y));
@@ -691,7 +712,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         p.prob[gr] = pr;
         if (p.loss_rows) p.loss_rows[gr] = loss;
       }
-      if (train) p.g_out[gr] = g;
+      if (train && r < RT) p.g_out[gr] = g;
     }
   }
   if (!train) return;
@@ -701,8 +722,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 
   // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E);
   // kLateBw0 shapes re-read them after the layer-0 backward GEMM (register budget)
-  const int nitemsF = kRowTile * F * KP4;
-  constexpr int UF = SH::GU;
+  const int nitemsF = RT * F * KP4;
+  constexpr int UF = kGU;
   float4 rowsF[UF];
   if constexpr (!SH::kLateBw0) {
 #pragma unroll
@@ -813,8 +834,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         dz_cur[r * ldz + c] = f2bf(v[i]);
         if (FP8 && a == 1) atomicMax(reinterpret_cast<unsigned*>(s_amax) + r, __float_as_uint(fabsf(bf2f(f2bf(v[i])))));
       }
-      *reinterpret_cast<uint2*>(p.dzT[a] + (size_t)c * Bp + row0 + rg * 4) =
-          make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      if (rg * 4 < RT)
+        *reinterpret_cast<uint2*>(p.dzT[a] + (size_t)c * Bp + row0 + rg * 4) =
+            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     }
   }
 #pragma unroll
@@ -936,8 +958,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
               if ((lane & 15) == 0) atomicMax(reinterpret_cast<unsigned*>(s_amax) + rb + i, __float_as_uint(m));
             }
           }
-          *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
-              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          if (rb < RT)
+            *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
+                make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) s_f32[(rb + i) * D0p + c] = acc[i];
@@ -1070,9 +1093,9 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
   return L;
 }
 
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT>
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT = kRowTile>
 static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
-  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG, BT>;
+  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG, BT, RT>;
   static bool attr_set = false;
   static int max_dyn = 0;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
@@ -1095,19 +1118,19 @@ static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
     ROCFM_REQUIRE(p.Bp / kRowTile <= limit, "deepfm_rows: batch_norm needs every workgroup of the batch resident "
                                             "at once (batch too large for one launch; use engine=torch)");
   }
-  hipLaunchKernelGGL(kern, dim3(p.Bp / kRowTile), dim3(kRowThreads), p.lds.total, stream, p);
+  hipLaunchKernelGGL(kern, dim3(p.Bp / RT), dim3(kRowThreads), p.lds.total, stream, p);
 }
 
 // Static shapes: branch-free train / inference kernels; the diagnostic (stamps, ablations)
 // instantiation only for the benchmark shape's training kernel.
-template <int KP4, class SH, bool BT>
+template <int KP4, class SH, bool BT, int RT>
 static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   if constexpr (SH::kStatic) {
     const bool diag = p.stamps != nullptr || p.ablate != 0;
     if (diag) {
       if constexpr (SH::F == 39 && SH::K == 10 && SH::nl == 3 && !BT) {
         ROCFM_REQUIRE(!p.fp8 && p.train, "deepfm_rows: diagnostics are built for the bf16 training kernel only");
-        launch_rows_impl<KP4, SH, false, kTrain, true, false>(p, stream);
+        launch_rows_impl<KP4, SH, false, kTrain, true, false, RT>(p, stream);
         return;
       } else {
         throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 shape "
@@ -1119,27 +1142,37 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
         throw std::invalid_argument("deepfm_rows: compute_dtype=fp8 supports input layers up to 512 wide");
       } else {
         if (p.train)
-          launch_rows_impl<KP4, SH, true, kTrain, false, BT>(p, stream);
+          launch_rows_impl<KP4, SH, true, kTrain, false, BT, RT>(p, stream);
         else
-          launch_rows_impl<KP4, SH, true, kInfer, false, BT>(p, stream);
+          launch_rows_impl<KP4, SH, true, kInfer, false, BT, RT>(p, stream);
         return;
       }
     }
     if (p.train)
-      launch_rows_impl<KP4, SH, false, kTrain, false, BT>(p, stream);
+      launch_rows_impl<KP4, SH, false, kTrain, false, BT, RT>(p, stream);
     else
-      launch_rows_impl<KP4, SH, false, kInfer, false, BT>(p, stream);
+      launch_rows_impl<KP4, SH, false, kInfer, false, BT, RT>(p, stream);
     return;
   }
   launch_rows_impl<KP4, SH, false, kDynamic, true, BT>(p, stream);
 }
 
+// rows per workgroup (RowsParams::row_tile): 8 doubles the workgroups of a batch (128 instead of
+// 64 at B = 1024 on 256 CUs) at the same per-workgroup weight-fragment traffic; static shapes only
 template <int KP4, class SH>
 static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
-  if (p.tbl_bf16)
-    launch_rows_t<KP4, SH, true>(p, stream);
-  else
-    launch_rows_t<KP4, SH, false>(p, stream);
+  const bool rt8 = SH::kStatic && p.row_tile == 8;
+  if (p.tbl_bf16) {
+    if (rt8)
+      launch_rows_t<KP4, SH, true, 8>(p, stream);
+    else
+      launch_rows_t<KP4, SH, true, 16>(p, stream);
+  } else {
+    if (rt8)
+      launch_rows_t<KP4, SH, false, 8>(p, stream);
+    else
+      launch_rows_t<KP4, SH, false, 16>(p, stream);
+  }
 }
 
 // Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
@@ -1166,6 +1199,7 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Bp % kRowTile == 0 && p.Bp >= p.B, "deepfm_rows: Bp must be a multiple of 16 and >= B");
   ROCFM_REQUIRE((p.Bp % 64) == 0 || !p.train, "deepfm_rows: training needs Bp % 64 == 0");
   p.magicF = (uint32_t)((1ull << 32) / (uint64_t)p.F + 1ull);
+  ROCFM_REQUIRE(p.row_tile == 0 || p.row_tile == 8 || p.row_tile == 16, "deepfm_rows: row_tile must be 0, 8 or 16");
   p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
   if (p.Bp / kRowTile == 0) return;

@@ -281,6 +281,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         if (push) {  // row-shard X3: straight into the owner's receive slot
           const uint32_t d = rr / (uint32_t)p.push_seg, j = rr - d * (uint32_t)p.push_seg;
           reinterpret_cast<float4*>(p.push.slot[d])[(size_t)j * KP4 + u4] = g[u];
+          if (p.push_mirror) reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];
           continue;
         }
         reinterpret_cast<float4*>(p.dense_grad)[idx4[u]] = g[u];

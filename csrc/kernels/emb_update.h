@@ -54,6 +54,10 @@ struct EmbUpdateParams {
   PushTarget push;
   int push_off_keys, push_off_rows;
   int push_seg;
+  // row-shard X3 push: also store each row gradient locally (dense_grad[rr]) — the shadow exchange
+  // (rocfm.parallel.validate) all-to-alls that local copy through RCCL and compares it bitwise
+  // with what the producers pushed into the owners' slots
+  int push_mirror;
 };
 
 struct EmbDenseParams {

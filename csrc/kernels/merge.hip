@@ -406,44 +406,57 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   merged_row_out<KP4>(p, row, w, a, b, acc);
 }
 
-// One thread per (replicated row, float4 column): Σ of the rank segments in rank order (the
-// owner merge's order, so replicated and owned rows take bit-identical updates), then the row
-// optimizer on the replica; the bucket part is cleared for the next step.
+// One thread per replicated row (all KP4 float4 columns): Σ of the rank segments in rank order
+// (the owner merge's order, so replicated and owned rows take bit-identical updates), then the
+// row optimizer on the replica; the bucket part is cleared for the next step.
+// The row's touched-count word is read AND cleared by this one thread.  With the bucket reduced
+// in place (h.zero == h.grads: world 1 / RCCL all-reduce) a per-column thread layout had the
+// c == 0 thread clear the word while sibling columns — in a later wave or workgroup when KP4
+// does not divide 64 — had yet to read it: those columns then skipped (sparse) or took an
+// L2-only update (exact), which made exact + hot rows non-reproducible under CU contention.
 template <int KP4>
-__device__ __forceinline__ void hot_apply_body(const HotApplyParams& h, const int i) {
-  if (i >= h.H * KP4) return;
-  const int r = i / KP4, c = i - r * KP4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+__device__ __forceinline__ void hot_apply_body(const HotApplyParams& h, const int r) {
+  if (r >= h.H) return;
+  float4 acc[KP4];
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   float cnt = 0.f;
   for (int q = 0; q < h.nseg; ++q) {
     const float* seg = h.grads + (size_t)q * h.seg_stride;
-    acc = f4add_m(acc, reinterpret_cast<const float4*>(seg)[(size_t)r * KP4 + c]);
+    const float4* s4 = reinterpret_cast<const float4*>(seg) + (size_t)r * KP4;
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) acc[c] = f4add_m(acc[c], s4[c]);
     cnt += seg[(size_t)h.H * KP4 * 4 + r];
   }
   if (h.zero) {
-    reinterpret_cast<float4*>(h.zero)[(size_t)r * KP4 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c == 0) h.zero[(size_t)h.H * KP4 * 4 + r] = 0.f;
+    float4* z4 = reinterpret_cast<float4*>(h.zero) + (size_t)r * KP4;
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) z4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    h.zero[(size_t)h.H * KP4 * 4 + r] = 0.f;
   }
   const bool has = cnt > 0.f;
   if (!has && !h.dense) return;
-  const size_t at = (size_t)r * KP4 + c;
-  float4 w = reinterpret_cast<const float4*>(h.rows)[at];
-  float4 a = h.s0 ? reinterpret_cast<const float4*>(h.s0)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 b = h.s1 ? reinterpret_cast<const float4*>(h.s1)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
   const OptStep st = opt_step(h.opt, *h.step);
-  float* wc = &w.x;
-  float* ac = &a.x;
-  float* bc = &b.x;
-  const float* gc = &acc.x;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    if (c * 4 + u >= h.K1) continue;
-    const float g = has ? gc[u] * h.grad_scale : 0.f;
-    opt_apply(h.opt, st, wc[u], g + h.l2 * wc[u], ac[u], bc[u]);
+  for (int c = 0; c < KP4; ++c) {
+    const size_t at = (size_t)r * KP4 + c;
+    float4 w = reinterpret_cast<const float4*>(h.rows)[at];
+    float4 a = h.s0 ? reinterpret_cast<const float4*>(h.s0)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 b = h.s1 ? reinterpret_cast<const float4*>(h.s1)[at] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* wc = &w.x;
+    float* ac = &a.x;
+    float* bc = &b.x;
+    const float* gc = &acc[c].x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (c * 4 + u >= h.K1) continue;
+      const float g = has ? gc[u] * h.grad_scale : 0.f;
+      opt_apply(h.opt, st, wc[u], g + h.l2 * wc[u], ac[u], bc[u]);
+    }
+    reinterpret_cast<float4*>(h.rows)[at] = w;
+    if (h.s0) reinterpret_cast<float4*>(h.s0)[at] = a;
+    if (h.s1) reinterpret_cast<float4*>(h.s1)[at] = b;
   }
-  reinterpret_cast<float4*>(h.rows)[at] = w;
-  if (h.s0) reinterpret_cast<float4*>(h.s0)[at] = a;
-  if (h.s1) reinterpret_cast<float4*>(h.s1)[at] = b;
 }
 
 // Roles by workgroup: [merge apply | MLP optimizer | serve of the NEXT step's requests (bounded-
@@ -481,7 +494,7 @@ void launch_search_t(const MergeParams& p, const DenseApplyParams* d, const Shar
   if (sv) ss = *sv;
   HotApplyParams hh{};
   if (hot) hh = *hot;
-  const int n_hot = hot ? cdiv(hot->H * KP4, kApplyThreads) : 0;
+  const int n_hot = hot ? cdiv(hot->H, kApplyThreads) : 0;  // one thread per replicated row
   if (n_apply + n_dense + n_serve + n_hot == 0) return;
   const dim3 grid(n_apply + n_dense + n_serve + n_hot), block(kApplyThreads);
   if (p.W <= 8)

@@ -25,6 +25,11 @@ from typing import List, Optional
 from .config import Config, parse_flags
 
 
+def _remaining_steps(max_steps: int, global_step: int) -> Optional[int]:
+    """Steps left to reach the global-step target ``max_steps`` (None = no limit)."""
+    return max(0, max_steps - global_step) if max_steps else None
+
+
 def run(cfg: Config) -> dict:
     import torch
 
@@ -53,7 +58,12 @@ def run(cfg: Config) -> dict:
         tr_fifos, va_fifos = pipe_mode_sources(cfg.num_epochs, info.local_rank, cfg.training_channel_name,
                                                cfg.evaluation_channel_name)
         out["channels"] = {"train": tr_fifos, "eval": va_fifos}
-        out["train"] = est.train(tr_fifos, 1, max_steps=cfg.max_steps or None)
+        # max_steps is a global-step target, as in file mode: a restarted job resumes toward it
+        max_steps = _remaining_steps(cfg.max_steps, est.global_step)
+        if max_steps is not None and max_steps <= 0:
+            out["train"] = {"global_step": est.global_step, "steps": 0}
+        else:
+            out["train"] = est.train(tr_fifos, 1, max_steps=max_steps)
         if va_fifos:
             out["eval"] = est.evaluate(va_fifos)
         if cfg.servable_model_dir:
@@ -70,7 +80,7 @@ def run(cfg: Config) -> dict:
             out["epochs"] = est.train_and_evaluate(tr_files, va_files, cfg.num_epochs)
         else:
             ep0, skip = est.resume_point(tr_files, cfg.num_epochs)  # restarted job: fast-forward
-            max_steps = (cfg.max_steps - est.global_step) if cfg.max_steps else None
+            max_steps = _remaining_steps(cfg.max_steps, est.global_step)
             if max_steps is not None and max_steps <= 0:
                 out["train"] = {"global_step": est.global_step, "steps": 0}
             else:

@@ -110,6 +110,11 @@ class Config:
     hbm_cache: bool = True  # single GPU, >1 epoch, no shuffle: keep the decoded first epoch in HBM and
     #                         train later epochs from it (the reference re-reads + re-parses every epoch)
     hbm_cache_gb: float = 64.0  # budget for that cache (decoded epoch: B·(8F + 4) bytes per batch)
+    # pre-decoded on-disk cache (rocfm.data.cache): each rank's first pass over its training shard is
+    # written raw (int32 ids, f32 values / labels) under this directory and every later epoch — and
+    # any later job on the same files, shard and batch size — memory-maps it instead of re-decoding
+    # the TFRecords ("" = off; file mode without record shuffle only)
+    decoded_cache_dir: str = ""
     ckpt_poll_steps: int = 200  # world > 1: steps between rank 0's broadcasts of the time-based save decision
     keep_checkpoint_max: int = 5
     eval_every_epoch: bool = True

@@ -190,10 +190,6 @@ class Estimator:
         fast-forwards the input stream (resume after a restart without re-training consumed data;
         the reference re-reads from the start, an Estimator limitation rocfm does not copy)."""
         cfg = self.cfg
-        # single GPU + graphs: groups of S batches decoded into one pinned ring, moved by the engine
-        # with one copy per group (copy stream → HBM ring) and trained S steps per graph launch
-        stream = self.engine_name == "fused" and not hasattr(self.eng, "eng") and cfg.use_hip_graph \
-            and self.device.type == "cuda"
         S = 16
         ds = self._dataset(files, num_epochs, training=True)
         limit = self._agreed_steps(ds)
@@ -201,6 +197,14 @@ class Estimator:
             limit = max(0, limit - skip_batches)
         if max_steps:
             limit = max_steps if limit is None else min(limit, max_steps)
+        # fused engine + graphs: groups of S batches decoded into one pinned ring, moved by the
+        # engine with one copy per group (copy stream → HBM ring) and trained S steps per graph
+        # launch — on one GPU, and with several ranks (DP / row-shard graphs with the exchange
+        # inline) whenever every rank streams an agreed number of batches and the exchanges are
+        # capturable (p2p, or RCCL)
+        stream = self.engine_name == "fused" and cfg.use_hip_graph and self.device.type == "cuda" \
+            and hasattr(self.eng, "train_stream") and getattr(self.eng, "graph_collectives", True) \
+            and (self.world == 1 or limit is not None)
         if stream:
             batches = self._host_batches(ds.groups(S, hold=2, skip=skip_batches, limit=limit))
         else:
@@ -265,6 +269,20 @@ class Estimator:
                 cache_nb = nb
                 batches = self._host_batches(self._dataset(files, 1, training=True).groups(S, hold=2))
                 batches = _timed(batches, timer)
+        # pre-decoded on-disk cache (rocfm.data.cache): the first pass over this rank's shard is
+        # written through, every later pass (later epochs, restarted or repeated jobs) memory-maps it
+        if stream and cfg.decoded_cache_dir and not cfg.perform_shuffle and not cfg.pipe_mode \
+                and cfg.on_bad_record != "skip":
+            from .data.cache import DecodedCache, cached_epochs
+
+            dc = DecodedCache.for_dataset(self._dataset(files, 1, training=True), cfg.decoded_cache_dir)
+            first = lambda sk, lim: self._dataset(files, 1, training=True).groups(S, hold=2, skip=sk, limit=lim)
+            if cache_nb:  # the HBM cache replays epochs 2..: only the first pass comes from the loader / disk
+                src = cached_epochs(dc, first, 1, S, hold=2)
+            else:
+                src = cached_epochs(dc, first, num_epochs, S, hold=2, skip=skip_batches, limit=limit)
+            batches = _timed(self._host_batches(src), timer)
+            self._log({"event": "decoded_cache", "path": dc.path, "complete": dc.complete()})
         try:
             with trace_range("train"):
                 if stream:

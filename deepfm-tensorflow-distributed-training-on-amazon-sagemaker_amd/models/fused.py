@@ -135,6 +135,11 @@ class FusedDeepFM:
         self.loss_code = 0 if spec.loss_type == "log_loss" else 1
         self.lr_scale = 1.0
         self.force_generic = bool(force_generic_kernels)
+        # examples per row-kernel workgroup (compile-time-shape kernels): 16, or 8 for twice the
+        # workgroups (ROCFM_ROW_TILE; 0 = the kernel's default)
+        self.row_tile = int(os.environ.get("ROCFM_ROW_TILE", "0"))
+        if self.row_tile not in (0, 8, 16):
+            raise ValueError(f"ROCFM_ROW_TILE must be 0, 8 or 16, got {self.row_tile}")
         if compute_dtype not in ("bf16", "fp8"):
             raise ValueError(f"compute_dtype must be bf16 or fp8, got {compute_dtype!r}")
         self.compute_dtype = compute_dtype
@@ -302,6 +307,7 @@ class FusedDeepFM:
         rp.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         rp.force_generic = 1 if self.force_generic else 0
         rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
+        rp.row_tile = self.row_tile
         rp.set_dims(L.dims)
         for l in range(L.nl):
             rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),
@@ -818,8 +824,6 @@ class FusedDeepFM:
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
             gm.replay()
-            if getattr(self, "_m_serial_side", False):  # (see FusedRowShard: exact + replicated rows)
-                side.wait_stream(main)
             side.wait_event(before)
             with torch.cuda.stream(side):
                 gs.replay()
@@ -880,7 +884,7 @@ class FusedDeepFM:
             self._precapture_multi(self._m_graphs, ("m",), n, self._multi_body)
 
     def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
-                     ring_batches: int = 0) -> int:
+                     ring_batches: int = 0, build=None, run=None) -> int:
         """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
 
         Batches are copied host → HBM on a copy stream into a device ring of 4·S batch slots, two
@@ -896,6 +900,9 @@ class FusedDeepFM:
         ``ring_batches`` ≥ the number of batches streamed sizes the HBM ring to hold them all, so
         that afterwards ``stream_ring()[i]`` is the i-th batch of this call (the decoded-epoch HBM
         cache of the Estimator: later epochs train from it via attach_pool).
+        ``build(S)`` / ``run(n)`` (the distributed wrappers, rocfm.parallel): (re)build the
+        multi-step structures for the attached ring, and launch one n-step graph with the step's
+        exchange inline; default: this engine's single-GPU graphs.
         """
         S = self._multi_S(int(steps_per_graph))[1]
         R = max(4 * S, (int(ring_batches) + S - 1) // S * S)
@@ -922,24 +929,30 @@ class FusedDeepFM:
             return e
 
         pending = []  # (event, host batch) kept alive until its copy has completed
+        carry = [None]  # the part of a group that did not fit the previous graph (same host memory)
 
         def stage(k):  # copy up to k more batches; returns how many were available
             nonlocal staged
             got = 0
             while got < k:
-                while len(pending) > hold - 1:  # the item `hold` back is recycled by this next()
-                    pending.pop(0)[0].synchronize()
-                b = next(it, None)
-                if b is None:
-                    break
+                if carry[0] is not None:
+                    b, carry[0] = carry[0], None
+                else:
+                    while len(pending) > hold - 1:  # the item `hold` back is recycled by this next()
+                        pending.pop(0)[0].synchronize()
+                    b = next(it, None)
+                    if b is None:
+                        break
                 ids, vals, labels = b
                 if ids.dim() == 2:
                     ids, vals, labels = ids.unsqueeze(0), vals.unsqueeze(0), labels.unsqueeze(0)
                 n = ids.shape[0]
                 if ids.shape[1] != self.B:
                     raise ValueError(f"batch has {ids.shape[1]} rows, engine built for {self.B}")
-                if got + n > k:
-                    raise ValueError(f"a group of {n} batches does not fit the {k - got} left of this graph (S={S})")
+                if got + n > k:  # split: the rest goes to the next graph's staging
+                    m = k - got
+                    carry[0] = (ids[m:], vals[m:], labels[m:])
+                    ids, vals, labels, n = ids[:m], vals[:m], labels[:m], m
                 with torch.cuda.stream(copy):
                     o = 0
                     while o < n:  # contiguous ring slots (split at the ring's end)
@@ -960,7 +973,9 @@ class FusedDeepFM:
             return 0
         cevs = [mark(copy)]  # cevs[j]: copies read by graph j's side chain (graph j+1's batches)
         main.wait_event(cevs[0])
-        if getattr(self, "m_req", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
+        if build is not None:
+            build(S)
+        elif getattr(self, "m_req", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
             self._build_multi(S)
             self._m_pool = self.pool_ids
         self._prime_multi()  # prepares steps i0 .. i0+S-1 from the ring
@@ -975,7 +990,10 @@ class FusedDeepFM:
             more = stage(S)
             cevs.append(mark(copy))
             self.sort_stream.wait_event(cevs[j])
-            self._run_multi_graph(n)
+            if run is not None:
+                run(n)
+            else:
+                self._run_multi_graph(n)
             sevs.append(self._m_side_ev)
             if after_steps is not None:
                 after_steps(i0 + done, n)

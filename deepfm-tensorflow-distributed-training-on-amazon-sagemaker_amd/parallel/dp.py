@@ -189,6 +189,44 @@ def attach_torch_dp(eng, embedding_update: str = "sparse") -> None:
         eng.exchange_rows = exchange_rows
 
 
+def shadow_prefix(w, batches, after_steps=None):
+    """Train the shadow-validation window of a distributed fused engine ``w`` (its first p2p steps,
+    per step with the collective shadow) from the head of a host batch stream.  Returns (the rest
+    of the stream, steps trained).  Items are single batches or stacked groups, as in
+    FusedDeepFM.train_stream; a group that straddles the window's end is split."""
+    import itertools
+
+    shadow = getattr(w, "shadow", None)
+    if shadow is None or not shadow.active:
+        return batches, 0
+    it = iter(batches)
+    dev = w.eng.device
+    got, rest = [], []
+    while len(got) < shadow.left:
+        b = next(it, None)
+        if b is None:
+            break
+        ids, vals, labels = b
+        if ids.dim() == 2:
+            ids, vals, labels = ids.unsqueeze(0), vals.unsqueeze(0), labels.unsqueeze(0)
+        k = min(ids.shape[0], shadow.left - len(got))
+        for i in range(k):
+            got.append((ids[i].to(dev), vals[i].to(dev), labels[i].to(dev)))
+        if k < ids.shape[0]:  # the rest of this group is trained by the stream (own host copy)
+            rest.append((ids[k:].clone(), vals[k:].clone(), labels[k:].clone()))
+    if not got:
+        return itertools.chain(rest, it), 0
+    e = w.eng
+    i0 = e._i
+    w.attach_pool(torch.stack([g[0] for g in got]), torch.stack([g[1] for g in got]),
+                  torch.stack([g[2] for g in got]), start=(-i0) % len(got))
+    for _ in got:
+        w.train_step()
+    if after_steps is not None:
+        after_steps(i0, len(got))
+    return itertools.chain(rest, it), len(got)
+
+
 # ================================================================================================
 # fused engine
 # ================================================================================================
@@ -324,6 +362,15 @@ class FusedDataParallel:
             e.wgrad_params[p].grads = e.dense_grads_flat.data_ptr()
         self._graphs = {}
         self._warm = 0
+        # self-validation (rocfm.parallel.validate): the first steps of a p2p run are shadowed by
+        # the collective; replica digests in check()
+        from .validate import Shadow, fault_rank
+
+        self.shadow = Shadow(e.device, steps=None if (self.p2p is not None and self.world > 1) else 0)
+        self.shadow.corrupt = fault_rank("corrupt_push", self.rank)
+        self._shadow_buf = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device) \
+            if self.shadow.active else None
+        self._corrupt_replica = fault_rank("corrupt_replica", self.rank)
 
     @property
     def fused_push(self) -> bool:
@@ -378,6 +425,8 @@ class FusedDataParallel:
     def _exchange(self):
         if self.p2p is not None:  # fused push: only the row count + the data hand-off are left
             self.p2p.push(self.p2p_params)
+            if self.shadow.active:
+                self._shadow_exchange()
             return
         if self.world == 1 and not self.force:  # one rank: recv aliases send (dp) / the bucket is the sum
             return
@@ -401,7 +450,7 @@ class FusedDataParallel:
             e.H.emb_dense_update(e.emb_dense_params[p], s)
 
     def _run(self, key, fn, collectives: bool = False):
-        if not self.use_graph or self._warm < 4:
+        if not self.use_graph or self._warm < 4 or self.shadow.active:
             fn()
             return
         g = self._graphs.get(key)
@@ -439,7 +488,69 @@ class FusedDataParallel:
             self._run(("b", p), lambda: self._phase_b(p))
         self._warm += 1
         e._i += 1
+        if self.shadow.step_done():
+            self._shadow_finish()
         self._after_steps(e._i - 1, e._i)
+
+    # ---- self-validation (rocfm.parallel.validate) ----------------------------------------------
+    def _shadow_exchange(self) -> None:
+        """The p2p all-gather just delivered every rank's slot: gather this rank's own slot through
+        the collective as well, compare bitwise, and let the merge consume the collective's copy."""
+        got = self.p2p.recv_tensor(torch.float32, (self.world * self.S,))
+        self.shadow.corrupt_(got)
+        own = got[self.rank * self.S:(self.rank + 1) * self.S].clone()
+        _all_gather_flat(self._shadow_buf, own)
+        self.shadow.compare(got, self._shadow_buf)
+
+    def _shadow_finish(self) -> None:
+        if self.shadow.finish():
+            msg = (f"exchange: p2p result differed from the collective in the first "
+                   f"{self.shadow.compared} validated exchanges on some rank; falling back to RCCL")
+            import logging
+
+            logging.getLogger("rocfm").warning(msg)
+            if self.rank == 0:
+                print(f"[rocfm] {msg}", flush=True)
+            self._fallback_to_collective()
+        self._shadow_buf = None
+
+    def _fallback_to_collective(self) -> None:
+        """Agreed switch from the p2p push to the process group's all-gather (every rank)."""
+        e, H = self.eng, self.eng.H
+        torch.cuda.synchronize(self.device)
+        self._graphs = {}
+        self._m_dp_S = None
+        self.p2p.close()
+        self.p2p = None
+        self.push_target = None
+        self.exchange = "rccl"
+        self.graph_collectives = self.use_graph and collectives_capturable()
+        self.recv = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device)
+        self._recv_ptr = self.recv.data_ptr()
+        for p in range(2):
+            for prm in (e.rows_params[p], e.wgrad_params[p], self.export_params[p]):
+                prm.push = H.PushTarget()
+            mp_ = self.merge_params[p]
+            mp_.keys = self._recv_ptr + 4 * self.off_keys
+            mp_.rows = self._recv_ptr + 4 * self.off_rows
+            mp_.counts = self._recv_ptr + 4 * self.off_cnt
+            e.dense_apply_params[p].grads = self._recv_ptr
+
+    def replicated_tensors(self):
+        e = self.eng
+        return [e.dense, e.emb, e.steps] + list(e.dense_slots) + list(e.emb_slots)
+
+    def verify_replicas(self) -> bool:
+        """Collective: every rank's replica (MLP, tables, optimizer slots, step) is bit-identical."""
+        if self.world == 1:
+            return True
+        torch.cuda.synchronize(self.device)
+        if self._corrupt_replica:  # fault injection (tests): one rank's replica drifts
+            self._corrupt_replica = False
+            self.eng.dense.view(-1)[0] += 1e-3
+        from .validate import replicas_agree
+
+        return replicas_agree(self.replicated_tensors())
 
     # ---- multi-step graphs (pool mode, capturable collectives) -----------------------------------
     # The single-GPU pipeline of FusedDeepFM (serial main stream per step, one batched fetch+sort
@@ -449,6 +560,7 @@ class FusedDataParallel:
     #            → emb_dense_update
     def _build_multi_dp(self, Smax: int) -> None:
         e, H = self.eng, self.eng.H
+        self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
         self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and self.world <= SEARCH_MAX_W
@@ -542,11 +654,40 @@ class FusedDataParallel:
         """``n`` steps from the attached pool.  With capturable collectives (RCCL) the steps are
         replayed from multi-step graphs (``steps_per_graph`` steps each, exchange included)."""
         e = self.eng
+        while n > 0 and self.shadow.active:  # validated steps first (eager, collective shadow)
+            self.train_step()
+            n -= 1
+        if n <= 0:
+            return
         if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
             self._train_steps_multi(n, steps_per_graph)
             return
         for _ in range(n):
             self.train_step()
+
+    # ---- streamed training (the Estimator's loader path at world > 1) ----------------------------
+    def _stream_build(self, S: int) -> None:
+        e = self.eng
+        if getattr(self, "_m_dp_S", None) != S or getattr(e, "_m_pool", None) is not e.pool_ids:
+            self._build_multi_dp(S)
+
+    def _stream_run(self, n: int) -> None:
+        e = self.eng
+        e._launch_multi(self._graphs, ("mdp",), n, self._enqueue_multi_dp, capture_error_mode="thread_local")
+        self._after_steps(e._i - n, e._i)
+
+    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
+                     ring_batches: int = 0) -> int:
+        """Host batches (single or stacked groups) → the HBM ring → multi-step graphs with the
+        exchange captured inline, like FusedDeepFM.train_stream (the single-GPU path): the per-step
+        H2D synchronisation of the per-step path is gone.  The shadow-validation window (first p2p
+        steps) trains per step first.  Every rank must stream the same number of batches."""
+        if not (self.graph_collectives and self.use_graph):
+            raise RuntimeError("train_stream needs capturable exchanges (p2p, or RCCL with graphs)")
+        batches, done = shadow_prefix(self, batches, after_steps)
+        n = self.eng.train_stream(batches, steps_per_graph, after_steps, hold, ring_batches,
+                                  build=self._stream_build, run=self._stream_run)
+        return done + n
 
     def close(self) -> None:
         """Release the captured graphs (required before destroy_process_group when they hold
@@ -557,16 +698,19 @@ class FusedDataParallel:
             self.p2p.close()
             self.p2p = None
 
-    def check(self) -> None:
+    def check(self, replicas: bool = True) -> None:
         """Raise if a rank exported more unique rows than the exchange capacity (rows past the
-        capacity would have been dropped from that step's update), or if a p2p exchange wait
-        timed out (a peer never arrived: its data for that step is missing)."""
+        capacity would have been dropped from that step's update), if a p2p exchange wait timed
+        out (a peer never arrived: its data for that step is missing), or (``replicas``; collective)
+        if the replicas are no longer bit-identical across ranks."""
         self.eng.check()
         if self.p2p is not None and self.p2p.errored():
             raise RuntimeError("DP p2p exchange: a peer wait timed out (rank missing or stalled)")
         if self.overflowed():
             raise RuntimeError(f"DP exchange overflow: a rank exported more unique rows than capacity {self.cap}; "
                                "rebuild with a larger capacity (default batch_size*field_size never overflows)")
+        if replicas and not self.verify_replicas():
+            raise RuntimeError("DP replicas diverged: the ranks' variables / optimizer slots are not bit-identical")
 
     def overflowed(self) -> bool:
         """True if, in any step so far, a rank produced more unique rows than the exchange capacity

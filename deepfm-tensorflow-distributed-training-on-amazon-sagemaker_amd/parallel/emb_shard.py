@@ -40,6 +40,7 @@ the fused DeepFM step).
 from __future__ import annotations
 
 import dataclasses
+import logging
 import math
 import os
 from collections import OrderedDict
@@ -52,6 +53,7 @@ from ..models.deepfm import TRUNC_NORMAL_STD, ModelSpec, init_params
 from ..optim import OptHParams, apply_dense, apply_rows, slot_names
 
 PAD = -1  # int32 view of 0xFFFFFFFF (request padding)
+log = logging.getLogger("rocfm")
 
 
 def _world_rank():
@@ -514,50 +516,7 @@ class FusedRowShard:
         e.dense_grads_flat = self.mlp_bucket[:self.P]
         slots = [cap, cap * Kp, cap * Kp, self.PX] + ([cap] if self.staleness else [])
         exs = open_exchanges(slots, dev, exchange, extra_floats=[0, NH * Kp] + [0] * (len(slots) - 2))
-        self.exchange = "p2p" if exs else "rccl"
-        self.mlp_push = self.grad_push = None  # X4 / X3 producer-side push targets (below)
-        self.p2p_x = {}
-        self.recv_pair = None  # staleness 1: request lists of consecutive steps (parity)
-        if exs:
-            self.x_ids, self.x_rows, self.x_grad, self.x_mlp = exs[:4]
-            self.x_all = list(exs)
-            self.recv_ids = self.x_ids.recv_tensor(torch.int32, (M,))
-            self.recv_ids.fill_(PAD)
-            self.rows_in = self.x_rows.recv_tensor(torch.float32, (M + NH, Kp))
-            self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
-            for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
-                self.p2p_x[t.data_ptr()] = ex
-            if self.staleness:
-                r2 = exs[4].recv_tensor(torch.int32, (M,))
-                r2.fill_(PAD)
-                self.p2p_x[r2.data_ptr()] = exs[4]
-                self.recv_pair = [self.recv_ids, r2]
-            self.graph_collectives = use_graph  # push kernels are capturable whatever the backend
-            # X4 pushed by its producer (csrc/kernels/push.h): the wgrad workgroups store the MLP
-            # gradients straight into every rank's X4 slot from inside the step tail, and the X4
-            # launch only hands the data off.  Same switch as the DP push
-            # (p2p.producer_push_enabled); replicated hot rows keep the copy (their sums ride the
-            # same bucket from the embedding role).
-            from .p2p import producer_push_enabled
-
-            if NH == 0 and producer_push_enabled(self.x_mlp):
-                self.mlp_push = self.x_mlp.push_target()
-                # X3 likewise: the embedding role stores each requested row's gradient sum straight
-                # into its owner's slot (row o·cap + j → owner o, row j)
-                self.grad_push = self.x_grad.push_target()
-        elif self.W == 1 and not self.force:
-            # one rank: every exchange is the identity, so the receive side IS the send side (rows
-            # and row gradients share one buffer each; the request list each step reads is that
-            # step's own send list, bound per step below) — no copies in the step
-            self.recv_ids = None
-            self.rows_in = self.rows_out
-            self.grad_back = self.grad_stage
-        else:
-            self.recv_ids = torch.full((M,), PAD, **i32)
-            self.rows_in = torch.zeros(M + NH, Kp, **f32)
-            self.grad_back = torch.zeros(M, Kp, **f32)
-            if self.staleness:
-                self.recv_pair = [self.recv_ids, torch.full((M,), PAD, **i32)]
+        self._bind_exchange(exs)
         self._p2p_params = {}
         # owner merge: binary search in the sorted request lists (small worlds), or position maps
         # filled by a scatter launch (direct addressing over the local rows, or a W·cap hash table
@@ -565,8 +524,6 @@ class FusedRowShard:
         from .dp import SEARCH_MAX_W, MergeMaps
 
         self.maps = MergeMaps(W, cap, Vs, dev) if W > SEARCH_MAX_W else None
-        self.rows_x = self.rows_in[:M]  # the X2 all-to-all part of rows_in
-        self.hot_rep = self.rows_in[M:]  # the replica
         self.hot_slots = [torch.zeros(NH, Kp, **f32) for _ in e.emb_slots] if NH else []
         self.hot_ids_dev = torch.full((max(NH, 1),), PAD, **i32)
         self.n_hot = 0
@@ -581,6 +538,78 @@ class FusedRowShard:
         self._build()
         if self.maps is not None:
             H.merge_init(self.owner_params[0], e.stream_ptr)
+        # self-validation (rocfm.parallel.validate): the first steps of a p2p run shadow every
+        # exchange through the collective; replica digests (MLP + replicated rows) in check()
+        from .validate import Shadow, fault_rank
+
+        self.shadow = Shadow(dev, steps=None if (self.exchange == "p2p" and W > 1) else 0)
+        self.shadow.corrupt = fault_rank("corrupt_push", r)
+        self._corrupt_replica = fault_rank("corrupt_replica", r)
+        self._set_mirror(self.shadow.active)
+
+    def _set_mirror(self, on: bool) -> None:
+        """X3 producer push: also keep each row gradient in grad_stage (the shadow's local copy)."""
+        for p in range(2):
+            self.eng.emb_params[p].push_mirror = 1 if (on and self.grad_push is not None) else 0
+
+    def _bind_exchange(self, exs) -> None:
+        """Receive-side buffers of the X1-X4 exchanges: the peer-mapped p2p slots (``exs``), the
+        send buffers themselves (one rank), or plain tensors for the collectives."""
+        from .p2p import producer_push_enabled
+
+        W, M, NH, Kp, dev = self.W, self.M, self.NH, self.eng.Kp, self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.exchange = "p2p" if exs else "rccl"
+        self.mlp_push = self.grad_push = None  # X4 / X3 producer-side push targets (below)
+        self.p2p_x = {}
+        self.recv_pair = None  # staleness 1: request lists of consecutive steps (parity)
+        self._p2p_params = {}
+        if exs:
+            self.x_ids, self.x_rows, self.x_grad, self.x_mlp = exs[:4]
+            self.x_all = list(exs)
+            self.recv_ids = self.x_ids.recv_tensor(torch.int32, (M,))
+            self.recv_ids.fill_(PAD)
+            self.rows_in = self.x_rows.recv_tensor(torch.float32, (M + NH, Kp))
+            self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
+            for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
+                self.p2p_x[t.data_ptr()] = ex
+            if self.staleness:
+                r2 = exs[4].recv_tensor(torch.int32, (M,))
+                r2.fill_(PAD)
+                self.p2p_x[r2.data_ptr()] = exs[4]
+                self.recv_pair = [self.recv_ids, r2]
+            self.graph_collectives = self.use_graph  # push kernels are capturable whatever the backend
+            # X4 pushed by its producer (csrc/kernels/push.h): the wgrad workgroups store the MLP
+            # gradients straight into every rank's X4 slot from inside the step tail, and the X4
+            # launch only hands the data off.  Same switch as the DP push
+            # (p2p.producer_push_enabled); replicated hot rows keep the copy (their sums ride the
+            # same bucket from the embedding role).
+            if NH == 0 and producer_push_enabled(self.x_mlp):
+                self.mlp_push = self.x_mlp.push_target()
+                # X3 likewise: the embedding role stores each requested row's gradient sum straight
+                # into its owner's slot (row o·cap + j → owner o, row j)
+                self.grad_push = self.x_grad.push_target()
+        elif W == 1 and not self.force:
+            # one rank: every exchange is the identity, so the receive side IS the send side (rows
+            # and row gradients share one buffer each; the request list each step reads is that
+            # step's own send list, bound per step below) — no copies in the step
+            self.x_all = []
+            self.recv_ids = None
+            self.rows_in = self.rows_out
+            self.grad_back = self.grad_stage
+        else:
+            self.x_all = []
+            self.recv_ids = torch.full((M,), PAD, **i32)
+            self.rows_in = torch.zeros(M + NH, Kp, **f32)
+            self.grad_back = torch.zeros(M, Kp, **f32)
+            if self.staleness:
+                self.recv_pair = [self.recv_ids, torch.full((M,), PAD, **i32)]
+            from .dp import collectives_capturable
+
+            self.graph_collectives = self.use_graph and collectives_capturable()
+        self.rows_x = self.rows_in[:M]  # the X2 all-to-all part of rows_in
+        self.hot_rep = self.rows_in[M:]  # the replica
 
     # ---- kernel parameter blocks ------------------------------------------------------------------
     def _route_params(self, ids, rsv, send, local, skl, counts, n):
@@ -849,7 +878,7 @@ class FusedRowShard:
             H.emb_dense_update(e.emb_dense_params[p], s)
 
     def _run(self, key, fn, collectives: bool = False):
-        if not self.use_graph or self._warm < 4:
+        if not self.use_graph or self._warm < 4 or self.shadow.active:
             fn()
             return
         g = self._graphs.get(key)
@@ -877,6 +906,11 @@ class FusedRowShard:
                 else:
                     prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
             ex.push(prm)
+            if self.shadow.active:  # the same all-to-all through the collective, compared bitwise
+                self.shadow.corrupt_(out)
+                want = torch.empty_like(out)
+                all_to_all_equal(want, inp)
+                self.shadow.compare(out, want)
         elif self.W > 1 or self.force:
             all_to_all_equal(out, inp)
         else:
@@ -899,12 +933,14 @@ class FusedRowShard:
     def _set_push(self, rows, wp, ep) -> None:
         """X4 / X3 producer push: the row kernel raises "entered" for both (their consumer, the
         previous update launch, is done), the wgrad role stores X4 and the embedding role X3."""
-        if self.mlp_push is not None:
-            rows.push = self.mlp_push
-            wp.push = self.mlp_push
+        none = self.H.PushTarget()  # W = 0: no push (also clears targets after a fallback)
+        mlp = self.mlp_push if self.mlp_push is not None else none
+        rows.push, wp.push = mlp, mlp
         if self.grad_push is not None:
             rows.push2 = self.grad_push
             ep.push, ep.push_seg = self.grad_push, self.cap
+        else:
+            rows.push2, ep.push, ep.push_seg = none, none, 0
 
     def _allreduce_mlp(self) -> None:
         """X4: the MLP gradients of every rank (p2p all-gather; the sum happens in dense_apply)."""
@@ -915,6 +951,15 @@ class FusedRowShard:
                 n = 0 if self.mlp_push is not None else self.PX
                 prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), n)
             self.x_mlp.push(prm)
+            if self.shadow.active:  # X4 is an all-gather: this rank's own slot holds its payload
+                from .dp import _all_gather_flat
+
+                got = self.x_mlp.recv_tensor(torch.float32, (self.W * self.x_mlp.slot,))
+                self.shadow.corrupt_(got)
+                want = torch.empty_like(got)
+                sl = self.x_mlp.slot
+                _all_gather_flat(want, got[self.rank * sl:(self.rank + 1) * sl].clone())
+                self.shadow.compare(got, want)
         elif self.W > 1 or self.force:
             all_reduce_(self.mlp_bucket)  # MLP grads + replicated-row sums, one collective
 
@@ -979,7 +1024,55 @@ class FusedRowShard:
             self._run(("update", p), lambda: self._phase_update(p))
         self._warm += 1
         e._i += 1
+        if self.shadow.step_done():
+            self._shadow_finish()
         self._after_steps(e._i - 1, e._i)
+
+    # ---- self-validation (rocfm.parallel.validate) ----------------------------------------------
+    def _shadow_finish(self) -> None:
+        self._set_mirror(False)
+        if self.shadow.finish():
+            msg = (f"row-shard exchange: p2p results differed from the collective in the first "
+                   f"{self.shadow.compared} validated exchanges on some rank; falling back to RCCL")
+            log.warning(msg)
+            if self.rank == 0:
+                print(f"[rocfm] {msg}", flush=True)
+            self._fallback_to_collective()
+
+    def _fallback_to_collective(self) -> None:
+        """Agreed switch of X1-X4 from the p2p pushes to the process group's collectives (every
+        rank).  The receive buffers' contents (replica, already-served rows / requests) move over."""
+        torch.cuda.synchronize(self.device)
+        self._graphs = {}
+        self._ms_S = None
+        old = [self.rows_in, self.grad_back] + (list(self.recv_pair) if self.recv_pair else [self.recv_ids])
+        keep = [t.clone() for t in old]
+        xs = self.x_all
+        self._bind_exchange(None)
+        new = [self.rows_in, self.grad_back] + (list(self.recv_pair) if self.recv_pair else [self.recv_ids])
+        for dst, src in zip(new, keep):
+            dst.copy_(src)
+        torch.cuda.synchronize(self.device)
+        for ex in xs:
+            ex.close()
+        self._build()
+
+    def replicated_tensors(self):
+        e = self.eng
+        return [e.dense, e.steps, self.hot_rep] + list(e.dense_slots) + list(self.hot_slots)
+
+    def verify_replicas(self) -> bool:
+        """Collective: the replicated state (MLP, its slots, the step, replicated hot rows) is
+        bit-identical on every rank."""
+        if self.W == 1:
+            return True
+        torch.cuda.synchronize(self.device)
+        if self._corrupt_replica:  # fault injection (tests)
+            self._corrupt_replica = False
+            self.eng.dense.view(-1)[0] += 1e-3
+        from .validate import replicas_agree
+
+        return replicas_agree(self.replicated_tensors())
 
     def _after_steps(self, i0: int, i1: int) -> None:
         if self.check_every and i1 // self.check_every != i0 // self.check_every:
@@ -994,6 +1087,11 @@ class FusedRowShard:
 
     def train_steps(self, n: int, steps_per_graph: int = 16) -> None:
         e = self.eng
+        while n > 0 and self.shadow.active:  # validated steps first (eager, collective shadow)
+            self.train_step()
+            n -= 1
+        if n <= 0:
+            return
         if self.graph_collectives and self.use_graph and not e._ring and steps_per_graph > 1:
             self._train_steps_multi(n, steps_per_graph)
             return
@@ -1042,6 +1140,7 @@ class FusedRowShard:
     # owner merge ‖ MLP optimizer → merge apply, collectives captured inline.
     def _build_multi_rs(self, Smax: int) -> None:
         e, H = self.eng, self.H
+        self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         W, cap, n, F = self.W, self.cap, self.n, e.F
         e._build_multi(Smax, shard=(W, self.Vs) + ((self.hot_ids_dev[: self.n_hot],) if self.n_hot else ()))
         e._m_pool = e.pool_ids
@@ -1100,11 +1199,6 @@ class FusedRowShard:
                 H.shard_route(rp, stream.cuda_stream)
 
         e._m_post = route_all
-        # replicated rows: the side chain of graph N (next batches' fetch, sort, route) runs AFTER
-        # main graph N instead of beside it.  Beside it, 4 identical exact-mode runs of ≥ 2 graphs
-        # were not bitwise equal (one graph, or this serialisation, were) and a sparse-mode run
-        # missed the single-GPU result once; the shared state is still to be found (README)
-        e._m_serial_side = self.NH > 0
         self._ms_S = Smax
 
     def _enqueue_multi_rs(self, q: int, S: int) -> None:
@@ -1152,6 +1246,40 @@ class FusedRowShard:
         e._primed = False
         self._pre_served = False
 
+    # ---- streamed training (the Estimator's loader path at world > 1) ----------------------------
+    def _stream_build(self, S: int) -> None:
+        e = self.eng
+        if getattr(self, "_ms_S", None) != S or getattr(e, "_m_pool", None) is not e.pool_ids:
+            self._build_multi_rs(S)
+
+    def _stream_run(self, n: int) -> None:
+        e = self.eng
+        e._launch_multi(self._graphs, ("mrs",), n, self._enqueue_multi_rs, capture_error_mode="thread_local")
+        self._after_steps(e._i - n, e._i)
+
+    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
+                     ring_batches: int = 0) -> int:
+        """Host batches → the HBM ring → multi-step graphs with X1-X4 inline (FusedDeepFM.train_stream
+        with this engine's graphs).  The shadow-validation window trains per step first."""
+        if not (self.graph_collectives and self.use_graph):
+            raise RuntimeError("train_stream needs capturable exchanges (p2p, or RCCL with graphs)")
+        from .dp import shadow_prefix
+
+        batches, done = shadow_prefix(self, batches, after_steps)
+        if self.NH and self.hot_ids is None:  # replicated ids from the stream's first group
+            first = next(iter(batches), None)
+            if first is None:
+                return done
+            ids = first[0] if first[0].dim() == 3 else first[0].unsqueeze(0)
+            self._choose_hot(ids[: min(len(ids), 8)].to(self.device))
+            import itertools
+
+            batches = itertools.chain([first], batches)
+        n = self.eng.train_stream(batches, steps_per_graph, after_steps, hold, ring_batches,
+                                  build=self._stream_build, run=self._stream_run)
+        self._pre_served = False
+        return done + n
+
     def train_on(self, batches):
         it = iter(batches)
         cur = next(it, None)
@@ -1168,9 +1296,10 @@ class FusedRowShard:
                 break
             nxt = next(it, None)
 
-    def check(self) -> None:
+    def check(self, replicas: bool = True) -> None:
         """Raise if any owner's request list overflowed the exchange capacity (or a request was
-        routed to the wrong owner) since construction."""
+        routed to the wrong owner) since construction, or (``replicas``; collective) if the
+        replicated state differs across ranks."""
         self.eng.check()
         ov, bad = int(self.overflow.item()), int(self.bad.item())
         if ov:
@@ -1181,6 +1310,8 @@ class FusedRowShard:
             raise RuntimeError("row-shard routing error: a rank received ids it does not own")
         if self.exchange == "p2p" and any(x.errored() for x in self.x_all):
             raise RuntimeError("row-shard p2p exchange: a peer wait timed out (rank missing or stalled)")
+        if replicas and not self.verify_replicas():
+            raise RuntimeError("row-shard replicas diverged: MLP / replicated rows differ across ranks")
 
     # ---- inference (collective) ------------------------------------------------------------------
     @torch.no_grad()

@@ -174,3 +174,13 @@ def test_fused_only_options_fail_loudly_on_the_torch_engine(data_dir, tmp_path):
                {"parallelism": "rowshard", "ps_staleness": 1}):
         with pytest.raises(ValueError):
             Estimator(_cfg(data_dir, str(tmp_path / "m"), **kw))
+
+
+def test_remaining_steps_is_a_global_target():
+    """max_steps counts global steps in both file and pipe mode: a restarted job that restored a
+    checkpoint trains only up to it (and not at all once it is reached)."""
+    from rocfm.cli import _remaining_steps
+
+    assert _remaining_steps(0, 40) is None
+    assert _remaining_steps(100, 40) == 60
+    assert _remaining_steps(100, 100) == 0 and _remaining_steps(100, 130) == 0

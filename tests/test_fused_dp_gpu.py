@@ -18,13 +18,26 @@ def _free_port():
     return port
 
 
-def _cfg():
+_LR = {"Adam": 1e-3, "Momentum": 0.02, "GD": 0.05}
+
+
+def _cfg(opt="Momentum"):
+    """Momentum by default: a linear optimizer, so DP ≡ single differs only by fp32 summation order
+    and the comparison is element-tight (``_assert_tight``); Adam turns last-bit differences on
+    ≈0-gradient rows into lr-sized steps and keeps one loose smoke case."""
     from rocfm.models.deepfm import ModelSpec
     from rocfm.optim import OptHParams
 
     spec = ModelSpec(feature_size=4000, field_size=39, embedding_size=10, layers=[64, 32], keep_probs=[1.0, 1.0],
                      l2_reg=1e-3)
-    return spec, OptHParams(name="Adam", lr=1e-3)
+    return spec, OptHParams(name=opt, lr=_LR[opt])
+
+
+def _assert_tight(got, exp, rtol=1e-5, atol=1e-7):
+    d = (got.float().cpu() - exp.float().cpu()).abs()
+    lim = atol + rtol * exp.float().cpu().abs()
+    bad = d > lim
+    assert not bad.any(), (int(bad.sum()), d.max().item(), (d - lim).max().item())
 
 
 def _batches(B, n, seed):
@@ -35,15 +48,19 @@ def _batches(B, n, seed):
     return [gen.batch(B, "cpu", g) for _ in range(n)]
 
 
-def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, update=None, push="1"):
+def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, update=None, push="1",
+            opt="Momentum", shadow=0, fault=""):
+    # shadow: validated (collective-shadowed) first steps, 0 = off (the equivalence tests keep
+    # their multi-step graph coverage); fault: ROCFM_FAULT of the validation tests
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH=push)
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH=push, ROCFM_SHADOW_STEPS=str(shadow),
+                      ROCFM_FAULT=fault)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from rocfm.models.deepfm import init_params
     from rocfm.parallel.dp import FusedDataParallel
 
-    spec, hp = _cfg()
+    spec, hp = _cfg(opt)
     B = 64
     update = update or ("exact" if mode == "dense_dp" else "sparse")
     eng = FusedDataParallel(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3),
@@ -64,9 +81,17 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
         for _ in range(steps):
             eng.train_step()
     torch.cuda.synchronize()
-    eng.check()
+    eng.check(replicas=False)
+    consistent = eng.verify_replicas()
+    diverged = False
+    try:
+        eng.check()
+    except RuntimeError as exc:
+        diverged = "replicas diverged" in str(exc)
     if rank == 0:
-        torch.save({"emb": eng.emb.cpu(), "dense": eng.dense.cpu()}, out_path)
+        torch.save({"emb": eng.emb.cpu(), "dense": eng.dense.cpu(), "slots": [x.cpu() for x in eng.emb_slots],
+                    "shadow": eng.shadow.status, "exchange": eng.exchange, "consistent": consistent,
+                    "diverged": diverged}, out_path)
     eng.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -95,17 +120,50 @@ def test_fused_dp_p2p_unfused_push(tmp_path, world, spg):
     _check_dp_vs_single(tmp_path, world, "dp", "p2p", 11 if spg else 3, spg, "sparse", push="0")
 
 
-def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, push="1"):
+def test_fused_dp_adam_smoke(tmp_path):
+    """Adam through the p2p exchange and multi-step graphs: the loose comparison."""
+    _check_dp_vs_single(tmp_path, 2, "dp", "p2p", 11, 4, "sparse", opt="Adam")
+
+
+@pytest.mark.parametrize("world,push", [(2, "1"), (4, "0")])
+def test_dp_shadow_exchange_validates_p2p(tmp_path, world, push):
+    """Self-validation: the first 8 steps shadow the p2p all-gather with the collective and compare
+    bitwise (status ok, p2p kept), then multi-step graphs; replica digests agree and the result is
+    the single-GPU one."""
+    dp = _check_dp_vs_single(tmp_path, world, "dp", "p2p", 13, 4, "sparse", push=push, shadow=8)
+    assert dp["shadow"] == "ok" and dp["exchange"] == "p2p" and dp["consistent"] and not dp["diverged"], dp
+
+
+def test_dp_shadow_exchange_catches_corrupt_push(tmp_path):
+    """ROCFM_FAULT=corrupt_push:1: rank 1 sees one flipped word per p2p exchange; the shadow
+    detects it, every rank falls back to RCCL (agreed), the validated steps consumed the
+    collective's data, so the replicas agree and the result is still the single-GPU one."""
+    dp = _check_dp_vs_single(tmp_path, 2, "dp", "p2p", 13, 4, "sparse", shadow=8, fault="corrupt_push:1")
+    assert dp["shadow"] == "mismatch" and dp["exchange"] == "rccl" and dp["consistent"], dp
+
+
+def test_dp_replica_check_catches_divergence(tmp_path):
+    """ROCFM_FAULT=corrupt_replica:1: one rank's MLP drifts; the collective digest check fails on
+    every rank (check() raises)."""
+    dp = _check_dp_vs_single(tmp_path, 2, "dp", "p2p", 3, 0, "sparse", fault="corrupt_replica:1", compare=False)
+    assert not dp["consistent"] and dp["diverged"], dp
+
+
+def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, push="1", opt="Momentum", shadow=0,
+                        fault="", compare=True):
     # ranks share this GPU, where the fused push is off by default: the workers force it (small
     # batches keep the spinning producers from starving a peer) unless the copy push is asked for
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_worker, args=(world, _free_port(), mode, out, exchange, steps, spg, update, push), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out, exchange, steps, spg, update, push, opt, shadow,
+                                      fault), nprocs=world, join=True, start_method="spawn")
     dp = torch.load(out, weights_only=True)
+    if not compare:
+        return dp
+    assert dp["consistent"] and not dp["diverged"], dp
     from rocfm.models.deepfm import init_params
     from rocfm.models.fused import FusedDeepFM
 
-    spec, hp = _cfg()
+    spec, hp = _cfg(opt)
     single = FusedDeepFM(spec, hp, 64 * world, torch.device("cuda"), params=init_params(spec, 3), use_graph=False,
                          embedding_update=update)
     batches = _batches(64 * world, steps, 11)
@@ -114,12 +172,18 @@ def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, pus
     for _ in range(steps):
         single.train_step()
     torch.cuda.synchronize()
-    # rank-partial sums reorder fp32 additions; Adam amplifies that for near-zero gradients
-    # (m/√v), so the tolerance grows with the number of steps (a missed or stale row would be off
-    # by a whole step, ≈lr = 1e-3)
-    atol = 2e-5 if steps <= 3 else 1e-4
-    torch.testing.assert_close(dp["dense"], single.dense.cpu(), rtol=2e-3, atol=atol)
-    torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=atol)
+    if opt != "Momentum":
+        # rank-partial sums reorder fp32 additions; Adam amplifies that for near-zero gradients
+        # (m/√v), so the tolerance grows with the number of steps
+        atol = 2e-5 if steps <= 3 else 1e-4
+        torch.testing.assert_close(dp["dense"], single.dense.cpu(), rtol=2e-3, atol=atol)
+        torch.testing.assert_close(dp["emb"], single.emb.cpu(), rtol=2e-3, atol=atol)
+        return dp
+    _assert_tight(dp["dense"], single.dense)
+    _assert_tight(dp["emb"], single.emb)
+    for got, exp in zip(dp["slots"], single.emb_slots):  # the momentum accumulators too
+        _assert_tight(got, exp)
+    return dp
 
 
 @pytest.mark.parametrize("update", ["sparse", "exact"])
@@ -154,8 +218,74 @@ def test_dp_multistep_graphs_world1_equal_single(mode, upd, merge, monkeypatch):
     torch.cuda.synchronize()
     assert dp.global_step() == one.global_step() == 21
     # same math; only fma contraction differs between the merge and the single-GPU update
-    torch.testing.assert_close(dp.emb, one.emb, rtol=2e-3, atol=2e-5)
-    torch.testing.assert_close(dp.dense, one.dense, rtol=2e-3, atol=2e-5)
+    _assert_tight(dp.emb, one.emb)
+    _assert_tight(dp.dense, one.dense)
     dp.check()
     if mode == "dp":
         assert dp.maps.hashed == (merge == "hash")
+
+
+def _stream_worker(rank, world, port, kind, out_path, shadow):
+    """Streamed (host groups → HBM ring → multi-step graphs, exchange inline) vs pool-fed
+    training of the same batches, both through the p2p exchange, with a shadow-validation window
+    that ends inside the first group."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH="1", ROCFM_SHADOW_STEPS=str(shadow))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from rocfm.models.deepfm import init_params
+
+    spec, hp = _cfg("Adam")
+    B, n, S = 64, 13, 4
+    batches = _batches(world * B, n, 11)
+    mine = [(b[0][rank * B:(rank + 1) * B], b[1][rank * B:(rank + 1) * B], b[2][rank * B:(rank + 1) * B])
+            for b in batches]
+
+    def build():
+        if kind == "rowshard":
+            from rocfm.parallel.emb_shard import FusedRowShard
+
+            return FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), use_graph=True,
+                                 exchange="p2p")
+        from rocfm.parallel.dp import FusedDataParallel
+
+        return FusedDataParallel(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), use_graph=True,
+                                 exchange="p2p")
+
+    res = {}
+    a = build()
+    groups = [tuple(torch.stack([m[j] for m in mine[i:i + S]]).pin_memory() for j in range(3))
+              for i in range(0, n, S)]
+    seen = []
+    assert a.train_stream(iter(groups), S, after_steps=lambda s, k: seen.append((s, k)), hold=2) == n
+    torch.cuda.synchronize()
+    a.check()
+    res["stream"] = (a.emb.cpu() if kind != "rowshard" else a.eng.emb.cpu(), a.dense.cpu(), a.global_step(),
+                     a.shadow.status, sum(k for _, k in seen))
+    a.close()
+    b = build()
+    b.attach_pool(*(torch.stack([m[j] for m in mine]).cuda() for j in range(3)))
+    b.train_steps(n, S)
+    torch.cuda.synchronize()
+    b.check()
+    res["pool"] = (b.emb.cpu() if kind != "rowshard" else b.eng.emb.cpu(), b.dense.cpu(), b.global_step(),
+                   b.shadow.status, n)
+    b.close()
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,world", [("dp", 2), ("dp", 4), ("rowshard", 2)])
+def test_streamed_multi_gpu_equals_pool_fed(tmp_path, kind, world):
+    """Multi-GPU loader path: DP / row-shard train_stream (what the Estimator runs at world > 1)
+    ≡ the pool-fed multi-step path, bitwise (Adam), with the shadow window (3 steps) split off the
+    first group."""
+    out = str(tmp_path / "st.pt")
+    mp.start_processes(_stream_worker, args=(world, _free_port(), kind, out, 3), nprocs=world, join=True,
+                       start_method="spawn")
+    r = torch.load(out, weights_only=True)
+    (ea, da, sa, sha, na), (eb, db, sb, shb, nb) = r["stream"], r["pool"]
+    assert sa == sb == 13 and na == 13 and sha == shb == "ok", (sa, sb, na, sha, shb)
+    assert torch.equal(ea, eb) and torch.equal(da, db)

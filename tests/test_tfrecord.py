@@ -253,3 +253,48 @@ def test_libsvm_cli_sharded(tmp_path):
         assert vals == [(f + 1) * 0.5 for f in range(5)]
     sizes = [len(T.decode_file(p, 5)[0]) for p in paths]
     assert sizes == [25, 26, 26, 26]
+
+
+def test_decoded_cache_epochs_equal_loader(tmp_path):
+    """rocfm.data.cache: the first pass is written through, later passes (and a later job) read
+    the raw memory-mapped cache; over several epochs with skip / limit the batches equal the C++
+    loader's multi-epoch stream exactly, and an interrupted first pass leaves no complete cache."""
+    import torch
+
+    from rocfm.data.cache import DecodedCache, cached_epochs
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.data.tfrecord import TFRecordDataset
+
+    files = []
+    for i in range(2):
+        p = str(tmp_path / f"tr{i}.tfrecords")
+        write_synthetic_tfrecord(p, 1500, 5000, 39, seed=i)
+        files.append(p)
+    B, S, E = 128, 4, 3
+
+    def ds(epochs):
+        return TFRecordDataset(files, 39, B, 5000, num_epochs=epochs, shard_count=2, shard_index=1, num_threads=2,
+                               pin_memory=False)
+
+    def flat(groups):
+        out = []
+        for g in groups:
+            if g[0].dim() == 2:
+                g = tuple(t.unsqueeze(0) for t in g)
+            out += [tuple(t[i].clone() for t in g) for i in range(g[0].shape[0])]
+        return out
+
+    ref = flat(ds(E).groups(S, hold=2))
+    nb = len(ref) // E
+    d = str(tmp_path / "cache")
+    first = lambda sk, lim: ds(1).groups(S, hold=2, skip=sk, limit=lim)
+    # an interrupted first pass (limit inside epoch 1) leaves no complete cache
+    part = flat(cached_epochs(DecodedCache.for_dataset(ds(1), d), first, E, S, limit=nb - 2))
+    assert len(part) == nb - 2 and not DecodedCache.for_dataset(ds(1), d).complete()
+    for skip, limit in ((0, None), (0, None), (nb + 3, 2 * nb - 5)):  # write-through, then from the cache
+        dc = DecodedCache.for_dataset(ds(1), d)
+        got = flat(cached_epochs(dc, first, E, S, skip=skip, limit=limit))
+        exp = ref[skip:] if limit is None else ref[skip:skip + limit]
+        assert len(got) == len(exp)
+        assert all(all(torch.equal(a, b) for a, b in zip(x, y)) for x, y in zip(got, exp))
+        assert dc.complete() and dc.num_batches() == nb

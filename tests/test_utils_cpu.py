@@ -113,3 +113,22 @@ def test_rank_info_from_env(monkeypatch):
     assert r.num_hosts == 2 and r.host_index == 1
     r = rank_info_from_env(worker_per_host=2)
     assert r.local_world == 2
+
+
+def test_pyproject_packages_exist():
+    """pyproject.toml installs `rocfm` from the hyphenated source directory (no symlink needed):
+    every listed package maps to a directory with an __init__.py."""
+    import os
+
+    import tomli
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = tomli.load(open(os.path.join(root, "pyproject.toml"), "rb"))["tool"]["setuptools"]
+    src = os.path.join(root, cfg["package-dir"]["rocfm"])
+    assert os.path.isdir(src) and not os.path.islink(src)
+    for pkg in cfg["packages"]:
+        d = os.path.join(src, *pkg.split(".")[1:])
+        assert os.path.isfile(os.path.join(d, "__init__.py")), pkg
+    on_disk = {os.path.relpath(r, src) for r, _, fs in os.walk(src) if "__init__.py" in fs and "__pycache__" not in r}
+    listed = {os.path.join(*p.split(".")[1:]) if "." in p else "." for p in cfg["packages"]}
+    assert on_disk == listed, (on_disk, listed)
