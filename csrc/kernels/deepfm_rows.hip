@@ -234,7 +234,7 @@ constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
 // discarded (no global store touches them), so the arithmetic of every valid row is unchanged.
 template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
-  static_assert(RT == 16 || RT == 8, "rows per workgroup: 16 or 8");
+  static_assert(RT == 16 || RT == 8 || RT == 4, "rows per workgroup: 16, 8 or 4");
   static_assert(RT == 16 || SH::kStatic, "8-row workgroups: compile-time shapes only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
@@ -466,13 +466,21 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if (train && !(ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
-    for (int it = t; it < D0p * (RT / 8); it += kRowThreads) {
-      const int c = RT == 8 ? it : it >> 1, h = RT == 8 ? 0 : it & 1;
-      uint32_t w[4];
+    if constexpr (RT >= 8) {
+      for (int it = t; it < D0p * (RT / 8); it += kRowThreads) {
+        const int c = RT == 8 ? it : it >> 1, h = RT == 8 ? 0 : it & 1;
+        uint32_t w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w[j] = (uint32_t)h0[(h * 8 + 2 * j) * lda + c] | ((uint32_t)h0[(h * 8 + 2 * j + 1) * lda + c] << 16);
-      *reinterpret_cast<uint4*>(p.actT[0] + (size_t)c * Bp + row0 + h * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int j = 0; j < 4; ++j)
+          w[j] = (uint32_t)h0[(h * 8 + 2 * j) * lda + c] | ((uint32_t)h0[(h * 8 + 2 * j + 1) * lda + c] << 16);
+        *reinterpret_cast<uint4*>(p.actT[0] + (size_t)c * Bp + row0 + h * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    } else {  // 4 rows × 1 column per item → one 8-B store
+      for (int c = t; c < D0p; c += kRowThreads) {
+        const uint32_t w0 = (uint32_t)h0[c] | ((uint32_t)h0[lda + c] << 16);
+        const uint32_t w1 = (uint32_t)h0[2 * lda + c] | ((uint32_t)h0[3 * lda + c] << 16);
+        *reinterpret_cast<uint2*>(p.actT[0] + (size_t)c * Bp + row0) = make_uint2(w0, w1);
+      }
     }
   }
 
@@ -1157,18 +1165,25 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   launch_rows_impl<KP4, SH, false, kDynamic, true, BT>(p, stream);
 }
 
-// rows per workgroup (RowsParams::row_tile): 8 doubles the workgroups of a batch (128 instead of
-// 64 at B = 1024 on 256 CUs) at the same per-workgroup weight-fragment traffic; static shapes only
+// rows per workgroup (RowsParams::row_tile, 0 = kDefaultRowTile): 8 doubles the workgroups of a
+// batch (128 instead of 64 at B = 1024 on 256 CUs) at the same per-workgroup weight-fragment
+// traffic — measured 35.9 → 33.3 µs per step in 20-step windows, 33.4 → 32.2 over 200 steps
+// (profiles/r3_row_tile.md); static shapes only (the runtime-shape kernel keeps 16)
+constexpr int kDefaultRowTile = 8;
 template <int KP4, class SH>
 static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
-  const bool rt8 = SH::kStatic && p.row_tile == 8;
+  const int rt = SH::kStatic ? (p.row_tile ? p.row_tile : kDefaultRowTile) : 16;
   if (p.tbl_bf16) {
-    if (rt8)
+    if (rt == 4)
+      launch_rows_t<KP4, SH, true, 4>(p, stream);
+    else if (rt == 8)
       launch_rows_t<KP4, SH, true, 8>(p, stream);
     else
       launch_rows_t<KP4, SH, true, 16>(p, stream);
   } else {
-    if (rt8)
+    if (rt == 4)
+      launch_rows_t<KP4, SH, false, 4>(p, stream);
+    else if (rt == 8)
       launch_rows_t<KP4, SH, false, 8>(p, stream);
     else
       launch_rows_t<KP4, SH, false, 16>(p, stream);
@@ -1199,7 +1214,8 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Bp % kRowTile == 0 && p.Bp >= p.B, "deepfm_rows: Bp must be a multiple of 16 and >= B");
   ROCFM_REQUIRE((p.Bp % 64) == 0 || !p.train, "deepfm_rows: training needs Bp % 64 == 0");
   p.magicF = (uint32_t)((1ull << 32) / (uint64_t)p.F + 1ull);
-  ROCFM_REQUIRE(p.row_tile == 0 || p.row_tile == 8 || p.row_tile == 16, "deepfm_rows: row_tile must be 0, 8 or 16");
+  ROCFM_REQUIRE(p.row_tile == 0 || p.row_tile == 4 || p.row_tile == 8 || p.row_tile == 16,
+                "deepfm_rows: row_tile must be 0, 4, 8 or 16");
   p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
   if (p.Bp / kRowTile == 0) return;
