@@ -89,4 +89,28 @@ struct SortAuxParams {
 };
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream);
 
+// Per-tile dedup of the sorted lookups (the row kernel pre-reduces duplicate ids inside each of its
+// workgroups' row tiles).  In a batch's sorted order the lookups of one id are ascending in position,
+// so those of one (id, row tile) pair — a "group" — are contiguous.  Every lookup gets its group's
+// index in the compacted (one entry per group) sorted list: pos[lookup] = c for the group's first
+// lookup, ~c for the others, and nxt[lookup] = the next lookup of its group (in-batch index, -1 at
+// the end); the compacted keys, their count and the embedding update's per-chunk run ends / run
+// heads are rebuilt over the compacted list.  Deterministic (no atomics).
+struct DedupParams {
+  const uint32_t* skeys;  // [S·n] sorted keys (per-batch segments; equal key ⇔ equal id in a segment)
+  const uint32_t* svals;  // [S·n] lookup index: batch_base + b·F + f, batch_base = k·n (val_base_step = n)
+  int n, S, F, rt;        // lookups per batch, batches, fields, examples per row-kernel workgroup
+  int val_base_step;      // n for multi-batch sorts (global indices), 0 for one batch's local indices
+  int32_t* pos;           // [S·n] by lookup index
+  int32_t* nxt;           // [S·n] by lookup index
+  uint32_t* ckeys;        // [S·n] compacted keys (segment k at k·n)
+  int32_t* count;         // [S] compacted entries per batch
+  int32_t* bcount;        // scratch [S][ceil(n / 1024)]
+  int chunk;              // entries per embedding-update workgroup
+  int32_t* chunk_end;     // [S][ceil(n / chunk)] (nullable) end of each chunk's last run (compacted)
+  int32_t* chunk_heads;   // [S][ceil(n / chunk)] (nullable) run heads per compacted chunk
+};
+void launch_dedup(const DedupParams& p, hipStream_t stream);
+int dedup_scratch_ints(int n, int S);
+
 }  // namespace rocfm

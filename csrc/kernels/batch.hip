@@ -175,6 +175,121 @@ void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
   }
 }
 
+// ---- per-tile dedup (DedupParams) ----------------------------------------------------------------
+constexpr int kDedupBlock = 1024;
+
+// Group head: first entry of its batch segment, or its id or row tile differs from the previous
+// entry's.  (Entries of one id are ascending in lookup index, so tiles are non-decreasing.)
+__device__ __forceinline__ bool dedup_head(const DedupParams& p, int k, int j) {
+  if (j == 0) return true;
+  const size_t o = (size_t)k * p.n;
+  if (p.skeys[o + j] != p.skeys[o + j - 1]) return true;
+  const int vb = k * p.val_base_step;
+  const int ta = ((int)p.svals[o + j] - vb) / p.F / p.rt, tb = ((int)p.svals[o + j - 1] - vb) / p.F / p.rt;
+  return ta != tb;
+}
+
+__global__ __launch_bounds__(kDedupBlock) void dedup_count_kernel(const DedupParams p, int nblk) {
+  __shared__ int s_w[kDedupBlock / 64];
+  const int k = blockIdx.y, blk = blockIdx.x, t = threadIdx.x;
+  const int j = blk * kDedupBlock + t;
+  const bool h = j < p.n && dedup_head(p, k, j);
+  const unsigned long long m = __ballot(h);
+  if ((t & 63) == 0) s_w[t >> 6] = __popcll(m);
+  __syncthreads();
+  if (t == 0) {
+    int c = 0;
+    for (int w = 0; w < kDedupBlock / 64; ++w) c += s_w[w];
+    p.bcount[(size_t)k * nblk + blk] = c;
+  }
+}
+
+__global__ __launch_bounds__(kDedupBlock) void dedup_write_kernel(const DedupParams p, int nblk) {
+  __shared__ int s_w[kDedupBlock / 64];
+  __shared__ int s_base;
+  const int k = blockIdx.y, blk = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t < 64) {  // heads before this block: Σ of the earlier blocks' counts (fixed order)
+    int b = 0;
+    for (int q = lane; q < blk; q += 64) b += p.bcount[(size_t)k * nblk + q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (t == 0) s_base = b;
+  }
+  const int j = blk * kDedupBlock + t;
+  const bool in = j < p.n;
+  const bool h = in && dedup_head(p, k, j);
+  const unsigned long long m = __ballot(h);
+  if (lane == 0) s_w[wave] = __popcll(m);
+  __syncthreads();
+  int before = s_base;
+  for (int w = 0; w < wave; ++w) before += s_w[w];
+  before += __popcll(m & ((1ull << lane) - 1ull));
+  if (!in) return;
+  const int c = before + (h ? 0 : -1);  // this lookup's group in the compacted list
+  const size_t o = (size_t)k * p.n;
+  const int vb = k * p.val_base_step;
+  const int lk = (int)p.svals[o + j] - vb;  // in-batch lookup index
+  p.pos[o + lk] = h ? c : ~c;
+  const bool more = j + 1 < p.n && !dedup_head(p, k, j + 1);
+  p.nxt[o + lk] = more ? (int)p.svals[o + j + 1] - vb : -1;
+  if (h) p.ckeys[o + c] = p.skeys[o + j];
+  if (j == p.n - 1) p.count[k] = c + 1;
+}
+
+// One workgroup of `chunk` threads per (batch, compacted chunk): the end of the chunk's last run
+// (binary search) and its run heads.
+__global__ __launch_bounds__(512) void dedup_chunks_kernel(const DedupParams p, int nch) {
+  __shared__ int s_w[8];
+  const int k = blockIdx.y, c = blockIdx.x, t = threadIdx.x;
+  const int cnt = p.count[k];
+  const uint32_t* kb = p.ckeys + (size_t)k * p.n;
+  const int i0 = c * p.chunk;
+  if (p.chunk_heads) {
+    int h = 0;
+    for (int i = i0 + t; i < min(i0 + p.chunk, cnt); i += blockDim.x) h += (i == 0 || kb[i] != kb[i - 1]) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+    if ((t & 63) == 0) s_w[t >> 6] = h;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_w[w];
+      p.chunk_heads[(size_t)k * nch + c] = tot;
+    }
+  }
+  if (p.chunk_end && t == 0) {
+    int end = cnt;
+    if (i0 < cnt) {
+      const int last = min(i0 + p.chunk, cnt) - 1;
+      const uint32_t key = kb[last];
+      int lo = last + 1, hi = cnt;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (kb[mid] == key) lo = mid + 1; else hi = mid;
+      }
+      end = lo;
+    }
+    p.chunk_end[(size_t)k * nch + c] = end;
+  }
+}
+
+int dedup_scratch_ints(int n, int S) { return S * ((n + kDedupBlock - 1) / kDedupBlock); }
+
+void launch_dedup(const DedupParams& p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.n > 0 && p.S > 0 && p.F > 0 && (p.rt == 4 || p.rt == 8 || p.rt == 16), "dedup: bad sizes");
+  ROCFM_REQUIRE(p.skeys && p.svals && p.pos && p.nxt && p.ckeys && p.count && p.bcount, "dedup: buffers missing");
+  ROCFM_REQUIRE(p.chunk > 0 && p.chunk <= 512 && (p.chunk_end || p.chunk_heads || true), "dedup: chunk");
+  const int nblk = (p.n + kDedupBlock - 1) / kDedupBlock;
+  hipLaunchKernelGGL(dedup_count_kernel, dim3(nblk, p.S), dim3(kDedupBlock), 0, stream, p, nblk);
+  hipLaunchKernelGGL(dedup_write_kernel, dim3(nblk, p.S), dim3(kDedupBlock), 0, stream, p, nblk);
+  if (p.chunk_end || p.chunk_heads) {
+    const int nch = (p.n + p.chunk - 1) / p.chunk;
+    hipLaunchKernelGGL(dedup_chunks_kernel, dim3(nch, p.S), dim3(std::min(512, (p.chunk + 63) / 64 * 64)), 0, stream,
+                       p, nch);
+  }
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.pool_batches > 0 && p.S > 0, "fetch_multi: empty pool / S");
   ROCFM_REQUIRE(p.cur_dst != p.cur_src && p.step_dst != p.step_src, "fetch_multi: counters must differ");

@@ -12,6 +12,7 @@ constexpr int kRowThreads = 512;  // 8 waves
 
 struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
   int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32, pos, amax;
+  int nxt, gr;          // dedup: int [16·F] next member of each lookup's group; f32 [16·F][Kp] gradient rows
   int bnr[kMaxHidden];  // batch_norm: f32 [16][dims[l+1]] post-ReLU values r of layer l (kept for backward)
   int bnst[kMaxHidden]; // batch_norm: f32 [2][dims[l+1]] batch mean, 1/sqrt(var + eps) of layer l
   int bndy, bntot;      // batch_norm backward scratch: f32 [16][max dim] dy, [2][max dim] column totals
@@ -77,7 +78,12 @@ struct RowsParams {
   int* bn_error;                      // set if a grid barrier timed out (the host check raises)
   PushTarget push;                    // producer push (push.h): workgroup 0 signals "entered"
   PushTarget push2;                   // a second exchange pushed by this step (row-shard X3)
-  int row_tile;                       // examples per workgroup: 16 (0 = default) or 8 (static shapes)
+  int row_tile;                       // examples per workgroup: 16, 8 or 4 (0 = default; static shapes)
+  // per-tile dedup (batch.h DedupParams): contrib_pos holds each lookup's compacted group index (c
+  // for the group's first lookup, ~c for the others) and contrib_nxt the next lookup of its group;
+  // phase F sums every group's gradient rows in LDS (lookup order) and writes ONE row per group
+  int dedup;
+  const int32_t* contrib_nxt;
 };
 
 struct WgradParams {

@@ -243,6 +243,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
   float* s_vals = reinterpret_cast<float*>(smem + L.vals);
   int32_t* s_pos = reinterpret_cast<int32_t*>(smem + L.pos);
+  int32_t* s_nxt = reinterpret_cast<int32_t*>(smem + L.nxt);  // (dedup only)
   float* s_wx = reinterpret_cast<float*>(smem + L.wx);
   float* s_S = reinterpret_cast<float*>(smem + L.S);
   float* s_ylin = reinterpret_cast<float*>(smem + L.ylin);
@@ -279,11 +280,13 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float* vals_g = p.vals;
     const int32_t* pos_g = p.contrib_pos ? p.contrib_pos : p.ids;  // any valid [B][F] int32 buffer
     const bool has_pos = p.contrib_pos != nullptr;
+    const bool dedup = p.dedup != 0;
+    const int32_t* nxt_g = dedup ? p.contrib_nxt : p.ids;
     const int nvalid = max(0, min(RT, p.B - row0)) * F;  // valid lookups of this tile
     const int last = max(p.B * F - 1, 0);                        // clamp target: a valid lookup
     int32_t idr[kItems];
     float vlr[kItems];
-    int32_t psr[kItems];
+    int32_t psr[kItems], nxr[kItems];
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
@@ -291,6 +294,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       idr[u] = ids_g[gi];
       vlr[u] = vals_g[gi];
       psr[u] = pos_g[gi];
+      nxr[u] = nxt_g[gi];
     }
     float br[SH::nl];
 #pragma unroll
@@ -309,6 +313,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         s_ids[i] = valid ? idr[u] : 0;
         s_vals[i] = valid ? vlr[u] : 0.f;
         s_pos[i] = (valid && has_pos) ? psr[u] : (int32_t)((size_t)row0 * F + i);
+        if (dedup) s_nxt[i] = (valid && nxr[u] >= 0) ? nxr[u] - row0 * F : -1;  // tile-local (same tile)
       }
     }
 #pragma unroll
@@ -326,6 +331,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       s_ids[i] = valid ? p.ids[(size_t)row0 * F + i] : 0;
       s_vals[i] = valid ? p.vals[(size_t)row0 * F + i] : 0.f;
       s_pos[i] = (valid && p.contrib_pos) ? p.contrib_pos[(size_t)row0 * F + i] : (int32_t)((size_t)row0 * F + i);
+      if (p.dedup) {
+        const int nx = valid ? p.contrib_nxt[(size_t)row0 * F + i] : -1;
+        s_nxt[i] = nx >= 0 ? nx - row0 * F : -1;
+      }
     }
 #pragma unroll
     for (int l = 0; l < NL; ++l)
@@ -1019,9 +1028,39 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
       dst[u] = s_pos[rf] * KP4 + c4;
     }
+    if (p.dedup) {  // the tile's rows stay in LDS: summed per group below
+      if (L.gr == L.f32) lds_barrier();  // (over dh0: every thread's reads of it are done)
+      float4* s_gr = reinterpret_cast<float4*>(smem + L.gr);
 #pragma unroll
-    for (int u = 0; u < UF; ++u)
-      if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
+      for (int u = 0; u < UF; ++u) {
+        const int idx0 = base + u * kRowThreads + t;
+        if (ok[u]) s_gr[idx0] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UF; ++u)
+        if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
+    }
+  }
+  if (p.dedup) {
+    // per-tile dedup: each group (equal id within this row tile) sums its lookups' rows in lookup
+    // order — head first, then along the nxt chain — and stores ONE row at its compacted index
+    lds_barrier();
+    const float4* s_gr = reinterpret_cast<const float4*>(smem + L.gr);
+    for (int idx = t; idx < nitemsF; idx += kRowThreads) {
+      const int rf = idx / KP4, c4 = idx - rf * KP4;
+      const int c = s_pos[rf];
+      if (c < 0 || row0 + fdiv(rf, magicF) >= p.B) continue;  // not a group head / padding row
+      float4 acc = s_gr[idx];
+      for (int j = s_nxt[rf]; j >= 0; j = s_nxt[j]) {
+        const float4 v = s_gr[j * KP4 + c4];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      reinterpret_cast<float4*>(p.contrib)[(size_t)c * KP4 + c4] = acc;
+    }
   }
   lds_barrier();
   ROWS_STAMP(12);
@@ -1045,7 +1084,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 // ------------------------------------------------------------------------------------------------
 static int align16(int x) { return (x + 15) & ~15; }
 
-RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn, int dedup_kp, int rt, bool gr_alias) {
   RowsLds L{};
   int off = 0;
   auto take = [&](int bytes) {
@@ -1076,6 +1115,13 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn) {
     L.dzB = take(kRowTile * L.ldz * 2);
   }
   L.f32 = take(kRowTile * dims[0] * 4);
+  if (dedup_kp > 0) {
+    L.nxt = take(kRowTile * F * 4);
+    // the tile's gradient rows: over the f32 scratch (dh0, dead once phase F has read it — the
+    // compile-time-shape kernels read all of it before the first row is stored), else their own
+    const int gb = rt * F * dedup_kp * 4;
+    L.gr = (gr_alias && gb <= kRowTile * dims[0] * 4) ? L.f32 : take(gb);
+  }
   if (bn) {
     for (int l = 0; l < nl; ++l) {
       L.bnr[l] = take(kRowTile * dims[l + 1] * 4);
@@ -1193,16 +1239,39 @@ static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
 // Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
 // the runtime-shape kernel.
 template <int F, int K, int D1, int D2, int D3>
-static bool try_static(const RowsParams& p, hipStream_t stream) {
+static bool static_match(const RowsParams& p) {
   const int nl = D3 ? 3 : (D2 ? 2 : 1);
   if (p.F != F || p.K != K || p.nl != nl || p.dims[1] != D1 || (nl >= 2 && p.dims[2] != D2) ||
       (nl >= 3 && p.dims[3] != D3))
     return false;
   for (int l = 0; l < nl; ++l)
     if (!p.WTs[l] || !p.Wbs[l]) return false;  // the static kernels load the frag_swz weight copies
+  return true;
+}
+
+template <int F, int K, int D1, int D2, int D3>
+static bool try_static(const RowsParams& p, hipStream_t stream) {
+  if (!static_match<F, K, D1, D2, D3>(p)) return false;
   constexpr int KP4 = (K + 1 + 3) / 4;
   launch_rows_tb<KP4, CtShape<F, K, D1, D2, D3>>(p, stream);
   return true;
+}
+
+static bool is_static(const RowsParams& p) {
+  return !p.force_generic && !p.bn &&
+         (static_match<39, 10, 128, 64, 32>(p) || static_match<39, 8, 128, 64, 32>(p) ||
+          static_match<39, 12, 128, 64, 32>(p) || static_match<39, 10, 64, 32, 0>(p) ||
+          static_match<39, 32, 128, 64, 32>(p));
+}
+
+// Examples per workgroup the launcher will use for these parameters (the per-tile dedup of the side
+// chain must cut the same tiles).
+int deepfm_rows_tile(const RowsParams& p) {
+  return is_static(p) ? (p.row_tile ? p.row_tile : kDefaultRowTile) : kRowTile;
+}
+
+RowsLds rows_lds_layout_for(const RowsParams& p) {
+  return rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn, p.dedup ? p.Kp : 0, deepfm_rows_tile(p), is_static(p));
 }
 
 void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
@@ -1216,7 +1285,8 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   p.magicF = (uint32_t)((1ull << 32) / (uint64_t)p.F + 1ull);
   ROCFM_REQUIRE(p.row_tile == 0 || p.row_tile == 4 || p.row_tile == 8 || p.row_tile == 16,
                 "deepfm_rows: row_tile must be 0, 4, 8 or 16");
-  p.lds = rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn);
+  ROCFM_REQUIRE(!p.dedup || (p.contrib_pos && p.contrib_nxt && !p.bn), "deepfm_rows: dedup needs contrib_pos / _nxt");
+  p.lds = rows_lds_layout_for(p);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
   if (p.Bp / kRowTile == 0) return;
   if (p.bn && p.train) {

@@ -1,5 +1,5 @@
 // Device body of the embedding-row update (emb_update.hip; also fused into step_tail.hip).
-// See emb_update.hip for the algorithm.  kChunk sorted entries per workgroup of kChunk threads.
+// See emb_update.hip for the algorithm.  kE ≤ kChunk sorted entries per workgroup of kChunk threads.
 #pragma once
 #include "emb_update.h"
 
@@ -41,7 +41,11 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
 // continuation chunks; then one 16-lane group per run applies the optimizer to the table row.
 // PUSH: the fused DP push variant (mode 2 with p.push set); a compile-time switch so the other
 // launches keep their memory-op stream (and waitcnt placement) free of the push's branches.
-template <int KP4, int kChunk, bool BT = false, bool PUSH = false>
+// kE < kChunk (the fused tail: 256 entries on 512 threads): twice the workgroups for the same
+// entries, so a chunk's run heads — its optimizer items, the scattered table / slot round trip
+// that bounds the slowest chunks — are spread over twice the CUs; the threads past kE load no
+// entry but take part in the end search, the continuation rounds and the optimizer items.
+template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
   __shared__ float4 s_rows[kChunk * KP4];
@@ -52,9 +56,13 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   __shared__ int s_nh, s_last_end, s_out_base;
   __shared__ int s_hb[2 * kWaves];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int c0 = bid * kChunk;
-  const int cend = min(c0 + kChunk, p.n);
+  static_assert(kE <= kChunk && kE % 64 == 0, "entries per chunk");
+  const int n = p.n_dev ? *p.n_dev : p.n;  // (dedup: the compacted list's length, ≤ p.n)
+  const int c0 = bid * kE;
+  if (c0 >= n) return;  // grid sized for p.n
+  const int cend = min(c0 + kE, n);
   const int i = c0 + t;
+  const bool live = t < kE && i < n;  // this thread holds one of the chunk's entries
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
   // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
@@ -77,7 +85,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   uint32_t key = 0xffffffffu;
   bool head = false;
   float4 v[KP4];
-  if (i < p.n) {
+  if (live) {
     key = p.skeys[i];
     head = (i == 0) || (p.skeys[i - 1] != key);
     const bool skip = p.max_key && key >= p.max_key;
@@ -91,7 +99,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   }
   // 2. wave-level segmented inclusive scan (segments: runs, cut at wave boundaries)
   {
-    const unsigned long long hm = __ballot(head || lane == 0 || i >= p.n);
+    const unsigned long long hm = __ballot(head || lane == 0 || !live);
     const unsigned long long below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const int seg = 63 - __clzll(hm & below);
 #pragma unroll
@@ -150,16 +158,16 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   {
     const uint32_t lk = s_hkey[nh - 1];
     const bool sentinel = p.max_key && lk >= p.max_key;  // sentinel padding sorts last: runs to n
-    int pos = sentinel ? p.n : cend;
-    if (t == 0) s_last_end = p.n;
+    int pos = sentinel ? n : cend;
+    if (t == 0) s_last_end = n;
     if (p.chunk_end != nullptr && !sentinel) {  // precomputed by the side chain (sort_aux)
-      pos = p.n;
+      pos = n;
       if (t == 0) s_last_end = ce_pre;
     }
     __syncthreads();
-    while (pos < p.n) {
+    while (pos < n) {
       const int j = pos + t;
-      const bool diff = (j >= p.n) || (p.skeys[j] != lk);
+      const bool diff = (j >= n) || (p.skeys[j] != lk);
       const unsigned long long dm = __ballot(diff);
       if (lane == 0) s_wcnt[wave] = dm ? (__ffsll((long long)dm) - 1) : 64;
       __syncthreads();
@@ -171,7 +179,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         }
       __syncthreads();
       if (found >= 0) {
-        if (t == 0) s_last_end = min(found, p.n);
+        if (t == 0) s_last_end = min(found, n);
         break;
       }
       pos += kChunk;

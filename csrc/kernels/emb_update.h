@@ -58,6 +58,9 @@ struct EmbUpdateParams {
   // (rocfm.parallel.validate) all-to-alls that local copy through RCCL and compares it bitwise
   // with what the producers pushed into the owners' slots
   int push_mirror;
+  // nullable: the entry count is this device word (per-tile dedup: the compacted list's length,
+  // written by the side chain); n is then the maximum and sizes the grid
+  const int32_t* n_dev;
 };
 
 struct EmbDenseParams {

@@ -43,6 +43,9 @@ void launch_emb_rows_update(EmbUpdateParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp <= 64 && p.K1 <= p.Kp, "emb_update: Kp must be a multiple of 4 and <= 64");
   if (p.id_stride <= 0) p.id_stride = 1;
   if (p.n <= 0) return;
+  // the side chain's precomputed run ends are cut at the FUSED tail's chunk (step_tail.hip); this
+  // launch's workgroups take kEmbChunk entries and find their last run's end themselves
+  p.chunk_end = nullptr;
   switch (p.Kp / 4) {
 #define ROCFM_KP4(N) \
   case N:            \

@@ -5,32 +5,55 @@
 // (≈70 wgrad + ⌈B·F/512⌉ embedding workgroups, all co-resident on 256 CUs).  This replaces two
 // serial launches (≈10 + 15 µs) or a second stream (whose fork/join inside a HIP graph costs more
 // than it overlaps) with ≈max of the two.
+#include "../ops.h"
 #include "emb_body.h"
 #include "wgrad_body.h"
+
+#include <cstdlib>
 
 namespace rocfm {
 
 constexpr int kTailThreads = 512;
+
+// Sorted entries per embedding workgroup of the tail (ROCFM_TAIL_CHUNK = 256 | 512).  The side
+// chain's per-chunk run ends / run-head counts are cut at the same size (tail_chunk binding).
+int tail_chunk_entries() {
+  static const int n = [] {
+    const char* v = std::getenv("ROCFM_TAIL_CHUNK");
+    const int x = v ? std::atoi(v) : kTailChunkDefault;
+    return (x == 256 || x == 512) ? x : kTailChunkDefault;
+  }();
+  return n;
+}
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
-template <int KP4, bool BT, bool PUSH>
+template <int KP4, bool BT, bool PUSH, int kE>
 __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                  const int n_emb) {
   const int bid = blockIdx.x;
   if (bid < n_emb)
-    emb_rows_body<KP4, kTailThreads, BT, PUSH>(e, bid);  // the longer role first: its workgroups dispatch first
+    emb_rows_body<KP4, kTailThreads, BT, PUSH, kE>(e, bid);  // the longer role first: its workgroups dispatch first
   else
     wgrad_body<PUSH>(w, bid - n_emb);
+}
+
+template <int KP4, bool PUSH, int kE>
+static void launch_tail_e(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
+                          hipStream_t stream) {
+  if (e.tbl_bf16)
+    hipLaunchKernelGGL((step_tail_kernel<KP4, true, PUSH, kE>), grid, block, 0, stream, w, e, n_emb);
+  else
+    hipLaunchKernelGGL((step_tail_kernel<KP4, false, PUSH, kE>), grid, block, 0, stream, w, e, n_emb);
 }
 
 template <int KP4, bool PUSH>
 static void launch_tail_t(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
                           hipStream_t stream) {
-  if (e.tbl_bf16)
-    hipLaunchKernelGGL((step_tail_kernel<KP4, true, PUSH>), grid, block, 0, stream, w, e, n_emb);
+  if (tail_chunk_entries() == 256)
+    launch_tail_e<KP4, PUSH, 256>(w, e, n_emb, grid, block, stream);
   else
-    hipLaunchKernelGGL((step_tail_kernel<KP4, false, PUSH>), grid, block, 0, stream, w, e, n_emb);
+    launch_tail_e<KP4, PUSH, 512>(w, e, n_emb, grid, block, stream);
 }
 
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
@@ -38,7 +61,7 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
                 "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
   const int n_wg = wgrad_prepare(w);
-  const int n_emb = e.n > 0 ? cdiv(e.n, kTailThreads) : 0;
+  const int n_emb = e.n > 0 ? cdiv(e.n, tail_chunk_entries()) : 0;
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
   const bool push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);

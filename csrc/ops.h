@@ -16,8 +16,11 @@
 namespace rocfm {
 
 // deepfm_rows.hip
-RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0);
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0, int dedup_kp = 0, int rt = 16,
+                        bool gr_alias = false);
+RowsLds rows_lds_layout_for(const RowsParams& p);  // the layout the launcher uses
 void launch_deepfm_rows(RowsParams p, hipStream_t stream);
+int deepfm_rows_tile(const RowsParams& p);
 
 // mlp_wgrad.hip
 void launch_mlp_wgrad(WgradParams p, hipStream_t stream);
@@ -27,6 +30,8 @@ void launch_dense_apply(DenseApplyParams p, hipStream_t stream);
 
 // step_tail.hip: mlp_wgrad + emb_rows_update as workgroup roles of one launch
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream);
+constexpr int kTailChunkDefault = 256;  // profiles/r3_dedup.md: 20-step windows 33.0 vs 34.6 µs
+int tail_chunk_entries();  // sorted entries per embedding workgroup of the fused tail
 
 // sort.hip
 size_t sort_pairs_temp_bytes(int n, int end_bit);

@@ -289,3 +289,11 @@ def test_streamed_multi_gpu_equals_pool_fed(tmp_path, kind, world):
     (ea, da, sa, sha, na), (eb, db, sb, shb, nb) = r["stream"], r["pool"]
     assert sa == sb == 13 and na == 13 and sha == shb == "ok", (sa, sb, na, sha, shb)
     assert torch.equal(ea, eb) and torch.equal(da, db)
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_dp_with_dedup(tmp_path, monkeypatch, update):
+    """Per-tile dedup (ROCFM_DEDUP=1) under DP: compacted per-rank export lists through the p2p
+    exchange and multi-step graphs ≡ the single-GPU engine (Momentum, element-tight)."""
+    monkeypatch.setenv("ROCFM_DEDUP", "1")
+    _check_dp_vs_single(tmp_path, 2, "dp", "p2p", 11, 4, update)

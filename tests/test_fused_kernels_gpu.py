@@ -436,6 +436,7 @@ def test_row_tile_8_equals_16(K, layers, dtype, monkeypatch):
     """8 or 4 examples per row-kernel workgroup (2× / 4× the workgroups) computes every valid row
     with the same arithmetic as 16 (padding rows of the MFMA tile are zero and never stored): Adam
     + dropout through multi-step graphs, a batch that is not a multiple of 16 — bitwise equal."""
+    monkeypatch.setenv("ROCFM_DEDUP", "0")  # (dedup groups depend on the row tile: test_dedup_*)
     spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=K, layers=layers,
                      keep_probs=[0.7] * len(layers), l2_reg=1e-3)
     hp = OptHParams(name="Adam", lr=2e-3)
@@ -457,3 +458,105 @@ def test_row_tile_8_equals_16(K, layers, dtype, monkeypatch):
         b = out[rt]
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[3], b[3]), rt
         assert all(torch.equal(x, y) for x, y in zip(a[2], b[2])), rt
+
+
+def _dedup_ref(ids_sorted, pos_sorted, F, rt):
+    """numpy reference of the per-tile dedup of one sorted batch."""
+    n = len(ids_sorted)
+    tile = (pos_sorted // F) // rt
+    head = np.ones(n, bool)
+    head[1:] = (ids_sorted[1:] != ids_sorted[:-1]) | (tile[1:] != tile[:-1])
+    c = np.cumsum(head) - 1
+    pos = np.zeros(n, np.int64)
+    nxt = np.full(n, -1, np.int64)
+    pos[pos_sorted] = np.where(head, c, ~c)
+    more = np.zeros(n, bool)
+    more[:-1] = ~head[1:]
+    nxt[pos_sorted[:-1][more[:-1]]] = pos_sorted[1:][more[:-1]]
+    return pos, nxt, ids_sorted[head], int(head.sum())
+
+
+@pytest.mark.parametrize("rt,chunk", [(8, 512), (16, 256), (4, 512)])
+def test_dedup_kernel_matches_reference(rt, chunk):
+    """batch.hip dedup: group index / next-member links / compacted keys / count / per-chunk run
+    ends and run heads of a sorted batch with hot ids (fixed ids in every row, a hot id in two
+    fields of one row) equal a numpy reference."""
+    from rocfm.ops import require_hip
+
+    H = require_hip()
+    B, F, V = 300, 39, 5000
+    g = torch.Generator().manual_seed(rt)
+    ids, _, _ = _batch(B, F, V, g)
+    ids[:, 20] = ids[:, 21]  # the same id twice in one row
+    n = B * F
+    dev = torch.device("cuda")
+    flat = ids.reshape(-1).cuda()
+    sk, sv = torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev)
+    temp = torch.zeros(max(H.sort_pairs_temp_bytes(n, 13), 16), dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    H.sort_pairs_iota(temp.data_ptr(), temp.numel(), flat.data_ptr(), sk.data_ptr(), sv.data_ptr(), n, 13, s)
+    nch = (n + chunk - 1) // chunk
+    out = {k: torch.full((n,), -7, dtype=torch.int32, device=dev) for k in ("pos", "nxt", "ck")}
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cend, chd = (torch.zeros(nch, dtype=torch.int32, device=dev) for _ in range(2))
+    bc = torch.zeros(H.dedup_scratch_ints(n, 1), dtype=torch.int32, device=dev)
+    d = H.DedupParams()
+    d.skeys, d.svals, d.n, d.S, d.F, d.rt, d.val_base_step = sk.data_ptr(), sv.data_ptr(), n, 1, F, rt, 0
+    d.pos, d.nxt, d.ckeys = out["pos"].data_ptr(), out["nxt"].data_ptr(), out["ck"].data_ptr()
+    d.count, d.bcount, d.chunk = cnt.data_ptr(), bc.data_ptr(), chunk
+    d.chunk_end, d.chunk_heads = cend.data_ptr(), chd.data_ptr()
+    H.dedup(d, s)
+    torch.cuda.synchronize()
+    pos, nxt, ck, c = _dedup_ref(sk.cpu().numpy().astype(np.int64), sv.cpu().numpy().astype(np.int64), F, rt)
+    assert int(cnt.item()) == c
+    np.testing.assert_array_equal(out["pos"].cpu().numpy(), pos)
+    np.testing.assert_array_equal(out["nxt"].cpu().numpy(), nxt)
+    np.testing.assert_array_equal(out["ck"].cpu().numpy()[:c], ck)
+    for j in range(nch):  # run end of each compacted chunk's last run, run heads per chunk
+        lo = j * chunk
+        if lo >= c:
+            assert int(cend[j]) == c
+            continue
+        last = min(lo + chunk, c) - 1
+        e = last + 1
+        while e < c and ck[e] == ck[last]:
+            e += 1
+        assert int(cend[j]) == e, j
+        seg = ck[lo:min(lo + chunk, c)]
+        heads = sum(1 for i in range(lo, min(lo + chunk, c)) if i == 0 or ck[i] != ck[i - 1])
+        assert int(chd[j]) == heads, (j, seg[:4])
+
+
+@pytest.mark.parametrize("rt", ["8", "16"])
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_dedup_equals_no_dedup(rt, update, monkeypatch):
+    """Per-tile dedup changes only the summation order of each id's gradient rows: with Momentum
+    every element matches the un-deduplicated engine to fp32 reorder bounds, and the multi-step
+    graphs equal the per-step launches bitwise (both dedup)."""
+    monkeypatch.setenv("ROCFM_ROW_TILE", rt)
+    spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=10, layers=[128, 64, 32],
+                     keep_probs=[0.8] * 3, l2_reg=1e-3)
+    hp = OptHParams(name="Momentum", lr=0.02)
+    g = torch.Generator().manual_seed(5)
+    B = 256
+    pool = [_batch(B, 39, 3000, g) for _ in range(5)]
+    ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
+    out = {}
+    for dd, graphs in ((False, True), (True, True), (True, False)):
+        e = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=graphs, embedding_update=update,
+                        dedup=dd)
+        assert e.dedup == dd
+        e.attach_pool(ids, vals, labels)
+        if graphs:
+            e.train_steps(13, 4)
+        else:
+            for _ in range(13):
+                e.train_step()
+        torch.cuda.synchronize()
+        e.check()
+        out[(dd, graphs)] = (e.emb.clone(), e.dense.clone(), [x.clone() for x in e.emb_slots])
+    a, b, c = out[(False, True)], out[(True, True)], out[(True, False)]
+    assert torch.equal(b[0], c[0]) and torch.equal(b[1], c[1])
+    for x, y in [(a[0], b[0]), (a[1], b[1])] + list(zip(a[2], b[2])):
+        d = (x - y).abs()
+        assert bool((d <= 1e-7 + 1e-5 * y.abs()).all()), d.max().item()

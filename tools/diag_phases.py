@@ -50,7 +50,7 @@ def main():
     for _ in range(6):
         eng.train_step()
     torch.cuda.synchronize()
-    nrows = eng.Bp // 16
+    nrows = eng.Bp // 4  # ≥ the row kernel's workgroups (4..16 examples each)
     s_rows = torch.zeros(nrows * 16, dtype=torch.int64, device=dev)
     s_wg = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
     s_emb = torch.zeros(((eng.n_lookup + 255) // 256) * 16, dtype=torch.int64, device=dev)  # ≥ per-chunk slots
@@ -89,7 +89,7 @@ def main():
     sk = eng.skeys[p].cpu().long()
     heads = torch.ones_like(sk, dtype=torch.bool)
     heads[1:] = sk[1:] != sk[:-1]
-    chunk = 512 if eng.Kp <= 32 else 256  # step_tail's / emb_update's entries per workgroup
+    chunk = eng.H.tail_chunk() if eng.Kp <= 48 else 256  # step_tail's / emb_update's entries per workgroup
     st = s_emb.view(-1, 16).cpu().double()
     nwg = (sk.numel() + chunk - 1) // chunk
     tot = (st[:nwg, 4] - st[:nwg, 0]) * 0.01
