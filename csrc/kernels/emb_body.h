@@ -52,6 +52,8 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   __shared__ float4 s_cont[kWaves * KP4];
   __shared__ int s_head[kChunk + 1];
   __shared__ uint32_t s_hkey[kChunk + 1];
+  __shared__ uint32_t s_hprev[kChunk + 1];  // sorted export directory: key of the entry before each head
+  __shared__ int s_total;
   __shared__ int s_wcnt[kWaves];
   __shared__ int s_nh, s_last_end, s_out_base;
   __shared__ int s_hb[2 * kWaves];
@@ -82,12 +84,13 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   ROCFM_STAMP(p.stamps, 0);
 
   // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
-  uint32_t key = 0xffffffffu;
+  uint32_t key = 0xffffffffu, prevk = 0xffffffffu;
   bool head = false;
   float4 v[KP4];
   if (live) {
     key = p.skeys[i];
-    head = (i == 0) || (p.skeys[i - 1] != key);
+    if (i > 0) prevk = p.skeys[i - 1];
+    head = (i == 0) || (prevk != key);
     const bool skip = p.max_key && key >= p.max_key;
     const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)i * p.Kp)
                                          : contrib_row4(p, p.svals[i] - p.val_base);
@@ -134,6 +137,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       tot += s_hb[kWaves + w];
     }
     s_out_base = b;
+    s_total = tot;
     if (bid == 0) *p.out_count = tot;
   }
   {
@@ -142,6 +146,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     if (head) {
       s_head[base + before] = i;
       s_hkey[base + before] = key;
+      s_hprev[base + before] = i > 0 ? prevk : 0xffffffffu;
     }
   }
   if (t == 0) {
@@ -266,6 +271,23 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       if (p.max_key && kk[u] >= p.max_key) continue;
       if (p.mode == 2) {
         const int slot = s_out_base + r;
+        if (sorted_out && p.dir_nb > 0 && u4 == 0) {  // this head opens the buckets (prev, own]
+          const uint32_t row_id = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;
+          const int bc = (int)min(row_id / p.dir_div, (uint32_t)p.dir_nb - 1u);
+          const uint32_t pk = s_hprev[r];
+          const int bp = pk == 0xffffffffu ? -1
+                                           : (int)min(((pk - p.id_offset) / (uint32_t)p.id_stride) / p.dir_div,
+                                                      (uint32_t)p.dir_nb - 1u);
+          const int b_end = (slot == s_total - 1) ? p.dir_nb : bc;  // the last head closes the directory
+          for (int bb = bp + 1; bb <= b_end; ++bb) {
+            const int v = bb <= bc ? slot : s_total;
+            if (push) {
+              for (int d = 0; d < p.push.W; ++d) reinterpret_cast<int32_t*>(p.push.slot[d] + p.push_off_dir)[bb] = v;
+            } else {
+              p.out_dir[bb] = v;
+            }
+          }
+        }
         if (slot < p.out_cap) {
           const uint32_t row_id = (kk[u] - p.id_offset) / (uint32_t)p.id_stride;  // the table row id
           if (push) {  // this rank's slot in every receive buffer (xGMI stores under the tail)

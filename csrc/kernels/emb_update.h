@@ -61,6 +61,13 @@ struct EmbUpdateParams {
   // nullable: the entry count is this device word (per-tile dedup: the compacted list's length,
   // written by the side chain); n is then the maximum and sizes the grid
   const int32_t* n_dev;
+  // mode 2 sorted export (chunk_heads): bucket directory of the exported keys (merge range mode):
+  // dir[b] = first output slot whose row id is ≥ b·dir_div, b = 0..dir_nb (dir[dir_nb] = count);
+  // out_dir (local) or, with push, every receive slot at push_off_dir
+  int32_t* out_dir;
+  int dir_nb;
+  uint32_t dir_div;
+  int push_off_dir;
 };
 
 struct EmbDenseParams {

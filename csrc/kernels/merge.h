@@ -66,6 +66,13 @@ struct MergeParams {
   unsigned long long* hpos;   // [hash_slots][W]
   int tbl_bf16;               // 1: emb holds bf16 rows (stochastic-rounded updates, common.h)
   int use_maps;               // merge_search_apply: 1 = apply through the maps a merge_scatter filled
+  // range mode (merge_range_apply): every source list ascending with a bucket directory —
+  // dirs + r·dir_stride holds nb + 1 offsets, dir[b] = first position of source r whose key is
+  // ≥ b·bucket_div (the sorted DP export writes it beside its keys)
+  const int32_t* dirs;
+  long long dir_stride;
+  int nb;
+  uint32_t bucket_div;
 };
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);
@@ -89,6 +96,15 @@ struct HotApplyParams {
   const int64_t* step;
   int dense;              // 1 (exact): every replicated row is updated (g = λ·θ when untouched)
 };
+
+// Range mode: one workgroup per key bucket stages the W sources' entries of its bucket (keys and
+// gradient rows, located through the directories: one round trip) in LDS, matches equal keys
+// there (LDS binary searches instead of the search mode's global ones), and the representative
+// (lowest rank holding the key) sums the rows in rank order and applies the optimizer — the same
+// arithmetic as the search / maps merges.  Buckets larger than the LDS stage fall back to global
+// binary searches inside their bucket.  d (nullable): the MLP optimizer as extra workgroups.
+void launch_merge_range_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream);
+int merge_range_lds_entries(int Kp);
 
 // search mode; d (nullable): the MLP optimizer launched as extra workgroups; sv (nullable): a
 // row-shard serve (shard.h) as further workgroups; hot (nullable): the replicated rows' update

@@ -481,6 +481,172 @@ __global__ __launch_bounds__(kApplyThreads) void merge_search_apply_kernel(Merge
   }
 }
 
+// ---- range mode ------------------------------------------------------------------------------
+constexpr int kRangeThreads = 256;
+// LDS stage per workgroup: small enough for several workgroups per CU (W = 8 launches ≈ 316 of them
+// on 256 CUs); larger buckets take the global-search fallback
+constexpr int kRangeLdsBytes = 36 * 1024;
+
+// Position of key in the ascending run [lo, hi) of an LDS key array, or -1
+__device__ __forceinline__ int lds_find(const uint32_t* k, int lo, int hi, uint32_t key) {
+  int len = hi - lo;
+  while (len > 0) {
+    const int half = len >> 1;
+    const uint32_t v = k[lo + half];
+    if (v == key) return lo + half;
+    if (v < key) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return -1;
+}
+
+// ... of a source list in global memory: positions [lo, hi) of source q
+__device__ __forceinline__ int glob_find(const MergeParams& p, int q, int lo, int hi, uint32_t key) {
+  const uint32_t* L = list_of(p, q);
+  int len = hi - lo;
+  while (len > 0) {
+    const int half = len >> 1;
+    const uint32_t v = L[lo + half];
+    if (v == key) return lo + half;
+    if (v < key) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return -1;
+}
+
+// The row's parameters / slots (mode 0), then the optimizer or the dense-gradient row
+template <int KP4>
+__device__ __forceinline__ void range_row_out(const MergeParams& p, uint32_t row, const float4 (&acc)[KP4]) {
+  const size_t base = (size_t)row * KP4;
+  float4 w[KP4], a[KP4], b[KP4];
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.mode == 0) {
+    const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
+    const float4* b4r = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb) + base;
+#pragma unroll
+    for (int c = 0; c < KP4; ++c) {
+      w[c] = tbl_load4_rt(p.emb, base + c, p.tbl_bf16 != 0);
+      a[c] = p.s0 ? a4r[c] : z;
+      b[c] = p.s1 ? b4r[c] : z;
+    }
+  }
+  merged_row_out<KP4>(p, row, w, a, b, acc);
+}
+
+template <int KP4>
+__device__ __forceinline__ void merge_range_body(const MergeParams& p, const int bkt, const int cap_lds) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* s_row = reinterpret_cast<float4*>(smem);                                 // [cap_lds][KP4]
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(smem + (size_t)cap_lds * KP4 * 16);  // [cap_lds]
+  __shared__ int s_lo[kMaxW], s_off[kMaxW + 1];
+  const int W = p.W, t = threadIdx.x;
+  if (t < W) {  // this bucket's range of source t: one round trip for all sources
+    const int len = len_of(p, t);
+    const int32_t* d = p.dirs + (size_t)t * p.dir_stride;
+    const int lo = min(max(d[bkt], 0), len), hi = min(max(d[bkt + 1], 0), len);
+    s_lo[t] = lo;
+    s_off[t + 1] = max(hi - lo, 0);
+  }
+  __syncthreads();
+  if (t == 0) {
+    s_off[0] = 0;
+    for (int q = 0; q < W; ++q) s_off[q + 1] += s_off[q];
+  }
+  __syncthreads();
+  const int m = s_off[W];
+  if (m == 0) return;
+  if (m <= cap_lds) {
+    // 1. stage every source's keys + gradient rows of the bucket (independent loads)
+    for (int e = t; e < m; e += kRangeThreads) {
+      int r = 0;
+      while (r + 1 < W && e >= s_off[r + 1]) ++r;
+      const int j = s_lo[r] + e - s_off[r];
+      s_key[e] = list_of(p, r)[j];
+      const float4* src = reinterpret_cast<const float4*>(p.rows + (size_t)r * p.row_stride + (size_t)j * p.Kp);
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) s_row[(size_t)e * KP4 + c] = src[c];
+    }
+    __syncthreads();
+    // 2. representatives (no lower rank holds the key) sum the rows in rank order
+    for (int e = t; e < m; e += kRangeThreads) {
+      int r = 0;
+      while (r + 1 < W && e >= s_off[r + 1]) ++r;
+      const uint32_t key = s_key[e];
+      if (key == kPadKey || key / p.key_div >= p.Vmap) continue;
+      bool rep = true;
+      for (int q = 0; q < r && rep; ++q) rep = lds_find(s_key, s_off[q], s_off[q + 1], key) < 0;
+      if (!rep) continue;
+      float4 acc[KP4];
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) acc[c] = s_row[(size_t)e * KP4 + c];
+      for (int q = r + 1; q < W; ++q) {
+        const int f = lds_find(s_key, s_off[q], s_off[q + 1], key);
+        if (f < 0) continue;
+#pragma unroll
+        for (int c = 0; c < KP4; ++c) acc[c] = f4add_m(acc[c], s_row[(size_t)f * KP4 + c]);
+      }
+      range_row_out<KP4>(p, key / p.key_div, acc);
+    }
+  } else {  // a bucket larger than the stage: global binary searches inside the bucket's ranges
+    for (int e = t; e < m; e += kRangeThreads) {
+      int r = 0;
+      while (r + 1 < W && e >= s_off[r + 1]) ++r;
+      const int j = s_lo[r] + e - s_off[r];
+      const uint32_t key = list_of(p, r)[j];
+      if (key == kPadKey || key / p.key_div >= p.Vmap) continue;
+      bool rep = true;
+      for (int q = 0; q < r && rep; ++q) rep = glob_find(p, q, s_lo[q], s_lo[q] + s_off[q + 1] - s_off[q], key) < 0;
+      if (!rep) continue;
+      float4 acc[KP4];
+      const float4* own = reinterpret_cast<const float4*>(p.rows + (size_t)r * p.row_stride + (size_t)j * p.Kp);
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) acc[c] = own[c];
+      for (int q = r + 1; q < W; ++q) {
+        const int f = glob_find(p, q, s_lo[q], s_lo[q] + s_off[q + 1] - s_off[q], key);
+        if (f < 0) continue;
+        const float4* src = reinterpret_cast<const float4*>(p.rows + (size_t)q * p.row_stride + (size_t)f * p.Kp);
+#pragma unroll
+        for (int c = 0; c < KP4; ++c) acc[c] = f4add_m(acc[c], src[c]);
+      }
+      range_row_out<KP4>(p, key / p.key_div, acc);
+    }
+  }
+}
+
+template <int KP4>
+__global__ __launch_bounds__(kRangeThreads) void merge_range_apply_kernel(MergeParams p, DenseApplyParams d,
+                                                                          int n_range, int n_dense, int cap_lds) {
+  if ((int)blockIdx.x < n_range)
+    merge_range_body<KP4>(p, blockIdx.x, cap_lds);
+  else
+    dense_apply_body<kRangeThreads>(d, blockIdx.x - n_range, n_dense);
+}
+
+template <int KP4>
+void launch_range_t(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+  const int cap_lds = merge_range_lds_entries(p.Kp);
+  const int lds = cap_lds * (KP4 * 16 + 4);
+  auto kern = merge_range_apply_kernel<KP4>;
+  static bool attr = false;
+  if (!attr) {
+    ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kRangeLdsBytes));
+    attr = true;
+  }
+  const int n_dense = d ? std::max(1, std::min(cdiv(d->n, kRangeThreads), 256)) : 0;
+  DenseApplyParams dd{};
+  if (d) dd = *d;
+  hipLaunchKernelGGL(kern, dim3(p.nb + n_dense), dim3(kRangeThreads), lds, stream, p, dd, p.nb, n_dense, cap_lds);
+}
+
 template <int KP4>
 void launch_search_t(const MergeParams& p, const DenseApplyParams* d, const ShardServeParams* sv,
                      const HotApplyParams* hot, hipStream_t stream) {
@@ -579,6 +745,31 @@ void launch_merge_search_apply(const MergeParams& p, const DenseApplyParams* d, 
 #undef ROCFM_KP4
     default:
       throw std::invalid_argument("merge: unsupported Kp");
+  }
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+int merge_range_lds_entries(int Kp) {
+  const int per = Kp * 4 + 4;  // gradient row + key
+  return std::min(512, kRangeLdsBytes / per / 64 * 64);
+}
+
+void launch_merge_range_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream) {
+  ROCFM_REQUIRE(p.W >= 1 && p.W <= kMaxW, "merge_range: 1 <= W <= 64");
+  ROCFM_REQUIRE(p.Kp % 4 == 0 && p.Kp >= 4 && p.Kp <= 64 && p.K1 <= p.Kp, "merge_range: bad Kp");
+  ROCFM_REQUIRE(p.key_div >= 1 && p.keys && p.rows && p.step && p.dirs && p.nb >= 1 && p.bucket_div >= 1,
+                "merge_range: keys / rows / step / directories missing");
+  ROCFM_REQUIRE(p.mode == 1 ? p.dense_grad != nullptr : p.emb != nullptr, "merge_range: missing outputs");
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N)                 \
+  case N:                            \
+    launch_range_t<N>(p, d, stream); \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("merge_range: unsupported Kp");
   }
   ROCFM_HIP_CHECK(hipGetLastError());
 }

@@ -560,3 +560,64 @@ def test_dedup_equals_no_dedup(rt, update, monkeypatch):
     for x, y in [(a[0], b[0]), (a[1], b[1])] + list(zip(a[2], b[2])):
         d = (x - y).abs()
         assert bool((d <= 1e-7 + 1e-5 * y.abs()).all()), d.max().item()
+
+
+@pytest.mark.parametrize("W,mode", [(2, 0), (3, 1), (8, 0)])
+def test_merge_range_equals_search(W, mode):
+    """merge.hip range mode (bucket directories, LDS-staged matching; one bucket holds more
+    entries than the LDS stage and takes the global-search fallback) sums every key's rows in the
+    search mode's rank order: the dense-gradient rows (mode 1) are bitwise equal; after the Adam
+    update (mode 0) the two kernels' instruction selection may differ in the last bit."""
+    from rocfm.ops import require_hip
+    from rocfm.parallel.dp import range_merge_buckets
+
+    H = require_hip()
+    dev = torch.device("cuda")
+    V, Kp = 2_000_000, 12
+    g = torch.Generator().manual_seed(W)
+    lists = []
+    for r in range(W):
+        hot = torch.arange(0, 600)  # bucket 0 crowded in every rank (> the LDS stage in total)
+        rnd = torch.randint(0, V, (3000 + 500 * r,), generator=g)
+        lists.append(torch.unique(torch.cat([hot, rnd])))
+    cap = (max(len(x) for x in lists) + 3) // 4 * 4
+    keys = torch.full((W, cap), -1, dtype=torch.int32)
+    for r, x in enumerate(lists):
+        keys[r, : len(x)] = x.to(torch.int32)
+    keys = keys.to(dev)
+    counts = torch.tensor([len(x) for x in lists], dtype=torch.int32, device=dev)
+    rows = torch.randn(W, cap, Kp, generator=g).to(dev)
+    nb = range_merge_buckets(W, cap)
+    div = (V + nb - 1) // nb
+    dirs = torch.stack([torch.searchsorted(x, torch.arange(nb + 1) * div).to(torch.int32) for x in lists]).to(dev)
+    assert int((dirs[:, 1] - dirs[:, 0]).sum()) > H.merge_range_lds_entries(Kp)  # the fallback bucket
+    step = torch.zeros(1, dtype=torch.int64, device=dev)
+    outs = []
+    for rng in (False, True):
+        emb = torch.randn(V, Kp, generator=torch.Generator().manual_seed(1)).to(dev)
+        s0, s1 = torch.zeros_like(emb), torch.zeros_like(emb)
+        dg, touched = torch.zeros_like(emb), torch.zeros(V, dtype=torch.int32, device=dev)
+        p = H.MergeParams()
+        p.keys, p.key_stride, p.rows, p.row_stride = keys.data_ptr(), cap, rows.data_ptr(), cap * Kp
+        p.counts, p.count_stride = counts.data_ptr(), 1
+        p.W, p.cap, p.Kp, p.K1, p.key_div, p.Vmap = W, cap, Kp, Kp - 1, 1, V
+        p.emb, p.s0, p.s1, p.l2, p.grad_scale = emb.data_ptr(), s0.data_ptr(), s1.data_ptr(), 1e-3, 1.0 / W
+        o = H.OptParams()
+        o.type, o.lr, o.beta1, o.beta2, o.eps = 0, 1e-3, 0.9, 0.999, 1e-8  # Adam
+        lrt = torch.full((1,), 1e-3, device=dev)
+        o.lrt = lrt.data_ptr()
+        p.opt, p.step, p.mode = o, step.data_ptr(), mode
+        p.dense_grad, p.touched = dg.data_ptr(), touched.data_ptr()
+        p.dirs, p.dir_stride, p.nb, p.bucket_div = dirs.data_ptr(), nb + 1, nb, div
+        s = torch.cuda.current_stream().cuda_stream
+        if rng:
+            H.merge_range_apply(p, None, s)
+        else:
+            H.merge_search_apply(p, None, s)
+        torch.cuda.synchronize()
+        outs.append((emb.cpu(), s0.cpu(), s1.cpu(), dg.cpu(), touched.cpu()))
+    for a, b in zip(*outs):
+        if mode == 1:
+            assert torch.equal(a, b)
+        else:
+            assert bool(((a.float() - b.float()).abs() <= 1e-6 * b.float().abs() + 1e-9).all())

@@ -20,6 +20,13 @@ from rocfm.data.synthetic import SyntheticCriteo  # noqa: E402
 from rocfm.ops import require_hip  # noqa: E402
 
 
+def range_buckets(W: int, cap: int) -> int:
+    """Buckets of the range merge: ≈192 gathered entries per workgroup, at least 64."""
+    from rocfm.parallel.dp import range_merge_buckets
+
+    return range_merge_buckets(W, cap)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--V", type=int, default=1_000_000)
@@ -27,13 +34,21 @@ def main():
     ap.add_argument("--F", type=int, default=39)
     ap.add_argument("--Kp", type=int, default=12)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--hash", action="store_true")
     a = ap.parse_args()
     H = require_hip()
     dev = torch.device("cuda")
     gen = SyntheticCriteo(a.V, a.F, seed=1)
     g = torch.Generator(device=dev).manual_seed(1)
+    # --hash: keys are a bijective multiplicative hash of the ids (id · odd mod 2^bits), spreading
+    # the Zipf-clustered ids uniformly over the key space (what the range merge's buckets need)
+    bits = max(1, (a.V - 1).bit_length())
     for W in (1, 2, 4, 8):
-        lists = [torch.unique(gen.batch(a.B, dev, g)[0].flatten().to(torch.int64)) for _ in range(W)]
+        lists = [gen.batch(a.B, dev, g)[0].flatten().to(torch.int64) for _ in range(W)]
+        if a.hash:
+            lists = [(x * 0x9E3779B1) & ((1 << bits) - 1) for x in lists]
+        lists = [torch.unique(x) for x in lists]
+        Vk = (1 << bits) if a.hash else a.V
         cap = (max(len(x) for x in lists) + 3) // 4 * 4
         keys = torch.full((W, cap), 0xFFFFFFFF, dtype=torch.int64)
         for r, x in enumerate(lists):
@@ -41,27 +56,38 @@ def main():
         keys32 = torch.from_numpy(keys.numpy().astype(np.uint32).view(np.int32)).to(dev)  # pads = 0xFFFFFFFF
         counts = torch.tensor([len(x) for x in lists], dtype=torch.int32, device=dev)
         rows = torch.randn(W, cap, a.Kp, device=dev)
-        dg = torch.zeros(a.V, a.Kp, device=dev)
-        touched = torch.zeros(a.V, dtype=torch.int32, device=dev)
+        dg = torch.zeros(Vk, a.Kp, device=dev)
+        touched = torch.zeros(Vk, dtype=torch.int32, device=dev)
         step = torch.zeros(1, dtype=torch.int64, device=dev)
-        pos = torch.full((W * a.V,), -1, dtype=torch.int32, device=dev)
-        rep = torch.full((a.V,), W, dtype=torch.int32, device=dev)
+        pos = torch.full((W * Vk,), -1, dtype=torch.int32, device=dev)
+        rep = torch.full((Vk,), W, dtype=torch.int32, device=dev)
         p = H.MergeParams()
         p.keys, p.key_stride = keys32.data_ptr(), cap
         p.rows, p.row_stride = rows.data_ptr(), cap * a.Kp
         p.counts, p.count_stride = counts.data_ptr(), 1
         p.W, p.cap, p.Kp, p.K1 = W, cap, a.Kp, a.Kp - 1
-        p.key_div, p.Vmap = 1, a.V
+        p.key_div, p.Vmap = 1, Vk
         p.pos, p.rep = pos.data_ptr(), rep.data_ptr()
         p.mode, p.dense_grad, p.touched, p.step = 1, dg.data_ptr(), touched.data_ptr(), step.data_ptr()
         p.emb = dg.data_ptr()  # merge_apply loads the table row in every mode (any valid [V][Kp] f32)
         p.grad_scale = 1.0 / W
+        # range mode: bucket directories of the sorted lists (what the sorted DP export writes)
+        nb = range_buckets(W, cap)
+        div = (Vk + nb - 1) // nb
+        bounds = torch.arange(nb + 1, dtype=torch.int64) * div
+        dirs = torch.zeros(W, nb + 1, dtype=torch.int32)
+        for r, x in enumerate(lists):
+            dirs[r] = torch.searchsorted(x.cpu(), bounds).to(torch.int32)
+        dirs = dirs.to(dev)
+        p.dirs, p.dir_stride, p.nb, p.bucket_div = dirs.data_ptr(), nb + 1, nb, div
         s = torch.cuda.current_stream().cuda_stream
         res = {}
-        for name in ("search", "maps"):
+        for name in ("search", "maps", "range"):
             def run():
                 if name == "search":
                     H.merge_search_apply(p, None, s)
+                elif name == "range":
+                    H.merge_range_apply(p, None, s)
                 else:
                     H.merge_scatter(p, s)
                     H.merge_apply(p, s)
@@ -74,7 +100,22 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[name] = e0.elapsed_time(e1) * 1000 / a.iters
-        print(f"W={W} cap={cap} entries={W * cap}: search {res['search']:.2f} us, maps {res['maps']:.2f} us")
+        print(f"W={W} cap={cap} entries={W * cap} buckets={nb}: search {res['search']:.2f} us, "
+              f"maps {res['maps']:.2f} us, range {res['range']:.2f} us")
+        # the three merges write the same dense gradient rows
+        outs = []
+        for name in ("search", "maps", "range"):
+            dg.zero_()
+            if name == "search":
+                H.merge_search_apply(p, None, s)
+            elif name == "range":
+                H.merge_range_apply(p, None, s)
+            else:
+                H.merge_scatter(p, s)
+                H.merge_apply(p, s)
+            torch.cuda.synchronize()
+            outs.append(dg.clone())
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), W
 
 
 if __name__ == "__main__":
