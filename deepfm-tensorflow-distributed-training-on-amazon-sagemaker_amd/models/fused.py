@@ -112,7 +112,8 @@ class FusedDeepFM:
                  embedding_update: str = "sparse", seed: int = 1234,
                  params: Optional[Dict[str, torch.Tensor]] = None, grad_scale: float = 1.0,
                  use_graph: bool = True, fuse_dense_opt: bool = True, dropout_seed: Optional[int] = None,
-                 force_generic_kernels: bool = False, compute_dtype: str = "bf16", table_dtype: str = "f32"):
+                 force_generic_kernels: bool = False, compute_dtype: str = "bf16", table_dtype: str = "f32",
+                 dedup: Optional[bool] = None):
         if len(spec.layers) > 6:
             raise ValueError("the fused engine supports at most 6 hidden layers")
         self.H = require_hip()
@@ -135,11 +136,11 @@ class FusedDeepFM:
         self.loss_code = 0 if spec.loss_type == "log_loss" else 1
         self.lr_scale = 1.0
         self.force_generic = bool(force_generic_kernels)
-        # examples per row-kernel workgroup (compile-time-shape kernels): 16, or 8 for twice the
-        # workgroups (ROCFM_ROW_TILE; 0 = the kernel's default)
+        # examples per row-kernel workgroup (compile-time-shape kernels): 16, 8 or 4 — more, smaller
+        # workgroups on the 256-CU chip (ROCFM_ROW_TILE; 0 = the kernel's default, 8)
         self.row_tile = int(os.environ.get("ROCFM_ROW_TILE", "0"))
-        if self.row_tile not in (0, 8, 16):
-            raise ValueError(f"ROCFM_ROW_TILE must be 0, 8 or 16, got {self.row_tile}")
+        if self.row_tile not in (0, 4, 8, 16):
+            raise ValueError(f"ROCFM_ROW_TILE must be 0, 4, 8 or 16, got {self.row_tile}")
         if compute_dtype not in ("bf16", "fp8"):
             raise ValueError(f"compute_dtype must be bf16 or fp8, got {compute_dtype!r}")
         self.compute_dtype = compute_dtype
@@ -206,11 +207,28 @@ class FusedDeepFM:
         self.dzT = [torch.zeros(L.dims[a], Bp, dtype=torch.bfloat16, device=dev) if a > 0 else None
                     for a in range(L.nl + 1)]
         self.n_lookup = B * F
+        # per-tile dedup (batch.h DedupParams; ROCFM_DEDUP=1, off by default): the row kernel sums
+        # the gradient rows of each id within its row tile and the embedding update walks one entry
+        # per (id, tile) — the numeric fields' fixed ids come as ≤ B/RT entries instead of B.
+        # Measured at the bench config (profiles/r3_dedup.md): the tail 13.3 → 12.3 µs, the row
+        # kernel +0.75 µs and the side chain's three extra launches per graph — no net gain
+        if dedup is None:
+            dedup = os.environ.get("ROCFM_DEDUP", "0") == "1"
+        self.dedup = bool(dedup) and not self.bn
         self.end_bit = max(1, math.ceil(math.log2(max(self.V, 2))))
         self.skeys = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
         self.svals = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
         tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
         self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
+        if self.dedup:  # per parity: group index / next member by lookup, compacted keys, count, run ends
+            n, nch = self.n_lookup, (self.n_lookup + self.H.tail_chunk() - 1) // self.H.tail_chunk()
+            self.d_pos = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.d_nxt = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.d_ckeys = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.d_count = torch.zeros(2, dtype=torch.int32, device=dev)
+            self.d_cend = [torch.zeros(nch, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.d_bcount = [torch.zeros(self.H.dedup_scratch_ints(n, 1), dtype=torch.int32, device=dev)
+                             for _ in range(2)]
         self.dense_grad = (torch.zeros_like(self.emb, dtype=torch.float32) if embedding_update == "exact" else None)
         # exact mode: rows whose dense_grad holds this step's gradient carry touched[row] = step + 1,
         # so the dense update reads / clears gradient rows only there (None: read every row —
@@ -308,6 +326,7 @@ class FusedDeepFM:
         rp.force_generic = 1 if self.force_generic else 0
         rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
         rp.row_tile = self.row_tile
+        rp.dedup = 1 if (train and self.dedup) else 0
         rp.set_dims(L.dims)
         for l in range(L.nl):
             rp.set_layer(l, self.WT[l].data_ptr(), self.Wb[l].data_ptr(), self.dense[L.offb[l]:].data_ptr(),
@@ -322,6 +341,9 @@ class FusedDeepFM:
             for l in range(L.nl):
                 rp.set_bn(l, self.dense[L.off_gamma[l]:].data_ptr(), self.dense[L.off_beta[l]:].data_ptr(),
                           self.bn_stats[l, 0].data_ptr(), self.bn_stats[l, 1].data_ptr())
+        if rp.dedup and rp.lds_bytes() > 160 * 1024 - 256:  # no room for the tile's gradient rows
+            self.dedup = False
+            rp.dedup = 0
         if rp.lds_bytes() > 160 * 1024 - 256:  # 256 B: the kernel's static LDS (diagnostic stamps)
             raise ValueError(f"field_size*embedding_size too large for the fused row kernel ({rp.lds_bytes()} B LDS)")
         return rp
@@ -409,6 +431,13 @@ class FusedDeepFM:
             self.emb_params.append(ep)
             if ed is not None:
                 self.emb_dense_params.append(ed)
+            if self.dedup:  # the per-step sort's dedup outputs of this parity (_sort)
+                rows.contrib_pos, rows.contrib_nxt = self.d_pos[p].data_ptr(), self.d_nxt[p].data_ptr()
+                ep.skeys, ep.n_dev, ep.sorted_contrib = self.d_ckeys[p].data_ptr(), self.d_count[p:].data_ptr(), 1
+                if self.Kp <= self.H.tail_max_kp():
+                    ep.chunk_end = self.d_cend[p].data_ptr()
+        if self.dedup:
+            self._rt = self.H.deepfm_rows_tile(self.rows_params[0])  # the row tiles the dedup must cut
         self.pred_params = self._rows_params(self.pred_ids, self.pred_vals, self.pred_labels, self.pred_prob,
                                              self.pred_loss, self.steps.data_ptr(), False)
         self._build_fetch()
@@ -530,6 +559,15 @@ class FusedDeepFM:
         self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.slot_ids[q].data_ptr(),
                                self.skeys[q].data_ptr(), self.svals[q].data_ptr(), self.n_lookup, self.end_bit,
                                stream.cuda_stream)
+        if self.dedup:
+            d = self.H.DedupParams()
+            d.skeys, d.svals, d.n, d.S, d.F, d.rt = (self.skeys[q].data_ptr(), self.svals[q].data_ptr(),
+                                                     self.n_lookup, 1, self.F, self._rt)
+            d.val_base_step = 0
+            d.pos, d.nxt, d.ckeys = self.d_pos[q].data_ptr(), self.d_nxt[q].data_ptr(), self.d_ckeys[q].data_ptr()
+            d.count, d.bcount = self.d_count[q:].data_ptr(), self.d_bcount[q].data_ptr()
+            d.chunk, d.chunk_end = self.H.tail_chunk(), self.d_cend[q].data_ptr()
+            self.H.dedup(d, stream.cuda_stream)
 
     def prime(self) -> None:
         """Fetch + sort the current step's batch into its slot (before the first step / after a reset)."""
@@ -688,6 +726,13 @@ class FusedDeepFM:
         self.m_nch = (n + self.m_chunk - 1) // self.m_chunk
         self.m_cend = torch.zeros(2, Smax * self.m_nch, **i32)
         self.m_chd = torch.zeros(2, Smax * self.m_nch, **i32) if heads else None
+        # per-tile dedup (rows of ONE batch per row tile): group links, compacted keys and counts
+        self.m_dedup = self.dedup and shard is None
+        if self.m_dedup:
+            self.m_nxt = torch.zeros(2, Smax * n, **i32)
+            self.m_ck = torch.zeros(2, Smax * n, **i32)
+            self.m_cnt = torch.zeros(2, Smax, **i32)
+            self.m_bcount = torch.zeros(self.H.dedup_scratch_ints(n, Smax), **i32)
         self.m_steps = torch.zeros(2, Smax, dtype=torch.int64, device=dev)
         self.m_lrt = torch.zeros(2, Smax, dtype=torch.float32, device=dev)
         self.m_cur = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -702,6 +747,11 @@ class FusedDeepFM:
                 rows, _, _, ep, _ = self.m_params[q][k]
                 rows.contrib_pos = self.m_pos[q, k * n:].data_ptr()
                 ep.sorted_contrib = 1
+                if self.m_dedup:
+                    rows.contrib_nxt = self.m_nxt[q, k * n:].data_ptr()
+                    ep.skeys, ep.n_dev = self.m_ck[q, k * n:].data_ptr(), self.m_cnt[q, k:].data_ptr()
+                else:
+                    rows.dedup = 0
                 if self.Kp <= self.H.tail_max_kp():  # the fused tail's 512-entry chunks
                     ep.chunk_end = self.m_cend[q, k * self.m_nch:].data_ptr()
         self._m_graphs = {}
@@ -753,7 +803,22 @@ class FusedDeepFM:
             a.chunk_heads = self.m_chd[1 - q].data_ptr()
         if not self.m_composite:  # sorted 64-bit keys → plain per-batch ids in m_sk
             a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
-        H.sort_aux(a, stream.cuda_stream)
+        if self.m_dedup:  # positions / run ends / run heads come from the dedup over the compacted list
+            a.chunk_end = a.chunk_heads = 0
+        if not (self.m_dedup and self.m_composite):  # (64-bit keys: sort_aux writes the plain ids)
+            H.sort_aux(a, stream.cuda_stream)
+        if self.m_dedup:
+            d = H.DedupParams()
+            d.skeys, d.svals, d.n, d.S, d.F, d.rt = (self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(),
+                                                     self.n_lookup, self.mS, self.F, self._rt)
+            d.val_base_step = self.n_lookup
+            d.pos, d.nxt, d.ckeys = (self.m_pos[1 - q].data_ptr(), self.m_nxt[1 - q].data_ptr(),
+                                     self.m_ck[1 - q].data_ptr())
+            d.count, d.bcount = self.m_cnt[1 - q].data_ptr(), self.m_bcount.data_ptr()
+            d.chunk, d.chunk_end = self.m_chunk, self.m_cend[1 - q].data_ptr()
+            if self.m_chd is not None:
+                d.chunk_heads = self.m_chd[1 - q].data_ptr()
+            H.dedup(d, stream.cuda_stream)
         if getattr(self, "_m_post", None) is not None:  # e.g. row-shard routing of the sorted batches
             self._m_post(1 - q, stream)
 

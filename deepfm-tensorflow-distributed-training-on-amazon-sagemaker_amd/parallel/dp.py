@@ -81,7 +81,22 @@ def _all_reduce(t: torch.Tensor) -> None:
 # beyond it a scatter into position maps + apply is faster (tools/bench_merge.py on one MI355X,
 # 7.5k keys per rank: W=1 3.9 vs 8.9 µs, W=2 9.8 vs 10.0, W=4 12.8 vs 10.0, W=8 20.6 vs 13.7)
 SEARCH_MAX_W = 2
-MERGE_MAP_BUDGET = 512 << 20  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
+MERGE_MAP_BUDGET = 512 << 20
+
+
+def range_merge_buckets(W: int, cap: int) -> int:
+    """Key buckets of the range merge (merge.hip range mode, one workgroup each): ≈192 gathered
+    entries per bucket on average, at least 64."""
+    return max(64, -(-W * cap // 192))
+
+
+def range_merge_enabled(W: int) -> bool:
+    """The range merge (bucket directories written by the sorted export; merge.hip range mode) for
+    the multi-step DP path with ≥ 2 ranks — opt-in (ROCFM_MERGE=range).  Measured against the
+    search / maps merges (profiles/r3_merge_range.md): no gain on Criteo-shape ids, whose
+    field-clustered Zipf ids crowd a few key buckets; 8.6 vs 10.6 µs at W = 4 only when the keys
+    are first spread by a bijective hash."""
+    return W >= 2 and os.environ.get("ROCFM_MERGE", "auto") == "range"  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
 
 
 class MergeMaps:
@@ -93,8 +108,8 @@ class MergeMaps:
 
     def __init__(self, W: int, cap: int, rows: int, device):
         choice = os.environ.get("ROCFM_MERGE", "auto")
-        if choice not in ("auto", "direct", "hash"):
-            raise ValueError(f"ROCFM_MERGE must be auto, direct or hash, got {choice!r}")
+        if choice not in ("auto", "direct", "hash", "range"):
+            raise ValueError(f"ROCFM_MERGE must be auto, direct, hash or range, got {choice!r}")
         direct_bytes = (W + 1) * rows * 4
         self.hashed = choice == "hash" or (choice == "auto" and direct_bytes > MERGE_MAP_BUDGET)
         i32 = dict(dtype=torch.int32, device=device)
@@ -259,6 +274,7 @@ class FusedDataParallel:
         self.p2p = None
         self.force = force_collectives()
         self.exchange = "rccl"  # DP all-gather transport (mode dp: p2p.open_exchanges may pick "p2p")
+        self.range = False  # range merge (mode dp, set below)
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
             from .dist import broadcast_tensors
@@ -282,10 +298,16 @@ class FusedDataParallel:
             cap = (int(capacity or e.n_lookup) + 3) // 4 * 4  # keeps every row 16-B aligned
             self.cap = cap
             Kp = e.Kp
-            # send buffer (f32 words): [MLP grads P | pad to 4 | count (int32) + pad 3 | keys cap (int32) |
-            # rows cap*Kp]  (every part from the count on 16-B aligned)
+            # range merge (multi-step path): the sorted export also writes a bucket directory
+            self.range = range_merge_enabled(self.world) and Kp <= H.tail_max_kp()
+            self.nb = range_merge_buckets(self.world, cap) if self.range else 0
+            self.bdiv = -(-e.V // self.nb) if self.range else 0
+            ndir = (self.nb + 1 + 3) // 4 * 4 if self.range else 0
+            # send buffer (f32 words): [MLP grads P | pad to 4 | count (int32) + pad 3 | dir nb+1 (int32,
+            # range merge) | keys cap (int32) | rows cap*Kp]  (every part from the count on 16-B aligned)
             self.off_cnt = (P + 3) // 4 * 4
-            self.off_keys = self.off_cnt + 4
+            self.off_dir = self.off_cnt + 4
+            self.off_keys = self.off_dir + ndir
             self.off_rows = self.off_keys + cap
             self.S = (self.off_rows + cap * Kp + 3) // 4 * 4  # float4 payload (p2p push)
             self.send = torch.zeros(self.S, dtype=torch.float32, device=e.device)
@@ -327,6 +349,7 @@ class FusedDataParallel:
                 ex = H.EmbUpdateParams()
                 src = e.emb_params[p]
                 ex.skeys, ex.svals, ex.n, ex.contrib = src.skeys, src.svals, src.n, src.contrib
+                ex.n_dev, ex.sorted_contrib, ex.chunk_end = src.n_dev, src.sorted_contrib, src.chunk_end
                 ex.K1, ex.Kp, ex.opt, ex.step = e.K1, e.Kp, src.opt, src.step
                 ex.mode = 2
                 ex.grad_scale = 1.0
@@ -563,7 +586,7 @@ class FusedDataParallel:
         self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
-        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and self.world <= SEARCH_MAX_W
+        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and (self.world <= SEARCH_MAX_W or self.range)
         e._build_multi(Smax, heads=self.m_sorted)
         e._m_pool = e.pool_ids
         S_, n = e.mS, e.n_lookup
@@ -581,7 +604,7 @@ class FusedDataParallel:
                     continue
                 da.grads, da.nseg, da.seg_stride = self._recv_ptr, self.world, self.S
                 ex = H.EmbUpdateParams()  # export: compacted (id, Σ grad row) into the send buffer
-                ex.skeys, ex.svals, ex.n = ep.skeys, ep.svals, n
+                ex.skeys, ex.svals, ex.n, ex.n_dev = ep.skeys, ep.svals, n, ep.n_dev
                 ex.val_base, ex.id_offset, ex.sorted_contrib, ex.chunk_end = ep.val_base, ep.id_offset, 1, ep.chunk_end
                 ex.contrib, ex.K1, ex.Kp = e.contrib.data_ptr(), e.K1, e.Kp
                 ex.opt, ex.step = ep.opt, ep.step
@@ -592,6 +615,9 @@ class FusedDataParallel:
                 ex.out_cap = self.cap
                 if self.m_sorted:
                     ex.chunk_heads, ex.nch = e.m_chd[q, k * e.m_nch:].data_ptr(), e.m_nch
+                if self.range:  # + the bucket directory of the exported keys
+                    ex.dir_nb, ex.dir_div = self.nb, self.bdiv
+                    ex.out_dir, ex.push_off_dir = self.send[self.off_dir:].data_ptr(), self.off_dir
                 self._set_push(rows, wp, ex)
                 mg = H.MergeParams()
                 src = self.merge_params[0]
@@ -600,6 +626,9 @@ class FusedDataParallel:
                           "overflow", "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos", "tbl_bf16"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
+                if self.range:
+                    mg.dirs, mg.dir_stride = self._recv_ptr + 4 * self.off_dir, self.S
+                    mg.nb, mg.bucket_div = self.nb, self.bdiv
                 rows.zero_word = self.send[self.off_cnt:].data_ptr()
                 if ed is not None:
                     ed.grad_scale = 1.0  # the merge applied 1/W
@@ -616,7 +645,11 @@ class FusedDataParallel:
             H.deepfm_rows(rows, s)  # (dp: also zeroes the export counter)
             e._tail(wp, ep, None, s)
             self._exchange()
-            if self.mode == "dp" and self.m_sorted:
+            if self.mode == "dp" and self.range:
+                H.merge_range_apply(mg, da, s)  # bucketed row merge ‖ MLP optimizer, one launch
+                if ed is not None:
+                    H.emb_dense_update(ed, s)
+            elif self.mode == "dp" and self.m_sorted:
                 H.merge_search_apply(mg, da, s)  # row merge ‖ MLP optimizer, one launch
                 if ed is not None:
                     H.emb_dense_update(ed, s)

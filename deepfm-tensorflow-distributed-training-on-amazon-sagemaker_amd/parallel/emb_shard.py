@@ -459,7 +459,7 @@ class FusedRowShard:
         self.eng = e = FusedDeepFM(spec_loc, hp, batch_size, dev, embedding_update=embedding_update, seed=seed,
                                    params=P, use_graph=False, fuse_dense_opt=False,
                                    dropout_seed=seed + 7919 * r, compute_dtype=compute_dtype,
-                                   table_dtype=table_dtype)
+                                   table_dtype=table_dtype, dedup=False)  # (rows are routed per owner)
         del P
         e.id_limit = self.V  # the id guard (ROCFM_CHECK_IDS) checks global ids, not local rows
         e._build_fetch()
