@@ -235,7 +235,7 @@ constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
 template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   static_assert(RT == 16 || RT == 8 || RT == 4, "rows per workgroup: 16, 8 or 4");
-  static_assert(RT == 16 || SH::kStatic, "8-row workgroups: compile-time shapes only");
+  static_assert(RT != 4 || SH::kStatic, "4-row workgroups: compile-time shapes only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
   const SH sh(p);
@@ -1208,28 +1208,34 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
       launch_rows_impl<KP4, SH, false, kInfer, false, BT, RT>(p, stream);
     return;
   }
-  launch_rows_impl<KP4, SH, false, kDynamic, true, BT>(p, stream);
+  launch_rows_impl<KP4, SH, false, kDynamic, true, BT, RT>(p, stream);
 }
 
 // rows per workgroup (RowsParams::row_tile, 0 = kDefaultRowTile): 8 doubles the workgroups of a
 // batch (128 instead of 64 at B = 1024 on 256 CUs) at the same per-workgroup weight-fragment
 // traffic — measured 35.9 → 33.3 µs per step in 20-step windows, 33.4 → 32.2 over 200 steps
-// (profiles/r3_row_tile.md); static shapes only (the runtime-shape kernel keeps 16)
+// (profiles/r3_row_tile.md).  The runtime-shape kernel takes 16 or 8 (4 asks for 8 there), and 16
+// with batch norm (its statistics partials are per 16-row workgroup).
 constexpr int kDefaultRowTile = 8;
+static int row_tile_for(const RowsParams& p, bool is_static_shape) {
+  const int rt = p.row_tile ? p.row_tile : kDefaultRowTile;
+  if (is_static_shape) return rt;
+  return p.bn ? 16 : (rt == 4 ? 8 : rt);
+}
 template <int KP4, class SH>
 static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
-  const int rt = SH::kStatic ? (p.row_tile ? p.row_tile : kDefaultRowTile) : 16;
+  const int rt = row_tile_for(p, SH::kStatic);
   if (p.tbl_bf16) {
-    if (rt == 4)
-      launch_rows_t<KP4, SH, true, 4>(p, stream);
-    else if (rt == 8)
+    if constexpr (SH::kStatic)
+      if (rt == 4) return launch_rows_t<KP4, SH, true, 4>(p, stream);
+    if (rt == 8)
       launch_rows_t<KP4, SH, true, 8>(p, stream);
     else
       launch_rows_t<KP4, SH, true, 16>(p, stream);
   } else {
-    if (rt == 4)
-      launch_rows_t<KP4, SH, false, 4>(p, stream);
-    else if (rt == 8)
+    if constexpr (SH::kStatic)
+      if (rt == 4) return launch_rows_t<KP4, SH, false, 4>(p, stream);
+    if (rt == 8)
       launch_rows_t<KP4, SH, false, 8>(p, stream);
     else
       launch_rows_t<KP4, SH, false, 16>(p, stream);
@@ -1267,7 +1273,7 @@ static bool is_static(const RowsParams& p) {
 // Examples per workgroup the launcher will use for these parameters (the per-tile dedup of the side
 // chain must cut the same tiles).
 int deepfm_rows_tile(const RowsParams& p) {
-  return is_static(p) ? (p.row_tile ? p.row_tile : kDefaultRowTile) : kRowTile;
+  return row_tile_for(p, is_static(p));
 }
 
 RowsLds rows_lds_layout_for(const RowsParams& p) {

@@ -121,7 +121,7 @@ class DecodedCache:
         if n == 0:
             raise FileNotFoundError(f"no complete decoded cache at {self.path}")
         B, F = self.B, self.F
-        mm = lambda k, dt, shape: np.memmap(os.path.join(self.path, f"{k}.bin"), dtype=dt, mode="r", shape=shape)
+        mm = lambda k, dt, shape: np.memmap(os.path.join(self.path, f"{k}.bin"), dtype=dt, mode="c", shape=shape)  # copy-on-write: writable views, never written
         return mm("ids", np.int32, (n, B, F)), mm("vals", np.float32, (n, B, F)), mm("labels", np.float32, (n, B))
 
     def groups(self, size: int, hold: int = 2, skip: int = 0, limit: Optional[int] = None,

@@ -430,12 +430,14 @@ def test_device_id_guard(monkeypatch):
         assert torch.isfinite(eng.emb).all()
 
 
-@pytest.mark.parametrize("K,layers,dtype", [(10, [128, 64, 32], "bf16"), (32, [128, 64, 32], "bf16"),
-                                            (10, [128, 64, 32], "fp8"), (10, [64, 32], "bf16")])
-def test_row_tile_8_equals_16(K, layers, dtype, monkeypatch):
+@pytest.mark.parametrize("K,layers,dtype,generic", [(10, [128, 64, 32], "bf16", False), (32, [128, 64, 32], "bf16", False),
+                                                    (10, [128, 64, 32], "fp8", False), (10, [64, 32], "bf16", False),
+                                                    (10, [128, 64, 32], "bf16", True), (32, [256, 128, 64], "bf16", False)])
+def test_row_tile_8_equals_16(K, layers, dtype, generic, monkeypatch):
     """8 or 4 examples per row-kernel workgroup (2× / 4× the workgroups) computes every valid row
     with the same arithmetic as 16 (padding rows of the MFMA tile are zero and never stored): Adam
-    + dropout through multi-step graphs, a batch that is not a multiple of 16 — bitwise equal."""
+    + dropout through multi-step graphs, a batch that is not a multiple of 16 — bitwise equal.
+    The runtime-shape kernel (generic, or the reference's 256-128-64 default) takes 16 and 8."""
     monkeypatch.setenv("ROCFM_DEDUP", "0")  # (dedup groups depend on the row tile: test_dedup_*)
     spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=K, layers=layers,
                      keep_probs=[0.7] * len(layers), l2_reg=1e-3)
@@ -445,16 +447,19 @@ def test_row_tile_8_equals_16(K, layers, dtype, monkeypatch):
     pool = [_batch(B, 39, 3000, g) for _ in range(5)]
     ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
     out = {}
-    for rt in (16, 8, 4):
+    tiles = (16, 8) if (generic or layers[0] > 128) else (16, 8, 4)
+    for rt in tiles:
         monkeypatch.setenv("ROCFM_ROW_TILE", str(rt))
-        e = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=True, compute_dtype=dtype)
+        e = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=True, compute_dtype=dtype,
+                        force_generic_kernels=generic)
+        assert e.H.deepfm_rows_tile(e.rows_params[0]) == rt
         e.attach_pool(ids, vals, labels)
         e.train_steps(13, 4)
         torch.cuda.synchronize()
         e.check()
         out[rt] = (e.emb.clone(), e.dense.clone(), [s.clone() for s in e.emb_slots], e.prob[:B].clone())
     a = out[16]
-    for rt in (8, 4):
+    for rt in tiles[1:]:
         b = out[rt]
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[3], b[3]), rt
         assert all(torch.equal(x, y) for x, y in zip(a[2], b[2])), rt

@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, go):
+def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, bar):
     import torch
 
     torch.set_num_threads(1)
@@ -44,7 +44,7 @@ def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, go):
         src = cache.groups(16, pin_memory=False)
     else:
         src = ds.groups(16, hold=2)
-    go.wait()
+    bar.wait()  # every process starts its timed pass together (cache mode: after its first pass)
     t0 = time.perf_counter()
     n = 0
     for g in src:
@@ -54,13 +54,11 @@ def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, go):
 
 def run(files, procs, threads, B, F, V, mode, cache_dir):
     ctx = mp.get_context("spawn")
-    q, go = ctx.Queue(), ctx.Event()
-    ps = [ctx.Process(target=_worker, args=(files, r, procs, threads, B, F, V, mode, cache_dir, q, go))
+    q, bar = ctx.Queue(), ctx.Barrier(procs)
+    ps = [ctx.Process(target=_worker, args=(files, r, procs, threads, B, F, V, mode, cache_dir, q, bar))
           for r in range(procs)]
     for p in ps:
         p.start()
-    time.sleep(2.0)  # imports + (cache mode) the untimed first pass
-    go.set()
     res = [q.get(timeout=1200) for _ in ps]
     for p in ps:
         p.join()
