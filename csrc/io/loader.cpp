@@ -38,6 +38,7 @@ BatchLoader::BatchLoader(const LoaderOptions& opt) : opt_(opt) {
     throw std::invalid_argument("bad shard spec");
   if (opt_.num_slots < 2) opt_.num_slots = 2;
   if (opt_.num_threads < 1) opt_.num_threads = 1;
+  defer_crc_ = opt_.verify_crc && !opt_.skip_bad && opt_.shard_count > 1 && !opt_.stream_mode;
   slots_.resize(opt_.num_slots);
   slot_state_.assign(opt_.num_slots, 0);
   slot_seq_.resize(opt_.num_slots);
@@ -178,8 +179,8 @@ size_t resync(const uint8_t* buf, size_t n, size_t from, size_t limit) {
 // back to the sequential scan_records, which also produces the reference error semantics.
 // TFRecord framing is a length chain; a single thread walking it is bound by one memory latency
 // per record (≈70-90 ns), i.e. it cannot feed more than ≈12 M records/s.
-bool index_parallel(const uint8_t* buf, size_t n, bool verify, bool skip_bad, int parts, std::vector<RecordRef>* out,
-                    size_t* bad) {
+bool index_parallel(const uint8_t* buf, size_t n, bool verify, bool verify_data, bool skip_bad, int parts,
+                    std::vector<RecordRef>* out, size_t* bad) {
   struct Part {
     size_t first = 0, end = 0, bad = 0;
     bool error = false;
@@ -204,7 +205,7 @@ bool index_parallel(const uint8_t* buf, size_t n, bool verify, bool skip_bad, in
       }
       const uint8_t* payload = buf + p + 12;
       bool ok = true;
-      if (verify) {
+      if (verify && verify_data) {
         uint32_t dcrc;
         memcpy(&dcrc, payload + len, 4);
         ok = mask_crc(crc32c(payload, len)) == dcrc;
@@ -260,16 +261,20 @@ void BatchLoader::reader_main() {
       size_t bad = 0;
     };
     const int parts = std::max(1, opt_.num_threads);
-    auto index = [this, parts](const std::string& path) {
+    // deferred data CRCs (defer_crc_, see loader.h): the walk checks the framing (length CRCs)
+    // only; each kept record's data CRC is checked by the decoder that decodes it
+    const bool vdata = !defer_crc_;
+    auto index = [this, parts, vdata](const std::string& path) {
       Indexed ix;
       ix.chunk = map_file(path);
       const size_t n = ix.chunk->size;
       const int np = (int)std::min<size_t>((size_t)parts, std::max<size_t>(1, n >> 22));
-      if (np < 2 || !index_parallel(ix.chunk->data, n, opt_.verify_crc, opt_.skip_bad, np, &ix.recs, &ix.bad)) {
+      if (np < 2 ||
+          !index_parallel(ix.chunk->data, n, opt_.verify_crc, vdata, opt_.skip_bad, np, &ix.recs, &ix.bad)) {
         if (np >= 2) ++fallbacks_;
         ix.recs.clear();
         ix.bad = 0;
-        scan_records(ix.chunk->data, n, opt_.verify_crc, opt_.skip_bad, &ix.recs, &ix.bad);
+        scan_records(ix.chunk->data, n, opt_.verify_crc, opt_.skip_bad, &ix.recs, &ix.bad, vdata);
       }
       return ix;
     };
@@ -393,6 +398,15 @@ void BatchLoader::worker_main() {
     int n = (int)job.recs.size();
     std::string err;
     for (int r = 0; r < n; ++r) {
+      if (defer_crc_) {
+        uint32_t dcrc;
+        memcpy(&dcrc, job.recs[r].data + job.recs[r].len, 4);
+        if (mask_crc(crc32c(job.recs[r].data, job.recs[r].len)) != dcrc) {
+          err = std::string("TFRecord: corrupt data CRC in batch ") + std::to_string(job.seq) + " record " +
+                std::to_string(r);
+          break;
+        }
+      }
       int st = decode_example(job.recs[r].data, job.recs[r].len, opt_.schema, s.labels + r,
                               s.ids + (size_t)r * F, s.vals + (size_t)r * F, opt_.max_id);
       if (st != kOk) {

@@ -8,6 +8,12 @@
 //                   shuffle buffer → cut batches of batch_size (tail dropped per epoch when
 //                   drop_remainder) → job queue
 //   N workers     : decode a job's records straight into output slot (seq % num_slots)
+// A sharded loader (shard_count > 1, verify_crc, no skip_bad) checks only the framing in the walk
+// and leaves each record's data CRC to the worker that decodes it: every rank walks the whole
+// file list (record-index sharding), so a full-CRC walk made P ranks checksum every byte P times
+// and stopped the aggregate decode rate scaling with the rank count (profiles/r3_loader_aggregate.md).
+// A corrupt record still fails the job, on the rank whose shard holds it.  skip_bad keeps the full
+// walk: dropping a bad record there shifts the record index every rank shards by.
 //   consumer      : next() returns slots strictly in sequence order; release() recycles them.
 // Output slots are caller-provided host buffers (Python passes pinned torch tensors so the H2D copy
 // is a true async DMA on a side HIP stream).
@@ -101,6 +107,7 @@ class BatchLoader {
   std::vector<std::thread> workers_;
   std::atomic<size_t> bad_{0}, seen_{0}, fallbacks_{0};
   bool started_ = false;
+  bool defer_crc_ = false;  // data CRCs checked by the decoders (see the header comment)
 };
 
 // Decode an entire TFRecord file (small files: validation sets, tests).

@@ -328,7 +328,7 @@ void frame_record(const uint8_t* payload, size_t n, std::string* out) {
 }
 
 size_t scan_records(const uint8_t* buf, size_t n, bool verify_crc, bool skip_bad, std::vector<RecordRef>* out,
-                    size_t* bad_records) {
+                    size_t* bad_records, bool verify_data) {
   size_t off = 0, cnt = 0;
   while (off + 12 <= n) {
     uint64_t len;
@@ -353,7 +353,7 @@ size_t scan_records(const uint8_t* buf, size_t n, bool verify_crc, bool skip_bad
     }
     const uint8_t* payload = buf + off + 12;
     bool ok = true;
-    if (verify_crc) {
+    if (verify_crc && verify_data) {
       uint32_t dcrc;
       memcpy(&dcrc, payload + len, 4);
       ok = mask_crc(crc32c(payload, len)) == dcrc;

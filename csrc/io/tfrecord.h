@@ -57,8 +57,9 @@ struct RecordRef {
   const uint8_t* data;
   uint32_t len;
 };
+// verify_data = false checks the framing only (length CRCs); the caller then owns the data CRCs.
 size_t scan_records(const uint8_t* buf, size_t n, bool verify_crc, bool skip_bad, std::vector<RecordRef>* out,
-                    size_t* bad_records);
+                    size_t* bad_records, bool verify_data = true);
 
 }  // namespace io
 }  // namespace rocfm

@@ -123,6 +123,11 @@ class Config:
     profile_steps: str = ""  # "a:b" — wrap steps [a,b) with torch.profiler / roctx ranges
     metrics_file: str = ""  # JSONL metrics output
     tensorboard: bool = True  # chief writes TF event files: model_dir (train) and model_dir/eval (utils/tensorboard.py)
+    # training-data sharding over ranks: "record" = Dataset.shard (every count-th record of the
+    # concatenated file list, the reference's semantics — every rank walks every file's framing);
+    # "file" = each rank reads files[index::count] only (like SageMaker's ShardedByS3Key input,
+    # README:87-92), so P ranks walk each byte once; needs at least `count` files
+    shard_policy: str = "record"
     crc_check: bool = True  # verify TFRecord CRCs
     on_bad_record: str = "fail"  # fail | skip
     max_steps: int = 0  # 0 → run num_epochs
@@ -176,6 +181,8 @@ class Config:
             raise ValueError(f"unknown optimizer {self.optimizer!r}")
         if self.loss_type not in ("log_loss", "square_loss"):
             raise ValueError(f"unknown loss_type {self.loss_type!r}")
+        if self.shard_policy not in ("record", "file"):
+            raise ValueError("shard_policy must be record or file")
         if self.dp_exchange not in ("auto", "p2p", "rccl"):
             raise ValueError(f"unknown dp_exchange {self.dp_exchange!r}")
         if self.task_type not in ("train", "eval", "infer", "export"):

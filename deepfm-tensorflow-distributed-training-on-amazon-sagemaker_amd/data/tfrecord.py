@@ -154,14 +154,27 @@ class TFRecordDataset:
     copy followed by using the device tensor) before advancing the iterator twice.  ``hold=h``
     delays the recycling: a batch's slot is released when batch t+h is requested (consumers that
     keep ``h`` asynchronous copies in flight; the pool grows to keep 4 slots for the decoders).
+
+    ``shard_policy="file"`` shards by file instead of by record: shard i reads ``files[i::count]``
+    (needs ≥ count files), so the ranks of one host walk each byte once instead of every rank walking
+    every file's framing (``profiles/r3_loader_aggregate.md``).
     """
 
     def __init__(self, files: Sequence[str], field_size: int, batch_size: int, feature_size: int = 0,
                  num_epochs: int = 1, shard_count: int = 1, shard_index: int = 0, drop_remainder: bool = True,
                  num_threads: int = 4, num_slots: int = 6, verify_crc: bool = True, skip_bad: bool = False,
                  shuffle_buffer: int = 0, seed: int = 0, stream_mode: bool = False, pin_memory: Optional[bool] = None,
-                 hold: int = 1):
+                 hold: int = 1, shard_policy: str = "record"):
         self.files = list(files)
+        if shard_policy not in ("record", "file"):
+            raise ValueError(f"shard_policy must be record or file, got {shard_policy!r}")
+        if shard_policy == "file" and int(shard_count) > 1:
+            if stream_mode:
+                raise ValueError("shard_policy=file: file mode only (a pipe-mode channel is one stream)")
+            if len(self.files) < int(shard_count):
+                raise ValueError(f"shard_policy=file needs at least {shard_count} files, got {len(self.files)}")
+            self.files = self.files[int(shard_index)::int(shard_count)]
+            shard_count, shard_index = 1, 0
         self.F = int(field_size)
         self.B = int(batch_size)
         self.hold = max(1, int(hold))

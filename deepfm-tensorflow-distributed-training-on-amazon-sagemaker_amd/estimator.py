@@ -147,6 +147,7 @@ class Estimator:
                                skip_bad=cfg.on_bad_record == "skip",
                                shuffle_buffer=(cfg.batch_size * 8 if (training and cfg.perform_shuffle) else 0),
                                seed=cfg.seed + self.info.rank, stream_mode=bool(cfg.pipe_mode),
+                               shard_policy=cfg.shard_policy if training else "record",
                                hold=2)  # _device_batches syncs batch t's H2D copy while t+1 is current
 
     def _host_batches(self, ds: Iterable):

@@ -204,6 +204,54 @@ def test_parallel_index_corruption_falls_back_to_sequential_semantics(tmp_path):
     assert np.array_equal(torch.cat([g[0] for g in got]).numpy(), keep)
 
 
+@pytest.mark.parametrize("threads", [1, 4])
+def test_sharded_loader_checks_data_crc_of_its_own_records(tmp_path, threads):
+    """Sharded loaders walk the framing only and leave data CRCs to the decoders of the records they
+    keep (loader.h): a corrupt record fails the rank whose shard holds it and no other; skip_bad
+    keeps the full-walk semantics (the bad record is dropped before sharding)."""
+    p, labels, ids, vals = _big(tmp_path)
+    data = bytearray(open(p, "rb").read())
+    off, k = 0, 0
+    while k < 12345:
+        (n,) = struct.unpack("<Q", data[off:off + 8])
+        off += 12 + n + 4
+        k += 1
+    data[off + 12 + 3] ^= 0xFF  # record k's payload
+    open(p, "wb").write(bytes(data))
+    for r in range(3):
+        ds = T.TFRecordDataset([p], 39, 1000, shard_count=3, shard_index=r, num_threads=threads, pin_memory=False)
+        if r == k % 3:
+            with pytest.raises(RuntimeError, match="corrupt data CRC"):
+                _collect(ds)
+        else:
+            got = torch.cat([g[0] for g in _collect(ds)]).numpy()
+            assert np.array_equal(got, ids[r::3][: len(got)]) and len(got) == (len(ids[r::3]) // 1000) * 1000
+    keep = np.delete(ids, k, axis=0)
+    for r in range(3):
+        ds = T.TFRecordDataset([p], 39, 1000, shard_count=3, shard_index=r, num_threads=threads, skip_bad=True,
+                               drop_remainder=False, pin_memory=False)
+        got = torch.cat([g[0] for g in _collect(ds)]).numpy()
+        assert np.array_equal(got, keep[r::3]) and ds.bad_records == 1
+
+
+def test_file_shard_policy(tmp_path):
+    files, per = [], []
+    for i in range(5):
+        f = str(tmp_path / f"tr{i}.tfrecords")
+        per.append(_write(f, 40 + 8 * i, seed=30 + i)[1])
+        files.append(f)
+    for r in range(2):
+        ds = T.TFRecordDataset(files, 5, 8, shard_count=2, shard_index=r, shard_policy="file", pin_memory=False)
+        got = torch.cat([b[0] for b in _collect(ds)]).numpy()
+        want = np.concatenate(per[r::2])
+        assert np.array_equal(got, want[: len(want) // 8 * 8])
+    with pytest.raises(ValueError, match="at least 6 files"):
+        T.TFRecordDataset(files, 5, 8, shard_count=6, shard_index=0, shard_policy="file")
+    from rocfm.config import Config
+    with pytest.raises(ValueError, match="shard_policy"):
+        Config(shard_policy="bytes", field_size=39, feature_size=100).validate()
+
+
 def test_groups_match_batches_skip_limit_tail(tmp_path):
     p = str(tmp_path / "g.tfrecords")
     _, ids, _ = _write(p, 1000, seed=6)

@@ -26,14 +26,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, bar):
+def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, bar, policy):
     import torch
 
     torch.set_num_threads(1)
     from rocfm.data.tfrecord import TFRecordDataset
 
     ds = TFRecordDataset(files, F, B, V, shard_count=procs, shard_index=rank, num_threads=threads,
-                         verify_crc=True, pin_memory=False, hold=2)
+                         verify_crc=True, pin_memory=False, hold=2, shard_policy=policy)
     if mode == "cache":
         from rocfm.data.cache import DecodedCache
 
@@ -52,10 +52,10 @@ def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, bar):
     q.put((rank, n * B, time.perf_counter() - t0))
 
 
-def run(files, procs, threads, B, F, V, mode, cache_dir):
+def run(files, procs, threads, B, F, V, mode, cache_dir, policy):
     ctx = mp.get_context("spawn")
     q, bar = ctx.Queue(), ctx.Barrier(procs)
-    ps = [ctx.Process(target=_worker, args=(files, r, procs, threads, B, F, V, mode, cache_dir, q, bar))
+    ps = [ctx.Process(target=_worker, args=(files, r, procs, threads, B, F, V, mode, cache_dir, q, bar, policy))
           for r in range(procs)]
     for p in ps:
         p.start()
@@ -64,7 +64,7 @@ def run(files, procs, threads, B, F, V, mode, cache_dir):
         p.join()
     ex = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
-    return {"mode": mode, "procs": procs, "threads_per_proc": threads, "examples": ex,
+    return {"mode": mode, "shard_policy": policy, "procs": procs, "threads_per_proc": threads, "examples": ex,
             "aggregate_examples_per_sec": round(ex / wall, 1),
             "per_proc_examples_per_sec": [round(r[1] / r[2], 1) for r in sorted(res)]}
 
@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--batch_size", type=int, default=1024)
     ap.add_argument("--feature_size", type=int, default=1_000_000)
     ap.add_argument("--modes", default="tfrecord,cache")
+    ap.add_argument("--shard_policy", default="record,file", help="record (Dataset.shard) and/or file")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     from rocfm.data.synthetic import write_synthetic_tfrecord
@@ -92,11 +93,14 @@ def main():
             files.append(p)
         out = {"host_cpus": os.cpu_count(), "records": per * a.files, "results": []}
         for mode in a.modes.split(","):
-            for P in (int(x) for x in a.procs.split(",")):
-                cache_dir = os.path.join(d, f"cache_{P}")
-                r = run(files, P, a.threads, a.batch_size, 39, a.feature_size, mode, cache_dir)
-                out["results"].append(r)
-                print(json.dumps(r), flush=True)
+            for pol in a.shard_policy.split(","):
+                if mode == "cache" and pol == "file":
+                    continue  # the cache reads only its own shard either way
+                for P in (int(x) for x in a.procs.split(",")):
+                    cache_dir = os.path.join(d, f"cache_{P}")
+                    r = run(files, P, a.threads, a.batch_size, 39, a.feature_size, mode, cache_dir, pol)
+                    out["results"].append(r)
+                    print(json.dumps(r), flush=True)
         if a.json:
             with open(a.json, "w") as f:
                 json.dump(out, f, indent=1)
