@@ -34,6 +34,7 @@ import torch
 
 from ..optim import OPT_ID, OptHParams, init_slots, slot_names
 from ..ops import require_hip
+from ..utils import hazard
 from .deepfm import ModelSpec, init_params, mlp_names
 
 
@@ -117,6 +118,12 @@ class FusedDeepFM:
         if len(spec.layers) > 6:
             raise ValueError("the fused engine supports at most 6 hidden layers")
         self.H = require_hip()
+        # ROCFM_HAZARD=1: launches recorded, each new side/main graph pair checked for shared buffers
+        self._hazard = None
+        if hazard.enabled():
+            self._hazard = hazard.Recorder()
+            self._hazard.attach("eng", self)
+            self.H = hazard.HipProxy(self.H, self._hazard)
         self.spec, self.hp = spec, hp
         self.device = torch.device(device)
         self.B = int(batch_size)
@@ -864,14 +871,25 @@ class FusedDeepFM:
             if gm is None:
                 torch.cuda.synchronize(self.device)
                 gs, gm = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                rec = self._hazard
+                if rec is not None:
+                    rec.begin("side")
                 with torch.cuda.graph(gs, capture_error_mode=capture_error_mode):
                     self._prepare_multi(q, S, torch.cuda.current_stream(self.device))
+                if rec is not None:
+                    rec.begin("main")
                 with torch.cuda.graph(gm, capture_error_mode=capture_error_mode):
                     body(q, S)
+                if rec is not None:
+                    rec.end()
+                    rec.check(f"{key + (q, S)}")  # before the pair ever runs
                 graphs[key + (q, S, "side")], graphs[key + (q, S, "main")] = gs, gm
         if capture_only:
             return
         if eager:
+            rec = self._hazard
+            if rec is not None:
+                rec.begin("side")
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 self._prepare_multi(q, S, side)
@@ -879,7 +897,12 @@ class FusedDeepFM:
             ev.record(side)
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
+            if rec is not None:
+                rec.begin("main")
             body(q, S)
+            if rec is not None:
+                rec.end()
+                rec.check(f"eager {key + (q, S)}")
         else:
             # main graph submitted first: its kernels start while the host is still submitting the
             # side graph (a timed window otherwise begins with the side graph's whole submission);

@@ -267,6 +267,8 @@ class FusedDataParallel:
                                dropout_seed=seed + 7919 * self.rank, compute_dtype=compute_dtype,
                                table_dtype=table_dtype)
         e = self.eng
+        if e._hazard is not None:  # ROCFM_HAZARD=1: this driver's buffers join the checked set
+            e._hazard.attach("dp", self)
         self.use_graph = use_graph
         self.graph_collectives = use_graph and collectives_capturable()
         self.check_every = int(check_every)

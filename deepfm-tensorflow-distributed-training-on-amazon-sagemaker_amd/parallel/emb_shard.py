@@ -463,6 +463,8 @@ class FusedRowShard:
         del P
         e.id_limit = self.V  # the id guard (ROCFM_CHECK_IDS) checks global ids, not local rows
         e._build_fetch()
+        if e._hazard is not None:  # ROCFM_HAZARD=1: this driver's buffers join the checked set
+            e._hazard.attach("rs", self)
         self.H, self.device, self.embedding_update = e.H, e.device, embedding_update
         self.use_graph, self.check_every = use_graph, int(check_every)
         from .dp import collectives_capturable

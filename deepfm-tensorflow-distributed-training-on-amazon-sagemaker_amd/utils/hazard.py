@@ -1,0 +1,234 @@
+"""Cross-stream hazard checker for the two-graph multi-step launches (``ROCFM_HAZARD=1``).
+
+Every multi-step launch is a side graph (the next group's fetch, sort, sort aux, dedup; the
+row-shard routing) on the sort stream, running concurrently with the main graph (the steps and,
+distributed, the exchanges and merges) on the compute stream (``FusedDeepFM._launch_multi``).  The
+two share no buffer by construction: the side graph fills the parity 1-q buffers while the main
+graph consumes parity q.  Nothing enforces that, however — a buffer added to both chains without a
+parity index is a race that shows up only as rare run-to-run differences.
+
+With ``ROCFM_HAZARD=1`` the engine's extension handle is wrapped: every launcher call records the
+device buffers its arguments point into, with their role, and each newly captured graph pair is
+checked before it ever runs:
+
+* a parameter block's pointer fields are read by name, with the role from the field's declared type
+  in ``csrc/bindings.inc`` (``ROCFM_PTR(cls, field, const T*)`` = read, a non-const pointer = write);
+* the block's raw bytes (``.raw()``) are scanned for further pointers — arrays set through the
+  ``set_*`` methods (layer weights, activations, peer slots) — which count as writes (unknown role);
+* plain integer arguments that point into a known buffer (the sort launchers) count as writes.
+
+Pointers are resolved against every CUDA tensor reachable from the registered roots (the engine, and
+the DP / row-shard driver): attributes, and lists / tuples / dicts of tensors.  An access covers its
+tensor from its base pointer up to the next base pointer any recorded access uses inside the same
+tensor (so per-parity slices of one allocation stay apart).  Two accesses, one from each graph, that
+overlap with at least one write are a hazard: ``HazardError`` names both launches, fields and the
+buffer.  Torch ops and collectives inside a capture are not recorded (the HIP-extension launches only).
+"""
+from __future__ import annotations
+
+import bisect
+import os
+import re
+from collections import defaultdict
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_BINDINGS = os.path.join(_ROOT, "csrc", "bindings.inc")
+_PTR_RE = re.compile(r"ROCFM_PTR\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([^)]*)\)")
+
+
+class HazardError(RuntimeError):
+    pass
+
+
+def enabled() -> bool:
+    return os.environ.get("ROCFM_HAZARD", "0") == "1"
+
+
+_roles_cache: Optional[Dict[str, Dict[str, bool]]] = None
+
+
+def pointer_roles(path: str = _BINDINGS) -> Dict[str, Dict[str, bool]]:
+    """class name → {pointer field → writable} from the ROCFM_PTR declarations."""
+    global _roles_cache
+    if _roles_cache is not None and path == _BINDINGS:
+        return _roles_cache
+    roles: Dict[str, Dict[str, bool]] = defaultdict(dict)
+    with open(path) as f:
+        text = f.read()
+    for cls, field, typ in _PTR_RE.findall(text):
+        if cls == "cls":  # the macro's own definition
+            continue
+        roles[cls][field] = not typ.strip().startswith("const")
+    out = dict(roles)
+    if path == _BINDINGS:
+        _roles_cache = out
+    return out
+
+
+class Access:
+    __slots__ = ("section", "kernel", "field", "owner", "base", "write")
+
+    def __init__(self, section, kernel, field, owner, base, write):
+        self.section, self.kernel, self.field, self.owner, self.base, self.write = (
+            section, kernel, field, owner, base, write)
+
+    def __repr__(self):
+        return f"{self.kernel}.{self.field} {'W' if self.write else 'R'} {self.owner}+{self.base}"
+
+
+class TensorMap:
+    """Address → the registered tensor storage holding it.  Accesses are grouped by the OUTERMOST
+    registered range (the allocation) so that views kept as attributes compare with their base."""
+
+    def __init__(self):
+        self._items: List[Tuple[int, int, str]] = []
+
+    def add(self, name: str, t: torch.Tensor) -> None:
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda" or t.numel() == 0:
+            return
+        lo = t.data_ptr()
+        self._items.append((lo, lo + t.numel() * t.element_size(), name))
+
+    def lookup(self, ptr: int) -> Optional[Tuple[int, int, str]]:
+        """(allocation start, allocation end, name) of the outermost registered range with ptr."""
+        best = None
+        for lo, hi, name in self._items:
+            if lo <= ptr < hi and (best is None or hi - lo > best[1] - best[0]):
+                best = (lo, hi, name)
+        return best
+
+    @classmethod
+    def from_roots(cls, roots) -> "TensorMap":
+        m = cls()
+        for prefix, obj in roots:
+            for k, v in vars(obj).items():
+                _add_obj(m, f"{prefix}.{k}", v, 2)
+        return m
+
+
+def _add_obj(m: TensorMap, name: str, v, depth: int) -> None:
+    if isinstance(v, torch.Tensor):
+        m.add(name, v)
+    elif depth > 0 and isinstance(v, (list, tuple)):
+        for i, x in enumerate(v):
+            _add_obj(m, f"{name}[{i}]", x, depth - 1)
+    elif depth > 0 and isinstance(v, dict):
+        for k, x in v.items():
+            _add_obj(m, f"{name}[{k!r}]", x, depth - 1)
+
+
+class Recorder:
+    """Collects the launches of the current section ("side" / "main") per graph pair."""
+
+    def __init__(self):
+        self.roots: List[Tuple[str, object]] = []
+        self.section: Optional[str] = None
+        self.calls: Dict[str, List[Tuple[str, tuple]]] = defaultdict(list)
+        self.checked = 0
+
+    def attach(self, prefix: str, obj) -> None:
+        self.roots.append((prefix, obj))
+
+    def begin(self, section: str) -> None:
+        self.section = section
+        self.calls[section] = []
+
+    def end(self) -> None:
+        self.section = None
+
+    def note(self, name: str, args: tuple) -> None:
+        if self.section is not None:
+            self.calls[self.section].append((name, args))
+
+    # ---- analysis -------------------------------------------------------------------------------
+    def accesses(self, section: str, tmap: TensorMap) -> List[Access]:
+        roles = pointer_roles()
+        out = []
+        for kernel, args in self.calls.get(section, []):
+            for ai, a in enumerate(args):
+                if hasattr(a, "raw"):
+                    named = roles.get(type(a).__name__, {})
+                    seen = set()
+                    for field, w in named.items():
+                        v = int(getattr(a, field))
+                        if v:
+                            seen.add(v)
+                            hit = tmap.lookup(v)
+                            if hit:
+                                out.append(Access(section, kernel, field, hit[2], v - hit[0], w))
+                    raw = a.raw()
+                    for off in range(0, len(raw) - 7, 8):
+                        v = int.from_bytes(raw[off:off + 8], "little")
+                        if v and v not in seen:
+                            hit = tmap.lookup(v)
+                            if hit:
+                                seen.add(v)
+                                out.append(Access(section, kernel, f"@{off}", hit[2], v - hit[0], True))
+                elif isinstance(a, int) and not isinstance(a, bool) and a > 65536:
+                    hit = tmap.lookup(a)
+                    if hit:
+                        out.append(Access(section, kernel, f"arg{ai}", hit[2], a - hit[0], True))
+        return out
+
+    def check(self, tag: str = "") -> None:
+        """Raise HazardError when the recorded side and main sections conflict."""
+        tmap = TensorMap.from_roots(self.roots)
+        side, main = self.accesses("side", tmap), self.accesses("main", tmap)
+        found = conflicts(side, main, tmap)
+        self.checked += 1
+        if found:
+            lines = [f"  {a!r}  <->  {b!r}" for a, b in found[:20]]
+            raise HazardError(f"side/main graph hazard{(' in ' + tag) if tag else ''}: {len(found)} overlapping "
+                              "accesses with a write:\n" + "\n".join(lines))
+
+
+def conflicts(xs: List[Access], ys: List[Access], tmap: Optional[TensorMap] = None) -> List[Tuple[Access, Access]]:
+    """Pairs (x, y) whose extents overlap inside one tensor, at least one a write.  An access's
+    extent runs from its base to the next base any access uses in the same tensor."""
+    bases: Dict[str, List[int]] = defaultdict(list)
+    for a in xs + ys:
+        bases[a.owner].append(a.base)
+    for k in bases:
+        bases[k] = sorted(set(bases[k]))
+
+    def extent(a: Access) -> Tuple[int, int]:
+        b = bases[a.owner]
+        i = bisect.bisect_right(b, a.base)
+        return a.base, (b[i] if i < len(b) else 1 << 62)
+
+    out = []
+    by_owner = defaultdict(list)
+    for y in ys:
+        by_owner[y.owner].append(y)
+    for x in xs:
+        ex = extent(x)
+        for y in by_owner.get(x.owner, ()):
+            if not (x.write or y.write):
+                continue
+            ey = extent(y)
+            if ex[0] < ey[1] and ey[0] < ex[1]:
+                out.append((x, y))
+    return out
+
+
+class HipProxy:
+    """The extension module with every launcher call noted by ``rec`` (classes pass through)."""
+
+    def __init__(self, mod, rec: Recorder):
+        object.__setattr__(self, "_mod", mod)
+        object.__setattr__(self, "_rec", rec)
+
+    def __getattr__(self, name):
+        attr = getattr(self._mod, name)
+        if isinstance(attr, type) or not callable(attr):
+            return attr
+        rec = self._rec
+
+        def call(*args, **kwargs):
+            rec.note(name, tuple(args) + tuple(kwargs.values()))
+            return attr(*args, **kwargs)
+
+        return call
