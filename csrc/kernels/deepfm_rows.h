@@ -10,8 +10,26 @@ constexpr int kMaxHidden = 6;  // hidden MLP layers supported by the fused engin
 constexpr int kRowTile = 16;   // rows per workgroup = one 16-row MFMA M tile
 constexpr int kRowThreads = 512;  // 8 waves
 
+// compute_dtype=fp8: pre-quantised fp8-e4m3 copies of the input layer's weights, written by every
+// weight refresh (wgrad epilogue, dense apply) next to the bf16 swizzled copies, with ONE scale per
+// tensor taken from the previous weights' max |w| (delayed scaling: the refresh cannot know the
+// new weights' max before it has written them).  Step s's refresh quantises with amax[s & 1] and
+// accumulates the max of the weights it writes into amax[(s + 1) & 1], which step s's row kernel
+// zeroed; a host refresh (track = 0) presets both slots to the exact max.  inv_scale = amax / 448
+// of the copies' current quantisation: the row kernel's de-scale.
+constexpr float kFp8Max = 448.f;  // largest finite e4m3fn
+struct Fp8W0 {
+  uint8_t* f = nullptr;  // frag_swz(o, i, dims[0]) like WTs[0]
+  uint8_t* b = nullptr;  // frag_swz(i, o, dims[1]) like Wbs[0]
+  float* amax = nullptr;       // [2]
+  float* inv_scale = nullptr;  // [1]
+  int track = 0;
+};
+
 struct RowsLds {  // byte offsets into dynamic LDS (all multiples of 16)
   int ids, vals, wx, S, ylin, g, act[kMaxHidden + 1], dzA, dzB, f32, pos, amax;
+  int q8, ldq;          // fp8: the input layer's forward A operand (h0) quantised once per tile in
+                        // phase B, [16][ldq] e4m3 bytes
   int nxt, gr;          // dedup: int [16·F] next member of each lookup's group; f32 [16·F][Kp] gradient rows
   int bnr[kMaxHidden];  // batch_norm: f32 [16][dims[l+1]] post-ReLU values r of layer l (kept for backward)
   int bnst[kMaxHidden]; // batch_norm: f32 [2][dims[l+1]] batch mean, 1/sqrt(var + eps) of layer l
@@ -84,6 +102,8 @@ struct RowsParams {
   // phase F sums every group's gradient rows in LDS (lookup order) and writes ONE row per group
   int dedup;
   const int32_t* contrib_nxt;
+  Fp8W0 w8;  // fp8 kernels: the pre-quantised input-layer weights (the kernel reads f, b, inv_scale
+             // and, training, zeroes amax[(step + 1) & 1])
 };
 
 struct WgradParams {
@@ -113,6 +133,7 @@ struct WgradParams {
   int bn_dmax;
   int off_gamma[kMaxHidden], off_beta[kMaxHidden];
   PushTarget push;  // DP fused push (fuse_opt == 0): gradients go straight into the W receive slots
+  Fp8W0 w8;         // fused optimizer: refresh the fp8 input-layer copies too (f == nullptr: none)
 };
 
 struct DenseApplyParams {
@@ -134,6 +155,7 @@ struct DenseApplyParams {
   float grad_scale;
   int nseg;                // > 1: grads are nseg rank segments (DP all-gather), summed in rank order
   long long seg_stride;    // floats between segments
+  Fp8W0 w8;                // refresh the fp8 input-layer copies too (f == nullptr: none)
 };
 
 }  // namespace rocfm

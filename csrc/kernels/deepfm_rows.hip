@@ -32,6 +32,23 @@ namespace rocfm {
 namespace {
 
 __device__ __forceinline__ bf16x8 ld_frag(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// Input-layer weight fragments: bf16x8 from the swizzled bf16 copy, or (FP8) the 8 pre-quantised
+// e4m3 bytes at the same element offset of the fp8 copy (deepfm_rows.h Fp8W0) — one MFMA operand.
+template <bool FP8>
+struct W0Frag {
+  using type = bf16x8;
+};
+template <>
+struct W0Frag<true> {
+  using type = long;
+};
+template <bool FP8>
+__device__ __forceinline__ typename W0Frag<FP8>::type ld_w0(const uint16_t* bf, const uint8_t* f8, size_t off) {
+  if constexpr (FP8)
+    return *reinterpret_cast<const long*>(f8 + off);
+  else
+    return ld_frag(bf + off);
+}
 
 // fp8 (OCP e4m3fn, gfx950) quantisation of 8 bf16 values scaled by s into one MFMA operand
 // (byte j = element j; round-to-nearest-even conversion).
@@ -43,12 +60,6 @@ __device__ __forceinline__ long quant_fp8x8(bf16x8 v, float s) {
   hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((uint16_t)v[6]) * s, bf2f((uint16_t)v[7]) * s, hi, true);
   return (long)(uint32_t)lo | ((long)(uint32_t)hi << 32);
 }
-__device__ __forceinline__ float absmax_bf16x8(bf16x8 v, float m) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f((uint16_t)v[j])));
-  return m;
-}
-constexpr float kFp8Max = 448.f;  // largest finite e4m3fn
 
 __device__ __forceinline__ uint32_t pick4(const Philox4& b, int i) {
   return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
@@ -267,11 +278,15 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   ROWS_STAMP(0);
   if (p.zero_word != nullptr && blockIdx.x == 0 && t == 0) *p.zero_word = 0;
+  // fp8: de-scale of the pre-quantised input-layer weights; training zeroes the slot this step's
+  // weight refresh accumulates the new max into (deepfm_rows.h Fp8W0)
+  const float w8inv = FP8 ? *p.w8.inv_scale : 0.f;
+  if (FP8 && train && blockIdx.x == 0 && t == 0) p.w8.amax[((p.step ? *p.step : 0) + 1) & 1] = 0.f;
 
   // ---- phase 0: stage ids / values and every small parameter the later phases read -----------
   // The ids are the head of the kernel's latency chain (ids → gathered rows): their loads are
   // issued first; the layer-0 weight prefetch is issued behind them and lands during phase A.
-  bf16x8 fw0[SH::KSF0];
+  typename W0Frag<FP8>::type fw0[SH::KSF0];
   if constexpr (SH::kStatic) {
     // every load unconditional (clamped index, value selected afterwards): no exec branches in
     // the memory-op stream (see MODE above); the kernarg pointers are read up front
@@ -304,7 +319,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float bo = *p.b_out, fb = *p.fm_bias;
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-    for (int u = 0; u < SH::KSF0E; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
+    for (int u = 0; u < SH::KSF0E; ++u) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nt, u, sh.dim(0), lane));
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       const int i = t + u * kRowThreads;
@@ -405,6 +420,13 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         const int r = RT + i / (lda / 8), c8 = i - (r - RT) * (lda / 8);
         *reinterpret_cast<uint4*>(h0 + r * lda + 8 * c8) = make_uint4(0u, 0u, 0u, 0u);
       }
+      if constexpr (FP8 && SH::kStatic) {
+        uint8_t* q8 = reinterpret_cast<uint8_t*>(smem + L.q8);
+        for (int i = t; i < (kRowTile - RT) * (SH::D0 / 8); i += kRowThreads) {
+          const int r = RT + i / (SH::D0 / 8), c8 = i - (r - RT) * (SH::D0 / 8);
+          *reinterpret_cast<long*>(q8 + r * L.ldq + 8 * c8) = 0;
+        }
+      }
     }
   }
   lds_barrier();
@@ -413,7 +435,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if constexpr (SH::kStatic && SH::KSF0E < SH::KSF0) {  // the rest of layer 0's forward fragments
     const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-    for (int u = SH::KSF0E; u < SH::KSF0; ++u) fw0[u] = ld_frag(p.WTs[0] + frag_at(nt, u, sh.dim(0), lane));
+    for (int u = SH::KSF0E; u < SH::KSF0; ++u) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nt, u, sh.dim(0), lane));
   }
 
   // ---- phase B: FM second order + first order (32 lanes per row) ------------------------------
@@ -459,10 +481,18 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         cterm += S * S - Q;
       }
     }
-    if (FP8) {  // row max |bf16(e)| = bf16(max |e|) (rounding is monotonic)
+    if constexpr (FP8) {  // row max |bf16(e)| = bf16(max |e|) (rounding is monotonic)
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o, 64));
-      if (q == 0) s_amax[r] = bf2f(f2bf(amx));
+      amx = bf2f(f2bf(amx));
+      if (q == 0) s_amax[r] = amx;
+      if constexpr (SH::kStatic) {  // this row's h0 → e4m3 (the layer-0 A operand), by its own lanes
+        const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
+        uint8_t* q8 = reinterpret_cast<uint8_t*>(smem + L.q8);
+        const float sa = kFp8Max / fmaxf(amx, 1e-30f);
+        for (int c8 = q; c8 < SH::D0 / 8; c8 += 32)
+          *reinterpret_cast<long*>(q8 + r * L.ldq + 8 * c8) = quant_fp8x8(ld_frag(h0 + r * L.lda[0] + 8 * c8), sa);
+      }
     }
     for (int f = q; f < F; f += 32) yw += s_wx[r * F + f];
 #pragma unroll
@@ -495,7 +525,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 
   // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
   bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
-  bf16x8 bw0[SH::NJB0H][SH::KSB0], bw1[SH::KSB1], bw2[SH::KSB2];
+  typename W0Frag<FP8>::type bw0[SH::NJB0H][SH::KSB0];
+  bf16x8 bw1[SH::KSB1], bw2[SH::KSB2];
   // forward layers 1..2 and the upper backward layers' fragments (a few KiB per wave)
   auto prefetch_upper = [&]() {
     if constexpr (SH::kStatic) {
@@ -532,7 +563,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         for (int j = 0; j < SH::NJB0; ++j) {
           const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
 #pragma unroll
-          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
         }
       }
     }
@@ -550,6 +581,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float inv_keep = 1.f / keep;
     lds_barrier();  // previous layer's tile (and phase A/B) complete
     ROWS_STAMP(3 + l);
+
     if constexpr (SH::kStatic && SH::kLateBw0) {
       if (l == 1 && !(ablate & 4)) prefetch_upper();
       // from the last hidden layer on, only its own forward fragments are live: the layer-0 backward
@@ -559,7 +591,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         for (int j = 0; j < SH::NJB0H; ++j) {
           const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
 #pragma unroll
-          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+          for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
         }
       }
     }
@@ -568,27 +600,22 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SH::kStatic) {
         const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
-        if (l == 0 && FP8) {
-          // fp8-e4m3 MFMA: weights quantised per output column (this wave owns whole columns, all
-          // of K in registers), activations per row; the product is de-scaled in the epilogue
-          float wm = 0.f;
+        if (l == 0) {
+          if constexpr (FP8) {
+            // fp8-e4m3 MFMA: the weights come pre-quantised (one scale per tensor, w8inv), the
+            // activations are quantised per row here; the product is de-scaled in the epilogue
+            const uint8_t* aq = reinterpret_cast<const uint8_t*>(smem + L.q8) + (lane & 15) * L.ldq + 8 * (lane >> 4);
 #pragma unroll
-          for (int u = 0; u < SH::KSF0; ++u) wm = absmax_bf16x8(fw0[u], wm);
-          wm = fmaxf(wm, __shfl_xor(wm, 16, 64));
-          wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
-          const float sb = kFp8Max / fmaxf(wm, 1e-30f);
-          const float sa = kFp8Max / fmaxf(s_amax[lane & 15], 1e-30f);
+            for (int u = 0; u < SH::KSF0; ++u)
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(*reinterpret_cast<const long*>(aq + 32 * u), fw0[u],
+                                                              acc, 0, 0, 0);
+            const int rbq = (lane >> 4) * 4;
 #pragma unroll
-          for (int u = 0; u < SH::KSF0; ++u)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(quant_fp8x8(ld_frag(ap + 32 * u), sa),
-                                                            quant_fp8x8(fw0[u], sb), acc, 0, 0, 0);
-          const int rbq = (lane >> 4) * 4;
+            for (int i = 0; i < 4; ++i) acc[i] *= (fmaxf(rbq + i < RT ? s_amax[rbq + i] : 0.f, 1e-30f) / kFp8Max) * w8inv;
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[i] *= (fmaxf(s_amax[rbq + i], 1e-30f) / kFp8Max) * (1.f / sb);
-        } else if (l == 0) {
-#pragma unroll
-          for (int u = 0; u < SH::KSF0; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
+            for (int u = 0; u < SH::KSF0; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
+          }
         } else if (l == 1) {
 #pragma unroll
           for (int u = 0; u < SH::KSF1; ++u) acc = mfma16x16x32(ld_frag(ap + 32 * u), fw1[u], acc);
@@ -861,6 +888,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     lds_barrier();
     if (a == NL) ROWS_STAMP(10);
     const int li = a - 1, Dout = sh.dim(a), Din = sh.dim(li);
+
     const int ntiles = Din >> 4;
     constexpr int NJ = SH::kStatic ? (SH::NJB0 > 1 ? SH::NJB0 : 1) : 4;
     for (int nt0 = wave; nt0 < ntiles; nt0 += NJ * kWaves) {
@@ -870,6 +898,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
         for (int j = 0; j < NJ; ++j) accs[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (li == 0 && SH::kLateBw0) {
+          if constexpr (SH::kLateBw0 && !FP8) {  // (the launcher keeps fp8 off these shapes)
           // tile-major, software-pipelined over the NJB0H fragment slots (see CtShape::NJB0H)
           bf16x8 av[SH::KSB0];
 #pragma unroll
@@ -884,45 +913,37 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
             if (j < SH::NJB0H && j + SH::NJB0H < SH::NJB0) {
               const int nt = min(wave + kWaves * (j + SH::NJB0H), sh.dim(0) / 16 - 1);
 #pragma unroll
-              for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_frag(p.Wbs[0] + frag_at(nt, u, sh.dim(1), lane));
+              for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
             }
           }
-        } else if (li == 0 && FP8) {
-          // fp8-e4m3 dgrad dh0 = dz·W0ᵀ: dz quantised per row (s_amax), W0ᵀ per output column d
-          // (this wave holds all of k = dims[1] of its tiles in registers); de-scaled after
-          float sb[NJ];
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            float wm = 0.f;
-            if (j < SH::NJB0H) {
-#pragma unroll
-              for (int u = 0; u < SH::KSB0; ++u) wm = absmax_bf16x8(bw0[j][u], wm);
-            }
-            wm = fmaxf(wm, __shfl_xor(wm, 16, 64));
-            wm = fmaxf(wm, __shfl_xor(wm, 32, 64));
-            sb[j] = kFp8Max / fmaxf(wm, 1e-30f);
           }
-          const float sa = kFp8Max / fmaxf(s_amax[lane & 15], 1e-30f);
-#pragma unroll
-          for (int u = 0; u < SH::KSB0; ++u) {
-            const long av = quant_fp8x8(ld_frag(ap + 32 * u), sa);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-              if (j < SH::NJB0H && nt0 + kWaves * j < ntiles)
-                accs[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, quant_fp8x8(bw0[j][u], sb[j]), accs[j], 0, 0, 0);
-          }
-          const int rbq = (lane >> 4) * 4;
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) accs[j][i] *= (fmaxf(s_amax[rbq + i], 1e-30f) / kFp8Max) * (1.f / sb[j]);
         } else if (li == 0) {
+          if constexpr (FP8) {
+            // fp8-e4m3 dgrad dh0 = dz·W0ᵀ: dz quantised per row (s_amax), W0ᵀ pre-quantised (one
+            // scale per tensor, w8inv); de-scaled after
+            // (dz's 4 k-steps are quantised per wave: a shared LDS copy would cost a barrier)
+            const float sa = kFp8Max / fmaxf(s_amax[lane & 15], 1e-30f);
 #pragma unroll
-          for (int u = 0; u < SH::KSB0; ++u) {
-            const bf16x8 av = ld_frag(ap + 32 * u);
+            for (int u = 0; u < SH::KSB0; ++u) {
+              const long av = quant_fp8x8(ld_frag(ap + 32 * u), sa);
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                if (j < SH::NJB0H && nt0 + kWaves * j < ntiles)
+                  accs[j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av, bw0[j][u], accs[j], 0, 0, 0);
+            }
+            const int rbq = (lane >> 4) * 4;
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
-              if (j < SH::NJB0H && nt0 + kWaves * j < ntiles) accs[j] = mfma16x16x32(av, bw0[j][u], accs[j]);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) accs[j][i] *= (fmaxf(s_amax[rbq + i], 1e-30f) / kFp8Max) * w8inv;
+          } else {
+#pragma unroll
+            for (int u = 0; u < SH::KSB0; ++u) {
+              const bf16x8 av = ld_frag(ap + 32 * u);
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                if (j < SH::NJB0H && nt0 + kWaves * j < ntiles) accs[j] = mfma16x16x32(av, bw0[j][u], accs[j]);
+            }
           }
         } else if (li == 1) {
 #pragma unroll
@@ -1084,7 +1105,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 // ------------------------------------------------------------------------------------------------
 static int align16(int x) { return (x + 15) & ~15; }
 
-RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn, int dedup_kp, int rt, bool gr_alias) {
+RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn, int dedup_kp, int rt, bool gr_alias,
+                        bool fp8) {
   RowsLds L{};
   int off = 0;
   auto take = [&](int bytes) {
@@ -1115,6 +1137,10 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn, int dedup
     L.dzB = take(kRowTile * L.ldz * 2);
   }
   L.f32 = take(kRowTile * dims[0] * 4);
+  if (fp8) {
+    L.ldq = dims[0] + 16;
+    L.q8 = take(kRowTile * L.ldq);
+  }
   if (dedup_kp > 0) {
     L.nxt = take(kRowTile * F * 4);
     // the tile's gradient rows: over the f32 scratch (dh0, dead once phase F has read it — the
@@ -1277,7 +1303,8 @@ int deepfm_rows_tile(const RowsParams& p) {
 }
 
 RowsLds rows_lds_layout_for(const RowsParams& p) {
-  return rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn, p.dedup ? p.Kp : 0, deepfm_rows_tile(p), is_static(p));
+  return rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn, p.dedup ? p.Kp : 0, deepfm_rows_tile(p), is_static(p),
+                         p.fp8 != 0 && is_static(p));
 }
 
 void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
@@ -1292,6 +1319,8 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
   ROCFM_REQUIRE(p.row_tile == 0 || p.row_tile == 4 || p.row_tile == 8 || p.row_tile == 16,
                 "deepfm_rows: row_tile must be 0, 4, 8 or 16");
   ROCFM_REQUIRE(!p.dedup || (p.contrib_pos && p.contrib_nxt && !p.bn), "deepfm_rows: dedup needs contrib_pos / _nxt");
+  ROCFM_REQUIRE(!p.fp8 || (p.w8.f && p.w8.b && p.w8.amax && p.w8.inv_scale),
+                "deepfm_rows: compute_dtype=fp8 needs the pre-quantised input-layer copies (set_w8)");
   p.lds = rows_lds_layout_for(p);
   ROCFM_REQUIRE(p.lds.total <= 160 * 1024, "deepfm_rows: LDS budget exceeded (F*K too large)");
   if (p.Bp / kRowTile == 0) return;

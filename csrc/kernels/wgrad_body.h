@@ -39,6 +39,37 @@ __device__ __forceinline__ float dot_bf16x8_f32(uint4 v, const float* g) {
          bf2f(v.z & 0xffff) * g[4] + bf2f(v.z >> 16) * g[5] + bf2f(v.w & 0xffff) * g[6] + bf2f(v.w >> 16) * g[7];
 }
 
+// one f32 → fp8-e4m3 byte (saturating: a delayed scale can be exceeded by the new weights)
+__device__ __forceinline__ uint8_t fp8_e4m3(float x) {
+  x = fminf(fmaxf(x, -kFp8Max), kFp8Max);
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xff);
+}
+
+// The fp8 input-layer refresh (deepfm_rows.h Fp8W0) of this thread's weights: quantise with the
+// delayed scale and publish the de-scale; returns the wave's max |w| of the new weights (the caller
+// reduces it over the workgroup and adds it with ONE atomic max — hundreds of waves' atomics on one
+// address serialise in L2: +2.8 µs on the step tail; max is order-independent, so the result is
+// deterministic).  `N` weights (i, o, w) per thread; every lane of the wave must call it (shuffles).
+template <int N>
+__device__ __forceinline__ float fp8_refresh(const Fp8W0& q8, int64_t step, int Din, int Dout, const int* ii,
+                                             const int* oo, const float* w, const bool* valid, bool publish) {
+  const float src = fmaxf(q8.amax[step & 1], 1e-30f);
+  const float qs = kFp8Max / src;
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    if (!valid[e]) continue;
+    const uint8_t v = fp8_e4m3(w[e] * qs);
+    q8.f[frag_swz(oo[e], ii[e], Din)] = v;
+    q8.b[frag_swz(ii[e], oo[e], Dout)] = v;
+    m = fmaxf(m, fabsf(w[e]));
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  if (publish) *q8.inv_scale = src / kFp8Max;
+  return m;
+}
+
 }  // namespace
 
 constexpr int kWgThreads = 512;  // 8 waves: each takes 1/8 of the batch
@@ -49,6 +80,7 @@ template <bool PUSH = false>
 __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) {
   __shared__ __attribute__((aligned(16))) float s_red[(kWgThreads / 64) * 16 * 64];
   __shared__ uint16_t s_T[32 * 34];
+  __shared__ float s_m8[kWgThreads / 64];  // fp8 refresh: per-wave max |w|
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
@@ -131,7 +163,20 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
         }
         s_T[ol[e] * 34 + il[e]] = hw;
       }
+      const bool q8 = li == 0 && p.w8.f;
+      if (q8) {
+        const int ii[2] = {ti * 32 + il[0], ti * 32 + il[1]}, oo[2] = {to * 32 + ol[0], to * 32 + ol[1]};
+        const bool ok[2] = {true, true};
+        const float m = fp8_refresh<2>(p.w8, p.step ? *p.step : 0, Din, Dout, ii, oo, w, ok, bid == 0 && t == 0);
+        if (lane == 0) s_m8[wave] = m;
+      }
       __syncthreads();
+      if (q8 && p.w8.track && t == 0) {  // one atomic per workgroup
+        float m = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kWgThreads / 64; ++ww) m = fmaxf(m, s_m8[ww]);
+        atomicMax(reinterpret_cast<unsigned*>(p.w8.amax + (((p.step ? *p.step : 0) + 1) & 1)), __float_as_uint(m));
+      }
       {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
         const int o = t >> 4, ip = (t & 15) * 2;
         const uint32_t v2 = (uint32_t)s_T[o * 34 + ip] | ((uint32_t)s_T[o * 34 + ip + 1] << 16);
@@ -216,6 +261,10 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
 template <int TPB = 256>
 __device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, const int bid, const int nblocks) {
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
+  const bool q8 = p.w8.f != nullptr && p.nl > 0;
+  const int64_t s8 = p.step ? *p.step : 0;
+  const float q8s = q8 ? kFp8Max / fmaxf(p.w8.amax[s8 & 1], 1e-30f) : 0.f;
+  float q8m = 0.f;  // max |w| of the layer-0 weights this thread refreshed
   for (int idx = bid * TPB + (int)threadIdx.x; idx < p.n; idx += nblocks * TPB) {
     float w = p.params[idx];
     if (p.apply) {
@@ -239,7 +288,27 @@ __device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, cons
           p.WTs[l][frag_swz(o, i, p.dims[l])] = h;
           p.Wbs[l][frag_swz(i, o, p.dims[l + 1])] = h;
         }
+        if (l == 0 && q8) {
+          const uint8_t v = fp8_e4m3(w * q8s);
+          p.w8.f[frag_swz(o, i, p.dims[0])] = v;
+          p.w8.b[frag_swz(i, o, p.dims[1])] = v;
+          q8m = fmaxf(q8m, fabsf(w));
+          if (k == 0) *p.w8.inv_scale = 1.f / q8s;
+        }
       }
+    }
+  }
+  if (q8 && p.w8.track) {  // (every thread of the block reaches this point) one atomic per block
+    __shared__ float s_q8[TPB / 64];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) q8m = fmaxf(q8m, __shfl_xor(q8m, d, 64));
+    if ((threadIdx.x & 63) == 0) s_q8[threadIdx.x >> 6] = q8m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = 0.f;
+#pragma unroll
+      for (int w = 0; w < TPB / 64; ++w) m = fmaxf(m, s_q8[w]);
+      if (m > 0.f) atomicMax(reinterpret_cast<unsigned*>(p.w8.amax + ((s8 + 1) & 1)), __float_as_uint(m));
     }
   }
 }

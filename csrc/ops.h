@@ -17,7 +17,7 @@ namespace rocfm {
 
 // deepfm_rows.hip
 RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0, int dedup_kp = 0, int rt = 16,
-                        bool gr_alias = false);
+                        bool gr_alias = false, bool fp8 = false);
 RowsLds rows_lds_layout_for(const RowsParams& p);  // the layout the launcher uses
 void launch_deepfm_rows(RowsParams p, hipStream_t stream);
 int deepfm_rows_tile(const RowsParams& p);

@@ -197,6 +197,14 @@ class FusedDeepFM:
         # MFMA-fragment-swizzled copies (common.h frag_swz): what the compile-time-shape row kernel loads
         self.WTs = [torch.zeros_like(w) for w in self.WT]
         self.Wbs = [torch.zeros_like(w) for w in self.Wb]
+        # compute_dtype=fp8: pre-quantised e4m3 copies of the input layer's swizzled weights, one
+        # scale per tensor from the previous weights' max |w| (deepfm_rows.h Fp8W0)
+        self.w8 = None
+        if self.compute_dtype == "fp8":
+            self.w8 = (torch.zeros(self.WTs[0].numel(), dtype=torch.uint8, device=dev),
+                       torch.zeros(self.Wbs[0].numel(), dtype=torch.uint8, device=dev),
+                       torch.zeros(2, dtype=torch.float32, device=dev),   # amax by step parity
+                       torch.zeros(1, dtype=torch.float32, device=dev))   # de-scale of the copies
         self.steps = torch.zeros(2, dtype=torch.int64, device=dev)   # global_step, by parity
         self.cursor = torch.zeros(2, dtype=torch.int64, device=dev)  # pool batch index, by parity
         self.lrt = torch.zeros(2, dtype=torch.float32, device=dev)     # per-step lr_t, by parity
@@ -333,6 +341,7 @@ class FusedDeepFM:
         rp.force_generic = 1 if self.force_generic else 0
         rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
         rp.row_tile = self.row_tile
+        self._set_w8(rp, 0)
         rp.dedup = 1 if (train and self.dedup) else 0
         rp.set_dims(L.dims)
         for l in range(L.nl):
@@ -377,6 +386,8 @@ class FusedDeepFM:
         for l in range(L.nl):
             wp.set_layer(l, L.offW[l], L.offb[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
             wp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
+        if self.fuse_dense_opt:
+            self._set_w8(wp, 1)
         if self.bn:
             wp.bn, wp.bn_grad, wp.bn_dmax = 1, self.bn_grad.data_ptr(), self.bn_dmax
             for l in range(L.nl):
@@ -392,6 +403,7 @@ class FusedDeepFM:
         for l in range(L.nl):
             dp.set_layer(l, L.offW[l], self.WT[l].data_ptr(), self.Wb[l].data_ptr())
             dp.set_swz(l, self.WTs[l].data_ptr(), self.Wbs[l].data_ptr())
+        self._set_w8(dp, 1)
         ep = H.EmbUpdateParams()
         ep.skeys, ep.svals = skeys_ptr, svals_ptr
         ep.n = self.n_lookup
@@ -557,10 +569,23 @@ class FusedDeepFM:
     def stream_ptr(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def _set_w8(self, prm, track: int) -> None:
+        if self.w8 is not None:
+            f, b, amax, inv = self.w8
+            prm.set_w8(f.data_ptr(), b.data_ptr(), amax.data_ptr(), inv.data_ptr(), int(track))
+
     def refresh_bf16(self) -> None:
+        """Rewrite the bf16 / swizzled (and fp8) weight copies from the f32 master weights."""
         dp = self.dense_apply_params[0]
         dp.apply = 0
+        if self.w8 is not None:  # host refresh: the exact max in both slots, no accumulation
+            L = self.layout
+            w0 = self.dense[L.offW[0]: L.offW[0] + L.dims[0] * L.dims[1]]
+            self.w8[2].copy_(w0.abs().max().reshape(1).expand(2))
+            self._set_w8(dp, 0)
         self.H.dense_apply(dp, self.stream_ptr)
+        if self.w8 is not None:
+            self._set_w8(dp, 1)
 
     def _sort(self, q: int, stream) -> None:
         self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.slot_ids[q].data_ptr(),

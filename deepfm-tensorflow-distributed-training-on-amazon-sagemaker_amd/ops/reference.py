@@ -79,7 +79,7 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
     bn_state = []
     for li, L in enumerate(layers):
         if fp8 and li == 0:
-            z = fp8_rowcol_matmul(h[-1], bf16(L["W"])) + L["b"]
+            z = fp8_row_tensor_matmul(h[-1], L["W"]) + L["b"]
         else:
             z = h[-1] @ bf16(L["W"]) + L["b"]
         a = torch.relu(z)
@@ -127,8 +127,8 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
         dz[nl] = bf16(torch.where(h[nl] > 0, g[:, None] * w_out[None, :] / keeps[nl - 1], torch.zeros_like(h[nl])))
     dh0 = None
     for a in range(nl, 0, -1):
-        if fp8 and a == 1:  # the input layer's dgrad on fp8 MFMA (dz per row, W0ᵀ per column)
-            dh = fp8_rowcol_matmul(dz[a], bf16(layers[0]["W"]).t())
+        if fp8 and a == 1:  # the input layer's dgrad on fp8 MFMA (dz per row, W0ᵀ per tensor)
+            dh = fp8_row_tensor_matmul(dz[a], layers[0]["W"].t())
         else:
             dh = dz[a] @ bf16(layers[a - 1]["W"]).t()
         if a - 1 >= 1:
@@ -157,14 +157,15 @@ def fused_step_reference(emb: torch.Tensor, layers: List[Dict[str, torch.Tensor]
 FP8_MAX = 448.0  # largest finite float8 e4m3fn
 
 
-def fp8_rowcol_matmul(A: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """A·W with A quantised to fp8-e4m3 per row and W per column (scale = 448 / max|·|), f32
-    accumulate, de-scaled — the fused kernel's compute_dtype=fp8 input-layer GEMMs (forward
-    h0·W0, and the dgrad dz1·W0ᵀ)."""
+def fp8_row_tensor_matmul(A: torch.Tensor, W: torch.Tensor, w_amax: Optional[float] = None) -> torch.Tensor:
+    """A·W on fp8-e4m3 operands: A quantised per row, W (the f32 master weights) with ONE scale
+    448 / w_amax (default: max |W|, what a host refresh uses; training refreshes use the previous
+    weights' max, deepfm_rows.h Fp8W0) — the fused kernel's pre-quantised input-layer GEMMs."""
     sa = FP8_MAX / A.abs().amax(1, keepdim=True).clamp_min(1e-30)
-    sb = FP8_MAX / W.abs().amax(0, keepdim=True).clamp_min(1e-30)
+    am = float(W.abs().max()) if w_amax is None else float(w_amax)
+    sb = FP8_MAX / max(am, 1e-30)
     Aq = (A * sa).to(torch.float8_e4m3fn).float()
-    Wq = (W * sb).to(torch.float8_e4m3fn).float()
+    Wq = (W * sb).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float()
     return (Aq @ Wq) * ((1.0 / sa) * (1.0 / sb))
 
 

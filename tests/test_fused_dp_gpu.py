@@ -225,6 +225,40 @@ def test_dp_multistep_graphs_world1_equal_single(mode, upd, merge, monkeypatch):
         assert dp.maps.hashed == (merge == "hash")
 
 
+@pytest.mark.parametrize("kind", ["dp", "rowshard"])
+def test_fp8_weight_copies_through_dense_apply(kind):
+    """compute_dtype=fp8 where the MLP weights are refreshed by the dense apply (DP merge launch /
+    row-shard owner update) instead of the tail's wgrad epilogue: after multi-step graphs the delayed
+    per-tensor amax slot holds max |W0| of the current weights, and training tracks the single-GPU
+    fp8 engine (same batches)."""
+    from rocfm.models.deepfm import init_params
+    from rocfm.models.fused import FusedDeepFM
+    from rocfm.parallel.dp import FusedDataParallel
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg()
+    batches = _batches(128, 5, 11)
+    pool = [torch.stack([b[i] for b in batches]).cuda() for i in range(3)]
+    dev = torch.device("cuda")
+    if kind == "dp":
+        drv = FusedDataParallel(spec, hp, 128, dev, params=init_params(spec, 3), use_graph=True, compute_dtype="fp8")
+    else:
+        drv = FusedRowShard(spec, hp, 128, dev, params=init_params(spec, 3), use_graph=True, compute_dtype="fp8")
+    one = FusedDeepFM(spec, hp, 128, dev, params=init_params(spec, 3), use_graph=True, compute_dtype="fp8")
+    drv.attach_pool(*pool)
+    one.attach_pool(*pool)
+    n = 13
+    drv.train_steps(n, 4)
+    one.train_steps(n, 4)
+    torch.cuda.synchronize()
+    e = drv.eng
+    L = e.layout
+    W0 = e.dense[L.offW[0]: L.offW[0] + L.dims[0] * L.dims[1]]
+    assert e.w8[2][n & 1].item() == W0.abs().max().item()
+    assert abs(e.w8[3].item() * 448.0 / W0.abs().max().item() - 1) < 0.05
+    torch.testing.assert_close(e.dense, one.dense, rtol=2e-3, atol=2e-4)
+
+
 def _stream_worker(rank, world, port, kind, out_path, shadow):
     """Streamed (host groups → HBM ring → multi-step graphs, exchange inline) vs pool-fed
     training of the same batches, both through the p2p exchange, with a shadow-validation window
