@@ -19,6 +19,8 @@
 #pragma once
 #include "../common.h"
 
+#include <vector>
+
 namespace rocfm {
 
 constexpr int kP2PMaxW = 16;
@@ -37,6 +39,15 @@ struct P2PParams {
 };
 
 void launch_p2p_push(const P2PParams& p, hipStream_t stream);
+
+// Up to kP2PMultiMax distinct exchanges handed off by one launch (their peer waits overlap).
+constexpr int kP2PMultiMax = 4;
+struct P2PMulti {
+  P2PParams x[kP2PMultiMax];
+  int start[kP2PMultiMax + 1];  // first workgroup of each exchange; start[n] = grid size
+  int n;
+};
+void launch_p2p_push_multi(const std::vector<P2PParams>& ps, hipStream_t stream);
 
 // Memory for peer-visible buffers.  kind: 0 uncached, 1 fine-grained, 2 plain hipMalloc.
 uintptr_t p2p_malloc(size_t bytes, int kind);

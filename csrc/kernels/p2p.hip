@@ -24,14 +24,15 @@ __device__ bool wait_geq(const uint32_t* p, uint32_t n, long long limit) {
   return false;
 }
 
-__global__ __launch_bounds__(kP2PThreads) void p2p_push_kernel(P2PParams p) {
+// One exchange's share of a push launch: workgroup bid of its nblocks = W * chunks.
+__device__ __forceinline__ void p2p_push_body(const P2PParams& p, const int bid, const int nblocks) {
   const int W = p.W, me = p.rank;
-  const int d = blockIdx.x / p.chunks, c = blockIdx.x - d * p.chunks;
+  const int d = bid / p.chunks, c = bid - d * p.chunks;
   __shared__ uint32_t s_n;
   if (threadIdx.x == 0) {
     const uint32_t n = __hip_atomic_load(p.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_n = n;
-    if (blockIdx.x == 0)  // this rank has entered exchange n: peers may overwrite its slots
+    if (bid == 0)  // this rank has entered exchange n: peers may overwrite its slots
       for (int r = 0; r < W; ++r)
         if (r != me) st_release_sys(p.sig[r] + me, n);
     if (d != me && !wait_geq(p.sig[me] + d, n, p.spin_limit)) atomicOr(p.error, 1);
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kP2PThreads) void p2p_push_kernel(P2PParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // "" = system scope
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t prev = __hip_atomic_fetch_add(p.ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {  // last workgroup: every payload store of this rank is done
+    if (prev == (uint32_t)nblocks - 1u) {  // last workgroup: every payload store of this rank is done
       __hip_atomic_store(p.ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence_system();
       for (int r = 0; r < W; ++r)
@@ -77,14 +78,51 @@ __global__ __launch_bounds__(kP2PThreads) void p2p_push_kernel(P2PParams p) {
   }
 }
 
+__global__ __launch_bounds__(kP2PThreads) void p2p_push_kernel(P2PParams p) {
+  p2p_push_body(p, blockIdx.x, gridDim.x);
+}
+
+// Several independent exchanges handed off by ONE launch (row-shard X3 + X4 + the next step's X1):
+// each exchange keeps its own flags and counters, so their peer waits overlap instead of running
+// as consecutive launches.  Workgroups [start[i], start[i+1]) serve exchange i.
+__global__ __launch_bounds__(kP2PThreads) void p2p_push_multi_kernel(P2PMulti m) {
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kP2PMultiMax; ++j)
+    if (j < m.n && (int)blockIdx.x >= m.start[j]) i = j;
+  p2p_push_body(m.x[i], blockIdx.x - m.start[i], m.start[i + 1] - m.start[i]);
+}
+
 }  // namespace
 
-void launch_p2p_push(const P2PParams& p, hipStream_t stream) {
+static void check_push(const P2PParams& p) {
   ROCFM_REQUIRE(p.W >= 1 && p.W <= kP2PMaxW && p.rank >= 0 && p.rank < p.W, "p2p: bad W/rank");
-  ROCFM_REQUIRE(p.chunks >= 1 && (long long)p.W * p.chunks < (1ll << 31), "p2p: bad chunks");
+  ROCFM_REQUIRE(p.chunks >= 1 && (long long)p.W * p.chunks < (1ll << 24), "p2p: bad chunks");
   ROCFM_REQUIRE(p.src && p.ctrl && p.error && p.n4 >= 0 && p.slot4 >= p.n4, "p2p: bad buffers");
   for (int r = 0; r < p.W; ++r) ROCFM_REQUIRE(p.recv[r] && p.sig[r], "p2p: peer buffer not mapped");
+}
+
+void launch_p2p_push(const P2PParams& p, hipStream_t stream) {
+  check_push(p);
   hipLaunchKernelGGL(p2p_push_kernel, dim3(p.W * p.chunks), dim3(kP2PThreads), 0, stream, p);
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
+
+void launch_p2p_push_multi(const std::vector<P2PParams>& ps, hipStream_t stream) {
+  ROCFM_REQUIRE(!ps.empty() && (int)ps.size() <= kP2PMultiMax, "p2p: 1..4 exchanges per multi push");
+  P2PMulti m{};
+  m.n = (int)ps.size();
+  int tot = 0;
+  for (int i = 0; i < m.n; ++i) {
+    check_push(ps[i]);
+    for (int j = 0; j < i; ++j)  // each exchange's counters are its own (one launch per exchange at a time)
+      ROCFM_REQUIRE(ps[j].ctrl != ps[i].ctrl, "p2p: one exchange twice in a multi push");
+    m.x[i] = ps[i];
+    m.start[i] = tot;
+    tot += ps[i].W * ps[i].chunks;
+  }
+  m.start[m.n] = tot;
+  hipLaunchKernelGGL(p2p_push_multi_kernel, dim3(tot), dim3(kP2PThreads), 0, stream, m);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

@@ -440,6 +440,8 @@ class FusedRowShard:
         # served after the previous update (staleness 0 there).
         self.staleness = int(staleness)
         self._pre_served = False
+        # ROCFM_P2P_MULTI=0: every p2p exchange as its own launch (A/B switch of _x3_x4 / x1_ahead)
+        self.combine_handoffs = os.environ.get("ROCFM_P2P_MULTI", "1") != "0"
         # hot-row replication (SURVEY §2.6 hybrid): the hot_rows most frequent ids (chosen from rank
         # 0's first batches, or set_hot_ids) are replicated on every rank — looked up locally, never
         # routed; their per-rank gradient sums ride the X4 MLP bucket and every rank applies the
@@ -516,7 +518,9 @@ class FusedRowShard:
         self.PX = (self.P + NH * (Kp + 1) + 3) // 4 * 4
         self.mlp_bucket = torch.zeros(self.PX, **f32)
         e.dense_grads_flat = self.mlp_bucket[:self.P]
-        slots = [cap, cap * Kp, cap * Kp, self.PX] + ([cap] if self.staleness else [])
+        # (5th: the request lists of odd steps — staleness 1, or the synchronous p2p path, whose X1 of
+        # step k+1 rides step k's X3/X4 hand-off launch)
+        slots = [cap, cap * Kp, cap * Kp, self.PX, cap]
         exs = open_exchanges(slots, dev, exchange, extra_floats=[0, NH * Kp] + [0] * (len(slots) - 2))
         self._bind_exchange(exs)
         self._p2p_params = {}
@@ -576,11 +580,10 @@ class FusedRowShard:
             self.grad_back = self.x_grad.recv_tensor(torch.float32, (M, Kp))
             for t, ex in ((self.recv_ids, self.x_ids), (self.rows_in, self.x_rows), (self.grad_back, self.x_grad)):
                 self.p2p_x[t.data_ptr()] = ex
-            if self.staleness:
-                r2 = exs[4].recv_tensor(torch.int32, (M,))
-                r2.fill_(PAD)
-                self.p2p_x[r2.data_ptr()] = exs[4]
-                self.recv_pair = [self.recv_ids, r2]
+            r2 = exs[4].recv_tensor(torch.int32, (M,))
+            r2.fill_(PAD)
+            self.p2p_x[r2.data_ptr()] = exs[4]
+            self.recv_pair = [self.recv_ids, r2]
             self.graph_collectives = self.use_graph  # push kernels are capturable whatever the backend
             # X4 pushed by its producer (csrc/kernels/push.h): the wgrad workgroups store the MLP
             # gradients straight into every rank's X4 slot from inside the step tail, and the X4
@@ -892,6 +895,50 @@ class FusedRowShard:
             self._graphs[key] = g
         g.replay()
 
+    def _p2p_prm(self, out, inp):
+        """(exchange, push parameters) of the p2p all-to-all of ``inp`` into ``out``."""
+        ex = self.p2p_x[out.data_ptr()]
+        key = (out.data_ptr(), inp.data_ptr())
+        prm = self._p2p_params.get(key)
+        if prm is None:
+            chunk = out.numel() // self.W
+            if self.grad_push is not None and ex is self.x_grad:  # X3 already in the slots
+                prm = self._p2p_params[key] = ex.params(inp.data_ptr(), 0)
+            else:
+                prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
+        return ex, prm
+
+    def _mlp_prm(self):
+        prm = self._p2p_params.get("mlp")
+        if prm is None:  # fused push: the payload is already in the slots, only the hand-off
+            n = 0 if self.mlp_push is not None else self.PX
+            prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), n)
+        return self.x_mlp, prm
+
+    def _x3_x4(self, x1_next=None) -> None:
+        """X3 row gradients + X4 MLP gradients (+ ``x1_next`` = (out, inp): the next step's X1
+        requests).  On the p2p path ONE hand-off launch carries all of them (p2p_push_multi: the
+        exchanges' peer waits overlap instead of running as consecutive launches); the shadow
+        window and the collectives run them one by one."""
+        if self.exchange == "p2p" and not self.shadow.active and self.combine_handoffs:
+            from .p2p import P2PExchange
+
+            pairs = [self._p2p_prm(self.grad_back, self.grad_stage), self._mlp_prm()]
+            if x1_next is not None:
+                pairs.append(self._p2p_prm(*x1_next))
+            P2PExchange.push_multi([a for a, _ in pairs], [b for _, b in pairs])
+            return
+        self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
+        self._allreduce_mlp()                                                   # X4 MLP grads
+        if x1_next is not None:
+            self._exchange(*x1_next)                                            # X1 of the next step
+
+    @property
+    def x1_ahead(self) -> bool:
+        """Synchronous p2p multi-step graphs: the X1 requests of step k+1 are handed off with
+        step k's X3/X4 (their routing is done by the side chain before the graph starts)."""
+        return not self.staleness and self.exchange == "p2p" and self.combine_handoffs
+
     def _exchange(self, out, inp):
         """Equal-split all-to-all of ``inp`` into ``out`` (X1-X3).  World 1 (no forced collectives):
         the receive side aliases the send side, nothing to move."""
@@ -899,14 +946,7 @@ class FusedRowShard:
             return
         ex = self.p2p_x.get(out.data_ptr())
         if ex is not None:
-            key = (out.data_ptr(), inp.data_ptr())
-            prm = self._p2p_params.get(key)
-            if prm is None:
-                chunk = out.numel() // self.W
-                if self.grad_push is not None and ex is self.x_grad:  # X3 already in the slots
-                    prm = self._p2p_params[key] = ex.params(inp.data_ptr(), 0)
-                else:
-                    prm = self._p2p_params[key] = ex.params(inp.data_ptr(), chunk, src_stride_floats=chunk)
+            ex, prm = self._p2p_prm(out, inp)
             ex.push(prm)
             if self.shadow.active:  # the same all-to-all through the collective, compared bitwise
                 self.shadow.corrupt_(out)
@@ -948,10 +988,7 @@ class FusedRowShard:
         """X4: the MLP gradients of every rank (p2p all-gather; the sum happens in dense_apply)."""
         e = self.eng
         if self.exchange == "p2p":
-            prm = self._p2p_params.get("mlp")
-            if prm is None:  # fused push: the payload is already in the slots, only the hand-off
-                n = 0 if self.mlp_push is not None else self.PX
-                prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), n)
+            _, prm = self._mlp_prm()
             self.x_mlp.push(prm)
             if self.shadow.active:  # X4 is an all-gather: this rank's own slot holds its payload
                 from .dp import _all_gather_flat
@@ -971,12 +1008,11 @@ class FusedRowShard:
             self._step_body_stale(p, serve_first=not self._pre_served)
             return
         side = self._fork_next(p)  # next batch's fetch + route overlaps the whole step
-        self._exchange(self.recv_ids, self.send_ids[p])                        # X1 requests
+        self._exchange(self._recv(p), self.send_ids[p])                         # X1 requests
         self._phase_serve(p)
         self._exchange(self.rows_x, self.rows_out[:self.M])                             # X2 rows
         self._phase_compute(p, with_side=False)
-        self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
-        self._allreduce_mlp()                                                   # X4 MLP grads
+        self._x3_x4()                                                           # X3 + X4
         self._phase_update(p)
         e._join(side)
 
@@ -990,9 +1026,7 @@ class FusedRowShard:
             self._phase_serve(p)
             self._exchange(self.rows_x, self.rows_out[:self.M])                         # X2 rows
         self._phase_compute(p, with_side=True)  # joins the side chain: batch 1-p is routed
-        self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
-        self._allreduce_mlp()                                                   # X4 MLP grads
-        self._exchange(self._recv(1 - p), self.send_ids[1 - p])                 # X1 of the next step
+        self._x3_x4((self._recv(1 - p), self.send_ids[1 - p]))                  # X3 + X4 + X1 of the next step
         if self.maps is not None:
             H.merge_scatter(self.owner_params[p], e.stream_ptr)
         H.merge_search_apply(self.owner_params[p], e.dense_apply_params[p], e.stream_ptr, self.serve[1 - p],
@@ -1017,7 +1051,7 @@ class FusedRowShard:
         elif self.graph_collectives:  # one graph per step, collectives included
             self._run(("step", p), lambda: self._step_body(p), collectives=True)
         else:
-            self._exchange(self.recv_ids, self.send_ids[p])
+            self._exchange(self._recv(p), self.send_ids[p])
             self._run(("serve", p), lambda: self._phase_serve(p))
             self._exchange(self.rows_x, self.rows_out[:self.M])
             self._run(("compute", p), lambda: self._phase_compute(p))
@@ -1187,7 +1221,7 @@ class FusedRowShard:
                           "hpos", "use_maps"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
-                par = k % 2 if self.staleness else 0
+                par = k % 2 if self.recv_pair is not None else 0
                 mg.keys = self._recv_ids_for(self.ms_send[q, k], par).data_ptr()
                 if ed is not None:
                     ed.grad_scale = 1.0
@@ -1209,21 +1243,22 @@ class FusedRowShard:
         e, H = self.eng, self.H
         s = torch.cuda.current_stream(self.device).cuda_stream
         st = self.staleness
+        ahead = self.x1_ahead  # X1 of step k+1 rides step k's X3/X4 hand-off
         for k in range(S):
             rows, wp, ep, da, ed, mg, sv, hot = self.ms_steps[q][k]
-            par = k % 2 if st else 0
-            if k == 0 or not st:  # (staleness 1: later steps were served by the previous update)
+            par = k % 2 if self.recv_pair is not None else 0
+            if k == 0 or not (st or ahead):  # (later steps: requested by the previous step)
                 self._exchange(self._recv(par), self.ms_send[q, k])             # X1 requests
+            if k == 0 or not st:  # (staleness 1: later steps were served by the previous update)
                 H.shard_serve(sv, s)
                 self._exchange(self.rows_x, self.rows_out[:self.M])                     # X2 rows
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
-            self._exchange(self.grad_back, self.grad_stage)                     # X3 row grads
-            self._allreduce_mlp()                                               # X4 MLP grads
+            nxt = (self._recv(1 - par), self.ms_send[q, k + 1]) if (st or ahead) and k + 1 < S else None
+            self._x3_x4(nxt)                                                    # X3 + X4 (+ X1 of step k+1)
             if self.maps is not None:
                 H.merge_scatter(mg, s)                                          # (larger worlds)
             if st and k + 1 < S:  # owner merge ‖ MLP opt ‖ serve of step k+1
-                self._exchange(self._recv(1 - par), self.ms_send[q, k + 1])     # X1 of step k+1
                 H.merge_search_apply(mg, da, s, self.ms_steps[q][k + 1][6], hot)
                 if ed is not None:
                     H.emb_dense_update(ed, s)

@@ -194,6 +194,18 @@ class P2PExchange:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         self.H.p2p_push(p, stream)
 
+    @staticmethod
+    def push_multi(exs: List["P2PExchange"], ps, stream: Optional[int] = None) -> None:
+        """Hand off several distinct exchanges (``ps[i]`` built by ``exs[i].params``) in ONE launch:
+        each keeps its own flags and counters, and their peer waits overlap (p2p.hip
+        p2p_push_multi_kernel).  Every rank must combine the same exchanges in the same launch."""
+        if len(exs) == 1:
+            exs[0].push(ps[0], stream)
+            return
+        if stream is None:
+            stream = torch.cuda.current_stream(exs[0].device).cuda_stream
+        exs[0].H.p2p_push_multi(list(ps), stream)
+
     def slot_ptr(self, r: int) -> int:
         return self.recv_ptr + r * self.slot * 4
 

@@ -148,7 +148,10 @@ class Recorder:
         roles = pointer_roles()
         out = []
         for kernel, args in self.calls.get(section, []):
-            for ai, a in enumerate(args):
+            flat = []
+            for a in args:  # (a list argument: one launch over several parameter blocks)
+                flat.extend(a if isinstance(a, (list, tuple)) else [a])
+            for ai, a in enumerate(flat):
                 if hasattr(a, "raw"):
                     named = roles.get(type(a).__name__, {})
                     seen = set()
