@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--table_dtype", default="f32", choices=["f32", "bf16"],
                     help="embedding table storage (bf16: stochastic-rounded updates, f32 optimizer slots)")
     ap.add_argument("--embedding_update", default="sparse", choices=["sparse", "exact"])
-    ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard"])
+    ap.add_argument("--parallelism", default="auto", choices=["auto", "dp", "dense_dp", "rowshard", "dp_owner"])
     ap.add_argument("--pool", type=int, default=32, help="distinct device-resident batches to cycle")
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--dp_exchange", default="auto", choices=["auto", "p2p", "rccl"],
@@ -133,7 +133,7 @@ def main():
     keeps = [float(x) for x in a.dropout.split(",")]
     spec = ModelSpec(a.feature_size, a.field_size, a.embedding_size, layers, keeps, l2_reg=a.l2_reg)
     hp = OptHParams(name=a.optimizer, lr=a.learning_rate)
-    if a.parallelism == "rowshard" or (a.engine == "fused" and a.feature_size > 20_000_000):
+    if a.parallelism in ("rowshard", "dp_owner") or (a.engine == "fused" and a.feature_size > 20_000_000):
         params = None  # tables drawn on the device (each rank's own shard in rowshard mode): a
         #                100M-1B-row table never materialises on the host
     else:
@@ -155,20 +155,22 @@ def main():
     if parallelism == "auto":
         parallelism = "dp"  # either update; dense_dp (dense all-reduce) only when asked for
     cap = None
-    if a.engine == "fused" and (world > 1 or a.parallelism in ("dp", "rowshard")) and parallelism != "dense_dp":
+    sharded = parallelism in ("rowshard", "dp_owner")  # owner-routed row gradients (emb_shard)
+    if a.engine == "fused" and (world > 1 or a.parallelism in ("dp", "rowshard", "dp_owner")) and parallelism != "dense_dp":
         if a.capacity == "auto":
             from rocfm.parallel.dp import pool_exchange_capacity
 
-            cap = pool_exchange_capacity(pool_ids, world if parallelism == "rowshard" else 1)
+            cap = pool_exchange_capacity(pool_ids, world if sharded else 1)
         elif a.capacity != "safe":
             cap = int(a.capacity)
     if a.engine == "fused":
-        if parallelism == "rowshard":
+        if sharded:
             from rocfm.parallel.emb_shard import FusedRowShard
 
             eng = FusedRowShard(spec, hp, B, dev, params=params, embedding_update=a.embedding_update, seed=a.seed,
                                 use_graph=not a.no_graph, capacity=cap, compute_dtype=a.compute_dtype, table_dtype=a.table_dtype,
-                                exchange=a.dp_exchange, staleness=a.ps_staleness, hot_rows=a.hot_rows)
+                                exchange=a.dp_exchange, staleness=a.ps_staleness, hot_rows=a.hot_rows,
+                                replicate_table=parallelism == "dp_owner")
         elif world > 1 or explicit_dp:
             from rocfm.parallel.dp import FusedDataParallel
 
@@ -192,13 +194,13 @@ def main():
     else:
         from rocfm.models.torch_engine import TorchDeepFM
 
-        if parallelism == "rowshard":
+        if sharded:  # (dp_owner: the same synchronous mathematics as rowshard in eager PyTorch)
             from rocfm.parallel.emb_shard import TorchRowShard
 
             eng = TorchRowShard(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
         else:
             eng = TorchDeepFM(spec, hp, dev, embedding_update=a.embedding_update, params=params, seed=a.seed)
-        if world > 1 and parallelism != "rowshard":
+        if world > 1 and not sharded:
             from rocfm.parallel.dp import attach_torch_dp
 
             attach_torch_dp(eng, a.embedding_update)

@@ -96,6 +96,7 @@ struct RowsParams {
   int* bn_error;                      // set if a grid barrier timed out (the host check raises)
   PushTarget push;                    // producer push (push.h): workgroup 0 signals "entered"
   PushTarget push2;                   // a second exchange pushed by this step (row-shard X3)
+  PushTarget push3;                   // a third (owner-sharded DP: X5, pushed by the owner merge)
   int row_tile;                       // examples per workgroup: 16, 8 or 4 (0 = default; static shapes)
   // per-tile dedup (batch.h DedupParams): contrib_pos holds each lookup's compacted group index (c
   // for the group's first lookup, ~c for the others) and contrib_nxt the next lookup of its group;

@@ -169,8 +169,8 @@ struct RtShape {
   static constexpr bool kStatic = false;
   static constexpr int KSF0 = 1, KSF1 = 1, KSF2 = 1, NJB0 = 1, KSB0 = 1, KSB1 = 1, KSB2 = 1;
   static constexpr int GU = 4;                 // gathered rows per thread per batch (phases A, F)
-  static constexpr int KSF0E = 1, NJB0H = 1;
-  static constexpr bool kLateBw0 = false;
+  static constexpr int KSF0E = 1, NJB0H = 1, NTF0 = 1, NTB1 = 1;
+  static constexpr bool kLateBw0 = false, kWide = false;
   int F, K, nl, d[kMaxHidden + 1];
   __device__ explicit RtShape(const RowsParams& p) : F(p.F), K(p.K), nl(p.nl) {
 #pragma unroll
@@ -204,11 +204,21 @@ struct CtShape {
   // layer-0 forward fragments prefetched at kernel entry; kLateBw0 shapes load the rest after the
   // gather (phase A holds GU gathered rows + their scaled copies in registers)
   static constexpr int KSF0E = kLateBw0 ? 8 : KSF0;
-  // registers for layer-0 backward fragments: all NJB0 tiles, or (kLateBw0) the first half — each
-  // slot is refilled with tile j + NJB0H right after tile j's MFMAs have been issued
-  static constexpr int NJB0H = kLateBw0 ? (NJB0 + 1) / 2 : NJB0;
+  // Wide first hidden layer (D1 = 256, the reference's default 256-128-64): each wave owns NTF0 = 2
+  // forward tiles of layer 0 and NTB1 = 2 backward tiles of layer 1.  Layer 0's forward fragments
+  // then stream through the KSF0 registers of one tile — slot u is refilled with the next tile's
+  // k-step u right after its MFMA has been issued — so the second tile's loads fly under the first
+  // tile's MFMAs and epilogue (the per-CU fragment bandwidth, not registers, bounds the layer).
+  static constexpr int NTF0 = (D1 / 16 + kWaves - 1) / kWaves;
+  static constexpr int NTB1 = NTF0;
+  static constexpr bool kWide = NTF0 > 1;
+  // registers for layer-0 backward fragments: all NJB0 tiles, or (kLateBw0) a ring of NJB0H tiles —
+  // slot j % NJB0H is refilled with tile j + NJB0H right after tile j's MFMAs have been issued (wide
+  // shapes: 4 slots of 8 k-steps, the rest of the register file holds the upper layers)
+  static constexpr int NJB0H = kLateBw0 ? (kWide ? 4 : (NJB0 + 1) / 2) : NJB0;
   __device__ explicit CtShape(const RowsParams&) {}
-  static_assert(D0 <= 1280 && D1 <= 128 && D2 <= 128 && D3 <= 128, "CtShape limits");
+  static_assert(D0 <= 1280 && D1 <= 256 && D2 <= 128 && D3 <= 128, "CtShape limits");
+  static_assert(!kWide || (kLateBw0 && NTF0 == 2), "CtShape: a 256-wide first layer needs the streamed layer 0");
   static_assert(D1 % 32 == 0 && D2 % 32 == 0 && D3 % 32 == 0, "hidden dims padded to 32");
   static_assert(GU <= 12, "CtShape: at most 12 gathered rows per thread");
 };
@@ -243,9 +253,12 @@ constexpr int kInfer = 0, kTrain = 1, kDynamic = 2;
 // RT: examples per workgroup (16, or 8 for twice the workgroups on a 256-CU chip).  The LDS tiles
 // and MFMA M tiles stay 16 rows; with RT = 8 rows 8..15 are zero padding whose outputs are
 // discarded (no global store touches them), so the arithmetic of every valid row is unchanged.
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT>
+// BN: a compile-time-shape kernel with batch_norm layers (16-row workgroups, grid barriers); the
+// runtime-shape kernel reads p.bn, the other compile-time-shape kernels have no batch-norm code.
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT, bool BN = false>
 __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsParams p) {
   static_assert(RT == 16 || RT == 8 || RT == 4, "rows per workgroup: 16, 8 or 4");
+  static_assert(!BN || (SH::kStatic && RT == kRowTile && !FP8), "batch_norm kernels: 16-row tiles, bf16");
   static_assert(RT != 4 || SH::kStatic, "4-row workgroups: compile-time shapes only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long s_stamp[16];
@@ -526,7 +539,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   // ---- prefetch (static shapes): forward layers 1..2 and every backward fragment ----------------
   bf16x8 fw1[SH::KSF1], fw2[SH::KSF2];
   typename W0Frag<FP8>::type bw0[SH::NJB0H][SH::KSB0];
-  bf16x8 bw1[SH::KSB1], bw2[SH::KSB2];
+  bf16x8 bw1[SH::NTB1][SH::KSB1], bw2[SH::KSB2];
   // forward layers 1..2 and the upper backward layers' fragments (a few KiB per wave)
   auto prefetch_upper = [&]() {
     if constexpr (SH::kStatic) {
@@ -542,9 +555,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
     if (train) {
       if constexpr (SH::nl >= 2) {
-        const int nt = min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
-        for (int u = 0; u < SH::KSB1; ++u) bw1[u] = ld_frag(p.Wbs[1] + frag_at(nt, u, sh.dim(2), lane));
+        for (int j = 0; j < SH::NTB1; ++j) {
+          const int nt = min(wave + kWaves * j, sh.dim(1) / 16 - 1);
+#pragma unroll
+          for (int u = 0; u < SH::KSB1; ++u) bw1[j][u] = ld_frag(p.Wbs[1] + frag_at(nt, u, sh.dim(2), lane));
+        }
       }
       if constexpr (SH::nl >= 3) {
         const int nt = min(wave, sh.dim(2) / 16 - 1);
@@ -596,11 +612,26 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
     }
     const int ntiles = Dout >> 4;
-    for (int nt = wave; nt < ntiles; nt += kWaves) {
+    // compile-time shapes: tile j of this wave is wave + 8j (layer 0 of a wide shape has 2, every
+    // other layer 1 — the outer loop then runs once); runtime shapes: one tile per iteration
+    constexpr int kNT = SH::kStatic ? SH::NTF0 : 1;
+    for (int nt0 = wave; nt0 < ntiles; nt0 += kNT * kWaves) {
+#pragma unroll
+     for (int j = 0; j < kNT; ++j) {
+      const int nt = nt0 + kWaves * j;
+      if (j > 0 && (l > 0 || nt >= ntiles)) break;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SH::kStatic) {
         const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
-        if (l == 0) {
+        if (l == 0 && SH::kWide && !FP8) {
+          // streamed layer 0: slot u is refilled with the next tile's k-step u right behind its MFMA
+          const int nxt = min(nt + kWaves, ntiles - 1);
+#pragma unroll
+          for (int u = 0; u < SH::KSF0; ++u) {
+            acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
+            if (j + 1 < kNT) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nxt, u, sh.dim(0), lane));
+          }
+        } else if (l == 0) {
           if constexpr (FP8) {
             // fp8-e4m3 MFMA: the weights come pre-quantised (one scale per tensor, w8inv), the
             // activations are quantised per row here; the product is de-scaled in the epilogue
@@ -630,7 +661,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
       const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
       const float bc = s_prm[L.prm_bias[l] + c];
-      if constexpr (!SH::kStatic) {
+      if constexpr (!SH::kStatic || BN) {
         if (p.bn) {  // training: keep r = relu(z) for the batch moments; inference: moving moments
           float* R = reinterpret_cast<float*>(smem + L.bnr[l]);
 #pragma unroll
@@ -661,8 +692,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       if (train && rb < RT)
         *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+     }
     }
-    if constexpr (!SH::kStatic) {
+    if constexpr (!SH::kStatic || BN) {
       if (p.bn && train) {
         // batch moments of r over all B rows: this workgroup's (mean, M2) per column → grid
         // barrier → Chan's combination in workgroup order (deterministic) → normalise, dropout
@@ -839,7 +871,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     }
   };
   bool bn_head = false;
-  if constexpr (!SH::kStatic) {
+  if constexpr (!SH::kStatic || BN) {
     if (p.bn) {  // dy of the last hidden layer's BN output: g·w_out through its dropout mask
       const int l = NL - 1, Dn = sh.dim(NL);
       float* DY = reinterpret_cast<float*>(smem + L.bndy);
@@ -905,12 +937,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           for (int u = 0; u < SH::KSB0; ++u) av[u] = ld_frag(ap + 32 * u);
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const int slot = j < SH::NJB0H ? j : j - SH::NJB0H;
+            const int slot = j % SH::NJB0H;
             if (nt0 + kWaves * j < ntiles) {
 #pragma unroll
               for (int u = 0; u < SH::KSB0; ++u) accs[j] = mfma16x16x32(av[u], bw0[slot][u], accs[j]);
             }
-            if (j < SH::NJB0H && j + SH::NJB0H < SH::NJB0) {
+            if (j + SH::NJB0H < SH::NJB0) {
               const int nt = min(wave + kWaves * (j + SH::NJB0H), sh.dim(0) / 16 - 1);
 #pragma unroll
               for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
@@ -947,7 +979,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           }
         } else if (li == 1) {
 #pragma unroll
-          for (int u = 0; u < SH::KSB1; ++u) accs[0] = mfma16x16x32(ld_frag(ap + 32 * u), bw1[u], accs[0]);
+          for (int u = 0; u < SH::KSB1; ++u) {
+            const bf16x8 av = ld_frag(ap + 32 * u);
+#pragma unroll
+            for (int j = 0; j < SH::NTB1; ++j) accs[j] = mfma16x16x32(av, bw1[j][u], accs[j]);
+          }
         } else {
 #pragma unroll
           for (int u = 0; u < SH::KSB2; ++u) accs[0] = mfma16x16x32(ld_frag(ap + 32 * u), bw2[u], accs[0]);
@@ -960,11 +996,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       for (int j = 0; j < NJ; ++j) {
         const int nt = nt0 + kWaves * j;
         if (nt >= ntiles) continue;
-        if (SH::kStatic && li > 0 && j > 0) continue;
+        if (SH::kStatic && li > 0 && j >= (li == 1 ? SH::NTB1 : 1)) continue;
         const f32x4 acc = accs[j];
         const int c = nt * 16 + (lane & 15), rb = (lane >> 4) * 4;
         if (li >= 1) {
-          if constexpr (!SH::kStatic) {
+          if constexpr (!SH::kStatic || BN) {
             if (p.bn) {  // gradient w.r.t. layer li-1's BN output, through its dropout mask
               float* DY = reinterpret_cast<float*>(smem + L.bndy);
               const float keep = p.keep[li - 1], inv_keep = 1.f / keep;
@@ -1005,7 +1041,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         }
       }
     }
-    if constexpr (!SH::kStatic) {
+    if constexpr (!SH::kStatic || BN) {
       if (p.bn && li >= 1) bn_backward(li - 1, dz_nxt);
     }
     uint16_t* tmp = dz_cur;
@@ -1092,8 +1128,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if (blockIdx.x == 0 && t == 0) {
     if (p.push.W > 0) push_signal_ready(p.push);
     if (p.push2.W > 0) push_signal_ready(p.push2);
+    if (p.push3.W > 0) push_signal_ready(p.push3);
   }
-  if constexpr (!SH::kStatic) {
+  if constexpr (!SH::kStatic || BN) {
     if (p.bn) bn_grid_exit(p);
   }
   if (DIAG && p.stamps != nullptr) {
@@ -1173,9 +1210,9 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn, int dedup
   return L;
 }
 
-template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT = kRowTile>
+template <int KP4, class SH, bool FP8, int MODE, bool DIAG, bool BT, int RT = kRowTile, bool BN = false>
 static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
-  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG, BT, RT>;
+  auto kern = deepfm_rows_kernel<KP4, SH, FP8, MODE, DIAG, BT, RT, BN>;
   static bool attr_set = false;
   static int max_dyn = 0;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950, minus the static part)
@@ -1206,15 +1243,26 @@ static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
 template <int KP4, class SH, bool BT, int RT>
 static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
   if constexpr (SH::kStatic) {
+    if (p.bn) {  // batch_norm: 16-row tiles, f32 table, bf16 (static_ok)
+      if constexpr (!BT && RT == kRowTile) {
+        if (p.train)
+          launch_rows_impl<KP4, SH, false, kTrain, false, false, kRowTile, true>(p, stream);
+        else
+          launch_rows_impl<KP4, SH, false, kInfer, false, false, kRowTile, true>(p, stream);
+        return;
+      } else {
+        throw std::logic_error("deepfm_rows: batch_norm kernels are built for 16-row tiles and f32 tables");
+      }
+    }
     const bool diag = p.stamps != nullptr || p.ablate != 0;
     if (diag) {
-      if constexpr (SH::F == 39 && SH::K == 10 && SH::nl == 3 && !BT) {
+      if constexpr (SH::F == 39 && (SH::K == 10 || SH::kWide) && SH::nl == 3 && !BT) {
         ROCFM_REQUIRE(!p.fp8 && p.train, "deepfm_rows: diagnostics are built for the bf16 training kernel only");
         launch_rows_impl<KP4, SH, false, kTrain, true, false, RT>(p, stream);
         return;
       } else {
-        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 shape "
-                                    "and an f32 table");
+        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 or "
+                                    "39x32 256-128-64 shape and an f32 table");
       }
     }
     if (p.fp8) {
@@ -1232,9 +1280,9 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
       launch_rows_impl<KP4, SH, false, kTrain, false, BT, RT>(p, stream);
     else
       launch_rows_impl<KP4, SH, false, kInfer, false, BT, RT>(p, stream);
-    return;
+  } else {
+    launch_rows_impl<KP4, SH, false, kDynamic, true, BT, RT>(p, stream);
   }
-  launch_rows_impl<KP4, SH, false, kDynamic, true, BT, RT>(p, stream);
 }
 
 // rows per workgroup (RowsParams::row_tile, 0 = kDefaultRowTile): 8 doubles the workgroups of a
@@ -1245,8 +1293,9 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
 constexpr int kDefaultRowTile = 8;
 static int row_tile_for(const RowsParams& p, bool is_static_shape) {
   const int rt = p.row_tile ? p.row_tile : kDefaultRowTile;
+  if (p.bn) return kRowTile;  // batch-norm statistics partials are per 16-row workgroup
   if (is_static_shape) return rt;
-  return p.bn ? 16 : (rt == 4 ? 8 : rt);
+  return rt == 4 ? 8 : rt;
 }
 template <int KP4, class SH>
 static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
@@ -1268,8 +1317,8 @@ static void launch_rows_tb(const RowsParams& p, hipStream_t stream) {
   }
 }
 
-// Compile-time-shape instantiations (the benchmark / notebook-style models).  Anything else runs
-// the runtime-shape kernel.
+// Compile-time-shape instantiations (the benchmark / notebook-style models, and the reference's
+// flag defaults k=32, 256-128-64 — PS:52,62).  Anything else runs the runtime-shape kernel.
 template <int F, int K, int D1, int D2, int D3>
 static bool static_match(const RowsParams& p) {
   const int nl = D3 ? 3 : (D2 ? 2 : 1);
@@ -1289,11 +1338,14 @@ static bool try_static(const RowsParams& p, hipStream_t stream) {
   return true;
 }
 
+// batch_norm runs the compile-time-shape kernels too, with an f32 table and bf16 MFMA
+static bool static_ok(const RowsParams& p) { return !p.force_generic && !(p.bn && (p.tbl_bf16 || p.fp8)); }
+
 static bool is_static(const RowsParams& p) {
-  return !p.force_generic && !p.bn &&
+  return static_ok(p) &&
          (static_match<39, 10, 128, 64, 32>(p) || static_match<39, 8, 128, 64, 32>(p) ||
           static_match<39, 12, 128, 64, 32>(p) || static_match<39, 10, 64, 32, 0>(p) ||
-          static_match<39, 32, 128, 64, 32>(p));
+          static_match<39, 32, 128, 64, 32>(p) || static_match<39, 32, 256, 128, 64>(p));
 }
 
 // Examples per workgroup the launcher will use for these parameters (the per-tile dedup of the side
@@ -1301,6 +1353,8 @@ static bool is_static(const RowsParams& p) {
 int deepfm_rows_tile(const RowsParams& p) {
   return row_tile_for(p, is_static(p));
 }
+
+bool deepfm_rows_static(const RowsParams& p) { return is_static(p); }
 
 RowsLds rows_lds_layout_for(const RowsParams& p) {
   return rows_lds_layout(p.dims, p.nl, p.F, p.K, p.bn, p.dedup ? p.Kp : 0, deepfm_rows_tile(p), is_static(p),
@@ -1328,10 +1382,10 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
     ROCFM_REQUIRE(p.bn_part && p.bn_grad && p.bn_sync && p.bn_error, "deepfm_rows: batch_norm buffers missing");
     for (int a = 1; a <= p.nl; ++a) ROCFM_REQUIRE(p.dims[a] <= p.bn_dmax, "deepfm_rows: bn_dmax < hidden dim");
   }
-  if (!p.force_generic && !p.bn) {
+  if (static_ok(p)) {
     if (try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
         try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream) ||
-        try_static<39, 32, 128, 64, 32>(p, stream)) {
+        try_static<39, 32, 128, 64, 32>(p, stream) || try_static<39, 32, 256, 128, 64>(p, stream)) {
       ROCFM_HIP_CHECK(hipGetLastError());
       return;
     }

@@ -48,7 +48,8 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
 template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
-  __shared__ float4 s_rows[kChunk * KP4];
+  __shared__ float4 s_rows[kE * KP4];  // the chunk's entries only (threads past kE hold none): with the
+                                       // fused tail's kE = 256 two 512-thread workgroups fit a CU at Kp = 36
   __shared__ float4 s_cont[kWaves * KP4];
   __shared__ int s_head[kChunk + 1];
   __shared__ uint32_t s_hkey[kChunk + 1];
@@ -113,8 +114,10 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         if (lane - d >= seg) v[u] = f4add(v[u], o);
       }
     }
+    if (t < kE) {  // (wave-uniform: kE is a multiple of 64)
 #pragma unroll
-    for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
+      for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
+    }
   }
   // 3. compact the heads in order
   const unsigned long long m = __ballot(head);

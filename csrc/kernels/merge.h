@@ -30,6 +30,7 @@
 #pragma once
 #include "../common.h"
 #include "optim.h"
+#include "push.h"
 
 namespace rocfm {
 
@@ -73,7 +74,28 @@ struct MergeParams {
   long long dir_stride;
   int nb;
   uint32_t bucket_div;
+  // owner-sharded DP (emb_shard replicate_table, mode 0): every updated row is also appended to a
+  // broadcast list — slot = atomicAdd(bc_count) — as (global id = row · bc_mul + bc_add, f32 row);
+  // the X5 all-gather carries the lists to every rank's full table replica (row_scatter)
+  int32_t* bc_count;  // nullable: no broadcast
+  uint32_t* bc_keys;
+  float* bc_rows;     // [bc_cap][Kp]
+  int bc_cap;
+  uint32_t bc_mul, bc_add;
+  PushTarget bc_push;  // W > 0: the lists go straight into every rank's X5 slot (keys at +4, rows at
+                       // +4 + bc_cap floats); the X5 launch then carries only bc_count + the hand-off
 };
+
+// Every rank's full table replica takes the rows the owners broadcast (X5): source r's list at
+// recv + r·slot_stride = [count int32 | pad 3 | keys cap | rows cap·Kp].
+struct RowScatterParams {
+  const float* recv;
+  long long slot_stride;  // floats
+  int W, cap, Kp;
+  float* table;           // [V][Kp] f32
+  uint32_t rows;          // V (keys ≥ V are skipped)
+};
+void launch_row_scatter(const RowScatterParams& p, hipStream_t stream);
 
 void launch_merge_scatter(const MergeParams& p, hipStream_t stream);
 void launch_merge_apply(const MergeParams& p, hipStream_t stream);

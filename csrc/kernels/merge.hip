@@ -102,6 +102,38 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scatter_kernel(MergeParam
   merge_scatter_body(p, blockIdx.x);
 }
 
+// Owner-sharded DP: append the updated row to the broadcast list (MergeParams::bc_*).
+// With bc_push the peers' "entered" flags (raised by their row kernels) are read at the start of the
+// merge body (bc_seen) and compared before the first store into their slots.
+__device__ __forceinline__ PushSeen bc_seen(const MergeParams& p) {
+  return (p.bc_count != nullptr && p.bc_push.W > 0) ? push_ready_load(p.bc_push) : PushSeen{};
+}
+
+template <int KP4>
+__device__ __forceinline__ void bcast_row(const MergeParams& p, uint32_t row, const float4 (&w)[KP4],
+                                          const PushSeen& seen) {
+  if (p.bc_count == nullptr) return;
+  const int s = atomicAdd(p.bc_count, 1);
+  if (s >= p.bc_cap) return;  // (cannot happen: bc_cap = W·cap ≥ every source's entries)
+  const uint32_t gid = row * p.bc_mul + p.bc_add;
+  if (p.bc_push.W > 0) {
+    push_wait_ready(p.bc_push, seen);
+    for (int d = 0; d < p.bc_push.W; ++d) {
+      float* b = p.bc_push.slot[d];
+      reinterpret_cast<uint32_t*>(b + 4)[s] = gid;
+      float4* o = reinterpret_cast<float4*>(b + 4 + p.bc_cap) + (size_t)s * KP4;
+#pragma unroll
+      for (int c = 0; c < KP4; ++c) o[c] = w[c];
+    }
+    push_drain();
+    return;
+  }
+  p.bc_keys[s] = gid;
+  float4* o = reinterpret_cast<float4*>(p.bc_rows) + (size_t)s * KP4;
+#pragma unroll
+  for (int c = 0; c < KP4; ++c) o[c] = w[c];
+}
+
 // One thread per source entry; only representatives (lowest rank holding the key) do work.
 // WMAX = 8 (one node): every later source's position and row are loaded before any is summed.
 template <int KP4, int WMAX>
@@ -132,6 +164,7 @@ __device__ __forceinline__ void merge_maps_body(const MergeParams& p, const int 
   };
   const int W = p.W;
   const size_t base = (size_t)row * KP4;
+  const PushSeen seen = bc_seen(p);
   // the table row and its optimizer slots depend only on the row: issued now, in the same round
   // trip as the other sources' positions (one dependent global round trip less per row)
   // (mode 1 does not need them; the loads are harmless there: emb / slots are always valid)
@@ -235,6 +268,7 @@ __device__ __forceinline__ void merge_maps_body(const MergeParams& p, const int 
     if (a4) a4[c] = a[c];
     if (b4) b4[c] = b[c];
   }
+  bcast_row<KP4>(p, row, w, seen);
 }
 
 template <int KP4, int WMAX>
@@ -263,7 +297,8 @@ __device__ __forceinline__ int len_of(const MergeParams& p, int q) {
 // Optimizer (mode 0) or dense-gradient row (mode 1) of one merged row: shared by the search apply
 template <int KP4>
 __device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t row, float4 (&w)[KP4], float4 (&a)[KP4],
-                                               float4 (&b)[KP4], const float4 (&acc)[KP4]) {
+                                               float4 (&b)[KP4], const float4 (&acc)[KP4],
+                                               const PushSeen& seen = PushSeen{}) {
   const size_t base = (size_t)row * KP4;
   if (p.mode == 1) {
     float4* dg = reinterpret_cast<float4*>(p.dense_grad) + base;
@@ -292,6 +327,7 @@ __device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t ro
     if (a4) a4[c] = a[c];
     if (b4) b4[c] = b[c];
   }
+  bcast_row<KP4>(p, row, w, seen);
 }
 
 // WMAX = 8: the W−1 searches advance together (≈log2(cap) rounds of up to 7 independent loads);
@@ -306,6 +342,7 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   const uint32_t row = key / p.key_div;
   const int W = p.W;
   const size_t base = (size_t)row * KP4;
+  const PushSeen seen = bc_seen(p);
   // the row's parameters and slots: issued before the searches (same as merge_apply)
   float4 w[KP4], a[KP4], b[KP4];
   const float4* a4r = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb) + base;
@@ -403,7 +440,7 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
       }
     }
   }
-  merged_row_out<KP4>(p, row, w, a, b, acc);
+  merged_row_out<KP4>(p, row, w, a, b, acc, seen);
 }
 
 // One thread per replicated row (all KP4 float4 columns): Σ of the rank segments in rank order
@@ -695,6 +732,45 @@ void check(const MergeParams& p) {
 }
 
 }  // namespace
+
+template <int KP4>
+__global__ __launch_bounds__(kMergeThreads) void row_scatter_kernel(RowScatterParams p) {
+  const long long per = (long long)p.cap * KP4;
+  const long long n = (long long)p.W * per;
+  for (long long it = (long long)blockIdx.x * kMergeThreads + threadIdx.x; it < n;
+       it += (long long)gridDim.x * kMergeThreads) {
+    const int r = (int)(it / per);
+    const long long e = it - r * per;
+    const int i = (int)(e / KP4), c = (int)(e - (long long)i * KP4);
+    const float* slot = p.recv + (size_t)r * p.slot_stride;
+    if (i >= reinterpret_cast<const int32_t*>(slot)[0]) continue;
+    const uint32_t key = reinterpret_cast<const uint32_t*>(slot + 4)[i];
+    if (key >= p.rows) continue;
+    const float4 v = reinterpret_cast<const float4*>(slot + 4 + p.cap)[(size_t)i * KP4 + c];
+    reinterpret_cast<float4*>(p.table)[(size_t)key * KP4 + c] = v;
+  }
+}
+
+void launch_row_scatter(const RowScatterParams& p, hipStream_t stream) {
+  ROCFM_REQUIRE(p.recv && p.table && p.W >= 1 && p.cap >= 0 && p.cap % 4 == 0 && p.Kp % 4 == 0 && p.Kp <= 64,
+                "row_scatter: bad parameters");
+  ROCFM_REQUIRE(p.slot_stride >= 4 + (long long)p.cap * (1 + p.Kp), "row_scatter: slot too small");
+  const long long n = (long long)p.W * p.cap * (p.Kp / 4);
+  if (n == 0) return;
+  const unsigned grid = (unsigned)std::min<long long>((n + kMergeThreads - 1) / kMergeThreads, 2048);
+  switch (p.Kp / 4) {
+#define ROCFM_KP4(N)                                                                        \
+  case N:                                                                                   \
+    hipLaunchKernelGGL(row_scatter_kernel<N>, dim3(grid), dim3(kMergeThreads), 0, stream, p); \
+    break;
+    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
+    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12) ROCFM_KP4(13) ROCFM_KP4(14) ROCFM_KP4(15) ROCFM_KP4(16)
+#undef ROCFM_KP4
+    default:
+      throw std::invalid_argument("row_scatter: unsupported Kp");
+  }
+  ROCFM_HIP_CHECK(hipGetLastError());
+}
 
 void launch_merge_init(const MergeParams& p, hipStream_t stream) {
   check(p);

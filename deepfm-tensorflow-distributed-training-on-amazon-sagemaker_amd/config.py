@@ -101,6 +101,7 @@ class Config:
     engine: str = "auto"  # auto | fused (HIP kernels) | torch (eager oracle; CPU or GPU)
     embedding_update: str = "sparse"  # sparse (lazy L2 + row optimizer) | exact (dense, faithful Q1)
     parallelism: str = "auto"  # auto | dp (replicated table) | rowshard (PS-equivalent) | dense_dp
+    #                            | dp_owner (replicated table, owner-sharded embedding optimizer)
     lr_scaling: str = "linear"  # linear (lr × world, HVD:171) | none
     compute_dtype: str = "bf16"  # bf16 | fp8: MLP MFMA operands in the fused engine (fp8: the input
     #                              layer's forward GEMM on e4m3 with dynamic per-row/per-column scales)
@@ -191,7 +192,7 @@ class Config:
             raise ValueError(f"unknown embedding_update {self.embedding_update!r}")
         if self.compute_dtype not in ("bf16", "fp8"):
             raise ValueError(f"compute_dtype must be bf16 or fp8, got {self.compute_dtype!r}")
-        if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard"):
+        if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard", "dp_owner"):
             raise ValueError(f"unknown parallelism {self.parallelism!r}")
         if self.engine not in ("auto", "fused", "torch"):
             raise ValueError(f"unknown engine {self.engine!r}")

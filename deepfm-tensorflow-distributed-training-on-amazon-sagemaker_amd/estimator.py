@@ -57,7 +57,7 @@ class Estimator:
         self.world = _world()
         self.hp = OptHParams(name=cfg.optimizer, lr=cfg.learning_rate)
         self.engine_name = self._pick_engine()
-        if params is None and cfg.parallelism != "rowshard":
+        if params is None and cfg.parallelism not in ("rowshard", "dp_owner"):
             params = init_params(self.spec, cfg.seed)
         P = params  # row-shard: None → every rank initialises only its own rows
         self.eng = self._build_engine(P)
@@ -94,7 +94,7 @@ class Estimator:
     def _build_engine(self, P):
         cfg = self.cfg
         cap = cfg.exchange_capacity or None
-        if cfg.parallelism == "rowshard":
+        if cfg.parallelism in ("rowshard", "dp_owner"):
             from .parallel.emb_shard import FusedRowShard, TorchRowShard
 
             if self.engine_name == "fused":
@@ -102,7 +102,7 @@ class Estimator:
                                      embedding_update=cfg.embedding_update, seed=cfg.seed,
                                      use_graph=cfg.use_hip_graph, capacity=cap, compute_dtype=cfg.compute_dtype, table_dtype=cfg.table_dtype,
                                      exchange=cfg.dp_exchange, staleness=cfg.ps_staleness,
-                                     hot_rows=cfg.hot_rows)
+                                     hot_rows=cfg.hot_rows, replicate_table=cfg.parallelism == "dp_owner")
             if cfg.ps_staleness or cfg.hot_rows or cfg.table_dtype != "f32":
                 raise ValueError("ps_staleness / hot_rows / table_dtype=bf16 need the fused engine (a GPU)")
             return TorchRowShard(self.spec, self.hp, self.device, embedding_update=cfg.embedding_update, params=P,

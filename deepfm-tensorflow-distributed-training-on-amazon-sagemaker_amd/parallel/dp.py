@@ -522,8 +522,9 @@ class FusedDataParallel:
         """The p2p all-gather just delivered every rank's slot: gather this rank's own slot through
         the collective as well, compare bitwise, and let the merge consume the collective's copy."""
         got = self.p2p.recv_tensor(torch.float32, (self.world * self.S,))
-        self.shadow.corrupt_(got)
+        # this rank's own slot is the reference it contributes: copied before a (test) fault lands
         own = got[self.rank * self.S:(self.rank + 1) * self.S].clone()
+        self.shadow.corrupt_(got)
         _all_gather_flat(self._shadow_buf, own)
         self.shadow.compare(got, self._shadow_buf)
 

@@ -428,8 +428,18 @@ class FusedRowShard:
                  embedding_update: str = "sparse", seed: int = 1234, use_graph: bool = True,
                  capacity: Optional[int] = None, check_every: int = 256, compute_dtype: str = "bf16",
                  exchange: Optional[str] = None, staleness: int = 0, hot_rows: int = 0,
-                 table_dtype: str = "f32"):
+                 table_dtype: str = "f32", replicate_table: bool = False):
         from ..models.fused import FusedDeepFM
+
+        # replicate_table (``parallelism=dp_owner``): owner-sharded DP.  Every rank keeps a FULL table
+        # replica for its forward (no X1/X2 before the row kernel); the embedding optimizer is
+        # sharded: owner o = id % W sums the row gradients sent to it (X3), applies lazy L2 + the row
+        # optimizer with its 1/W share of the slots, and broadcasts the updated rows (X5) into every
+        # replica.  Merge work and optimizer state per rank are 1/W of plain DP's.
+        self.replicate = bool(replicate_table)
+        if self.replicate and (staleness or hot_rows or embedding_update != "sparse" or table_dtype != "f32"):
+            raise ValueError("owner-sharded DP (dp_owner) runs the synchronous sparse update on an f32 table "
+                             "(no staleness, no hot rows)")
 
         if staleness not in (0, 1):
             raise ValueError(f"row-shard staleness must be 0 (synchronous) or 1, got {staleness}")
@@ -521,6 +531,15 @@ class FusedRowShard:
         # (5th: the request lists of odd steps — staleness 1, or the synchronous p2p path, whose X1 of
         # step k+1 rides step k's X3/X4 hand-off launch)
         slots = [cap, cap * Kp, cap * Kp, self.PX, cap]
+        # X5 (dp_owner): each owner's updated rows, [count | pad 3 | keys W·cap | rows W·cap·Kp]
+        self.capB = W * cap
+        self.S5 = 4 + self.capB * (1 + Kp)
+        self.emb_full = self.x5_send = None
+        if self.replicate:
+            slots.append(self.S5)
+            self.x5_send = torch.zeros(self.S5, **f32)
+            self.emb_full = (_gather_table(e.emb.float().contiguous(), self.V, W) if W > 1
+                             else e.emb[:self.V].float()).contiguous().clone()
         exs = open_exchanges(slots, dev, exchange, extra_floats=[0, NH * Kp] + [0] * (len(slots) - 2))
         self._bind_exchange(exs)
         self._p2p_params = {}
@@ -615,6 +634,22 @@ class FusedRowShard:
             self.graph_collectives = self.use_graph and collectives_capturable()
         self.rows_x = self.rows_in[:M]  # the X2 all-to-all part of rows_in
         self.hot_rep = self.rows_in[M:]  # the replica
+        # X5 (dp_owner): the owners' updated-row lists — peer-mapped slots (the owner merge pushes
+        # keys + rows itself; the X5 launch carries the counts), the send buffer itself (one rank),
+        # or a gathered tensor for the collective
+        self.x_bc = self.bc_push = self.bc_recv = None
+        if self.replicate:
+            if exs:
+                self.x_bc = exs[5]
+                self.x_all = list(exs)
+                self.bc_recv_ptr, self.bc_slot = self.x_bc.recv_ptr, self.x_bc.slot
+                self.bc_push = self.x_bc.push_target()
+            elif W == 1 and not self.force:
+                self.bc_recv, self.bc_slot = self.x5_send, self.S5
+                self.bc_recv_ptr = self.x5_send.data_ptr()
+            else:
+                self.bc_recv, self.bc_slot = torch.zeros(W * self.S5, **f32), self.S5
+                self.bc_recv_ptr = self.bc_recv.data_ptr()
 
     # ---- kernel parameter blocks ------------------------------------------------------------------
     def _route_params(self, ids, rsv, send, local, skl, counts, n):
@@ -641,6 +676,7 @@ class FusedRowShard:
             rp = e.rows_params[p]
             rp.ids, rp.emb = self.local_idx[p].data_ptr(), self.rows_in.data_ptr()
             rp.tbl_bf16 = 0  # the row kernel's table is the f32 received-rows buffer
+            self._bind_replica(rp, e.slot_ids[p])
             lp = e.emb_params[p]  # local: Σ lookup grads per received row → grad_stage
             lp.skeys, lp.svals, lp.n = self.skl[p].data_ptr(), self.rsv[p].data_ptr(), self.n
             lp.mode, lp.dense_grad, lp.max_key, lp.grad_scale = 1, self.grad_stage.data_ptr(), 0, 1.0
@@ -659,6 +695,7 @@ class FusedRowShard:
             op.s0, op.s1 = e._slot_ptrs(e.emb_slots)
             op.l2, op.grad_scale = float(self.spec.l2_reg), 1.0 / self.W
             op.opt, op.step = e._opt(p), e.steps[p:].data_ptr()
+            self._bind_bcast(op)
             if self.embedding_update == "exact":
                 op.mode, op.dense_grad = 1, e.dense_grad.data_ptr()
                 op.touched = e.touched.data_ptr()  # the owner's dense update reads these rows
@@ -679,6 +716,59 @@ class FusedRowShard:
         self.pred_route[0].n_hot = 0  # predictions read the owners' (flushed) rows
         self.hot_params = [self._hot_params(lp_, self.owner_params[p].opt, self.owner_params[p].step)
                            for p, lp_ in enumerate(e.emb_params[:2])]
+
+    # ---- owner-sharded DP (replicate_table) --------------------------------------------------------
+    def _bind_replica(self, rp, ids) -> None:
+        """dp_owner: the row kernel gathers the batch's global ids from the full replica, and its
+        workgroup 0 also raises "entered" for X5 (the previous step's row_scatter, the last reader
+        of this rank's X5 slots, is done); it zeroes this step's X5 row counter."""
+        if not self.replicate:
+            return
+        rp.ids, rp.emb, rp.tbl_bf16 = ids.data_ptr(), self.emb_full.data_ptr(), 0
+        rp.push3 = self.bc_push if self.bc_push is not None else self.H.PushTarget()
+        rp.zero_word = self.x5_send.data_ptr()
+
+    def _bind_bcast(self, op) -> None:
+        """dp_owner: the owner merge appends every updated row (global id, f32 row) to X5."""
+        if not self.replicate:
+            return
+        op.bc_count = self.x5_send.data_ptr()
+        op.bc_keys = self.x5_send[4:].data_ptr()
+        op.bc_rows = self.x5_send[4 + self.capB:].data_ptr()
+        op.bc_cap, op.bc_mul, op.bc_add = self.capB, self.W, self.rank
+        op.bc_push = self.bc_push if self.bc_push is not None else self.H.PushTarget()
+
+    def _x5(self) -> None:
+        """X5 all-gather of the owners' updated rows, then every replica takes them (row_scatter)."""
+        if self.x_bc is not None:  # p2p: keys + rows already pushed by the merge; counts + hand-off here
+            prm = self._p2p_params.get("x5")
+            if prm is None:
+                prm = self._p2p_params["x5"] = self.x_bc.params(self.x5_send.data_ptr(), 4)
+            self.x_bc.push(prm)
+            if self.shadow.active:  # an all-gather: this rank's own slot holds its list
+                from .dp import _all_gather_flat
+
+                sl = self.bc_slot
+                got = self.x_bc.recv_tensor(torch.float32, (self.W * sl,))
+                own = got[self.rank * sl:(self.rank + 1) * sl].clone()  # (before a fault hits the copy)
+                self.shadow.corrupt_(got)
+                want = torch.empty_like(got)
+                _all_gather_flat(want, own)
+                self.shadow.compare(got, want)
+        elif self.W > 1 or self.force:
+            from .dp import _all_gather_flat
+
+            _all_gather_flat(self.bc_recv, self.x5_send)
+        sp = self.H.RowScatterParams()
+        sp.recv, sp.slot_stride, sp.W, sp.cap, sp.Kp = self.bc_recv_ptr, self.bc_slot, self.W, self.capB, self.eng.Kp
+        sp.table, sp.rows = self.emb_full.data_ptr(), self.V
+        self.H.row_scatter(sp, self.eng.stream_ptr)
+
+    def _sync_full(self) -> None:
+        """Rebuild the full replica from the owners' shards (after a checkpoint restore)."""
+        e = self.eng
+        full = _gather_table(e.emb.float().contiguous(), self.V, self.W) if self.W > 1 else e.emb[:self.V].float()
+        self.emb_full.copy_(full)
 
     # ---- hot-row replication ----------------------------------------------------------------------
     def _bind_hot_out(self, ep) -> None:
@@ -915,7 +1005,7 @@ class FusedRowShard:
             prm = self._p2p_params["mlp"] = self.x_mlp.params(self.mlp_bucket.data_ptr(), n)
         return self.x_mlp, prm
 
-    def _x3_x4(self, x1_next=None) -> None:
+    def _x3_x4(self, x1_next=None, x1_now=None) -> None:
         """X3 row gradients + X4 MLP gradients (+ ``x1_next`` = (out, inp): the next step's X1
         requests).  On the p2p path ONE hand-off launch carries all of them (p2p_push_multi: the
         exchanges' peer waits overlap instead of running as consecutive launches); the shadow
@@ -924,10 +1014,13 @@ class FusedRowShard:
             from .p2p import P2PExchange
 
             pairs = [self._p2p_prm(self.grad_back, self.grad_stage), self._mlp_prm()]
-            if x1_next is not None:
-                pairs.append(self._p2p_prm(*x1_next))
+            for x1 in (x1_now, x1_next):
+                if x1 is not None:
+                    pairs.append(self._p2p_prm(*x1))
             P2PExchange.push_multi([a for a, _ in pairs], [b for _, b in pairs])
             return
+        if x1_now is not None:
+            self._exchange(*x1_now)                                             # X1 of this step (dp_owner)
         self._exchange(self.grad_back, self.grad_stage)                         # X3 row grads
         self._allreduce_mlp()                                                   # X4 MLP grads
         if x1_next is not None:
@@ -937,7 +1030,7 @@ class FusedRowShard:
     def x1_ahead(self) -> bool:
         """Synchronous p2p multi-step graphs: the X1 requests of step k+1 are handed off with
         step k's X3/X4 (their routing is done by the side chain before the graph starts)."""
-        return not self.staleness and self.exchange == "p2p" and self.combine_handoffs
+        return not self.staleness and not self.replicate and self.exchange == "p2p" and self.combine_handoffs
 
     def _exchange(self, out, inp):
         """Equal-split all-to-all of ``inp`` into ``out`` (X1-X3).  World 1 (no forced collectives):
@@ -994,10 +1087,11 @@ class FusedRowShard:
                 from .dp import _all_gather_flat
 
                 got = self.x_mlp.recv_tensor(torch.float32, (self.W * self.x_mlp.slot,))
+                sl = self.x_mlp.slot
+                own = got[self.rank * sl:(self.rank + 1) * sl].clone()  # (before a fault hits the copy)
                 self.shadow.corrupt_(got)
                 want = torch.empty_like(got)
-                sl = self.x_mlp.slot
-                _all_gather_flat(want, got[self.rank * sl:(self.rank + 1) * sl].clone())
+                _all_gather_flat(want, own)
                 self.shadow.compare(got, want)
         elif self.W > 1 or self.force:
             all_reduce_(self.mlp_bucket)  # MLP grads + replicated-row sums, one collective
@@ -1008,6 +1102,13 @@ class FusedRowShard:
             self._step_body_stale(p, serve_first=not self._pre_served)
             return
         side = self._fork_next(p)  # next batch's fetch + route overlaps the whole step
+        if self.replicate:  # dp_owner: the forward reads the full replica; X1 only keys the merge
+            self._phase_compute(p, with_side=False)
+            self._x3_x4(None, (self._recv(p), self.send_ids[p]))                # X1 + X3 + X4
+            self._phase_update(p)
+            self._x5()                                                          # X5 updated rows
+            e._join(side)
+            return
         self._exchange(self._recv(p), self.send_ids[p])                         # X1 requests
         self._phase_serve(p)
         self._exchange(self.rows_x, self.rows_out[:self.M])                             # X2 rows
@@ -1050,6 +1151,11 @@ class FusedRowShard:
             self._pre_served = True
         elif self.graph_collectives:  # one graph per step, collectives included
             self._run(("step", p), lambda: self._step_body(p), collectives=True)
+        elif self.replicate:
+            self._run(("compute", p), lambda: self._phase_compute(p))
+            self._x3_x4(None, (self._recv(p), self.send_ids[p]))
+            self._run(("update", p), lambda: self._phase_update(p))
+            self._x5()
         else:
             self._exchange(self._recv(p), self.send_ids[p])
             self._run(("serve", p), lambda: self._phase_serve(p))
@@ -1095,7 +1201,8 @@ class FusedRowShard:
 
     def replicated_tensors(self):
         e = self.eng
-        return [e.dense, e.steps, self.hot_rep] + list(e.dense_slots) + list(self.hot_slots)
+        full = [self.emb_full] if self.replicate else []
+        return [e.dense, e.steps, self.hot_rep] + list(e.dense_slots) + list(self.hot_slots) + full
 
     def verify_replicas(self) -> bool:
         """Collective: the replicated state (MLP, its slots, the step, replicated hot rows) is
@@ -1204,6 +1311,7 @@ class FusedRowShard:
                 rows, wp, da, ep, ed = e.m_params[q][k]
                 rows.ids, rows.emb = self.ms_local[q, k].data_ptr(), self.rows_in.data_ptr()
                 rows.tbl_bf16 = 0
+                self._bind_replica(rows, e.m_ids[q, k])
                 wp.grads = e.dense_grads_flat.data_ptr()
                 self._set_push(rows, wp, ep)
                 ep.skeys, ep.n = self.ms_skl[q, k].data_ptr(), n
@@ -1218,7 +1326,8 @@ class FusedRowShard:
                 for f in ("keys", "rows", "counts", "key_stride", "row_stride", "count_stride", "W", "cap", "Kp",
                           "K1", "key_div", "Vmap", "emb", "s0", "s1", "l2", "grad_scale", "mode",
                           "dense_grad", "touched", "tbl_bf16", "pos", "rep", "hash_slots", "hkeys", "hrep",
-                          "hpos", "use_maps"):
+                          "hpos", "use_maps", "bc_count", "bc_keys", "bc_rows", "bc_cap", "bc_mul", "bc_add",
+                          "bc_push"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
                 par = k % 2 if self.recv_pair is not None else 0
@@ -1247,15 +1356,17 @@ class FusedRowShard:
         for k in range(S):
             rows, wp, ep, da, ed, mg, sv, hot = self.ms_steps[q][k]
             par = k % 2 if self.recv_pair is not None else 0
-            if k == 0 or not (st or ahead):  # (later steps: requested by the previous step)
+            rep_ = self.replicate  # dp_owner: no serve / X2; X1 rides this step's X3/X4 hand-off
+            if not rep_ and (k == 0 or not (st or ahead)):  # (later steps: requested by the previous step)
                 self._exchange(self._recv(par), self.ms_send[q, k])             # X1 requests
-            if k == 0 or not st:  # (staleness 1: later steps were served by the previous update)
+            if not rep_ and (k == 0 or not st):  # (staleness 1: later steps were served by the previous update)
                 H.shard_serve(sv, s)
                 self._exchange(self.rows_x, self.rows_out[:self.M])                     # X2 rows
             H.deepfm_rows(rows, s)
             e._tail(wp, ep, None, s)                                            # wgrad ‖ Σ rows per request
             nxt = (self._recv(1 - par), self.ms_send[q, k + 1]) if (st or ahead) and k + 1 < S else None
-            self._x3_x4(nxt)                                                    # X3 + X4 (+ X1 of step k+1)
+            now = (self._recv(par), self.ms_send[q, k]) if rep_ else None
+            self._x3_x4(nxt, now)                                               # X3 + X4 (+ X1)
             if self.maps is not None:
                 H.merge_scatter(mg, s)                                          # (larger worlds)
             if st and k + 1 < S:  # owner merge ‖ MLP opt ‖ serve of step k+1
@@ -1267,6 +1378,8 @@ class FusedRowShard:
             H.merge_search_apply(mg, da, s, None, hot)                          # owner merge ‖ MLP opt ‖ hot
             if ed is not None:
                 H.emb_dense_update(ed, s)
+            if rep_:
+                self._x5()                                                      # X5 updated rows → replicas
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         e = self.eng
@@ -1425,6 +1538,8 @@ class FusedRowShard:
         sd = _localize(sd, self.row_sets(), self.V, self.W, self.rank, self.Vs, self.n_loc)
         self.eng.load_state_dict(sd, strict=strict)
         self._load_hot()
+        if self.replicate:
+            self._sync_full()
         if self.maps is not None:
             self.maps.reset()  # the hash merge tags words with the step, which just moved
         self._pre_served = False

@@ -42,7 +42,7 @@ def _ref_inputs(eng: FusedDeepFM, spec: ModelSpec, step: int, keeps):
 @pytest.mark.parametrize("K,layers,generic", [(10, [128, 64, 32], False), (10, [128, 64, 32], True),
                                               (32, [256, 128, 64], False), (8, [48, 16], False),
                                               (10, [64, 32], False), (32, [128, 64, 32], False),
-                                              (32, [128, 64, 32], True)])
+                                              (32, [128, 64, 32], True), (32, [256, 128, 64], True)])
 def test_fused_step_gradients_match_oracle(K, layers, generic):
     torch.manual_seed(0)
     dev = torch.device("cuda")
@@ -335,17 +335,22 @@ def _bn_params(spec, seed):
     return P
 
 
-@pytest.mark.parametrize("layers,keep", [([128, 64, 32], 0.5), ([64, 32], 1.0)])
-def test_fused_batch_norm_matches_oracle(layers, keep):
+@pytest.mark.parametrize("layers,keep,generic", [([128, 64, 32], 0.5, False), ([128, 64, 32], 0.5, True),
+                                                ([64, 32], 1.0, False), ([64, 32], 1.0, True)])
+def test_fused_batch_norm_matches_oracle(layers, keep, generic):
     """batch_norm=True on the fused row kernel (batch moments via in-launch grid reductions):
     forward, MLP / γ / β / embedding gradients and the moving-moment updates match the fp32
     oracle with the same bf16 rounding points and dropout masks; inference uses the moving
-    moments.  B=192 leaves 4 all-padding workgroups in the grid."""
+    moments.  B=192 leaves 4 all-padding workgroups in the grid.  Both the compile-time-shape
+    kernel (PS:316-338 batch_norm on the fast path) and the runtime-shape one."""
     dev = torch.device("cuda")
     spec = _bn_spec(layers, keep)
     B, K = 192, 10
     P = _bn_params(spec, 7)
-    eng = FusedDeepFM(spec, OptHParams(name="GD", lr=1.0), B, dev, params=P, use_graph=False)
+    eng = FusedDeepFM(spec, OptHParams(name="GD", lr=1.0), B, dev, params=P, use_graph=False,
+                      force_generic_kernels=generic)
+    assert eng.H.deepfm_rows_static(eng.rows_params[0]) == (not generic)
+    assert eng.H.deepfm_rows_tile(eng.rows_params[0]) == 16
     gen = torch.Generator().manual_seed(2)
     ids, vals, labels = _batch(B, 39, 5000, gen)
     emb, lays, w_out, b_out, fmb, masks = _ref_inputs(eng, spec, 0, spec.keep_probs)
@@ -387,10 +392,11 @@ def test_fused_batch_norm_matches_oracle(layers, keep):
     assert _rel(prob.cpu(), ref2["prob"]) < 2e-3
 
 
-def test_fused_batch_norm_multistep_graph_equals_per_step():
+@pytest.mark.parametrize("layers", [[64, 32], [128, 64, 32]])
+def test_fused_batch_norm_multistep_graph_equals_per_step(layers):
     """Grid-barrier counters reset between launches: multi-step graph replays of the batch-norm
     row kernel train bit-identically to per-step eager launches."""
-    spec = _bn_spec([64, 32], 0.7)
+    spec = _bn_spec(layers, 0.7)
     g = torch.Generator().manual_seed(4)
     pool = [_batch(128, 39, 5000, g) for _ in range(5)]
     ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
@@ -687,3 +693,33 @@ def test_merge_range_equals_search(W, mode):
             assert torch.equal(a, b)
         else:
             assert bool(((a.float() - b.float()).abs() <= 1e-6 * b.float().abs() + 1e-9).all())
+
+
+@pytest.mark.parametrize("dedup", [False, True])
+def test_wide_static_kernel_equals_runtime_shape(dedup, monkeypatch):
+    """The reference's flag defaults (k=32, 256-128-64; PS:52,62) run a compile-time-shape row
+    kernel whose layer-0 forward streams two tiles per wave through one tile's registers and whose
+    layer-1 backward owns two tiles per wave.  Its k-order per tile is the runtime-shape kernel's,
+    so Adam + dropout through multi-step graphs match it to fp32 reorder bounds (dedup: the
+    per-tile gradient-row sums, which only the static kernel's LDS has room for at this shape)."""
+    monkeypatch.setenv("ROCFM_DEDUP", "1" if dedup else "0")
+    spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=32, layers=[256, 128, 64],
+                     keep_probs=[0.7] * 3, l2_reg=1e-3)
+    hp = OptHParams(name="Momentum", lr=0.02)
+    g = torch.Generator().manual_seed(33)
+    B = 200
+    pool = [_batch(B, 39, 3000, g) for _ in range(5)]
+    ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
+    out = {}
+    for generic in (True, False):
+        e = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=True,
+                        force_generic_kernels=generic)
+        assert e.dedup == (dedup and not generic)
+        e.attach_pool(ids, vals, labels)
+        e.train_steps(13, 4)
+        torch.cuda.synchronize()
+        e.check()
+        out[generic] = (e.emb.clone(), e.dense.clone(), e.prob[:B].clone())
+    for x, y in zip(out[True], out[False]):
+        d = (x - y).abs()
+        assert bool((d <= 1e-6 + 1e-4 * y.abs()).all()), d.max().item()

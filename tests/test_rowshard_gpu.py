@@ -145,14 +145,14 @@ def _single(update, nsteps, B=128, opt="Adam", disjoint=False):
     return single
 
 
-def _world1(update, mode, n=11, opt="Momentum", hot=0, staleness=0, disjoint=False):
+def _world1(update, mode, n=11, opt="Momentum", hot=0, staleness=0, disjoint=False, replicate=False):
     """A 1-rank FusedRowShard trained eagerly, per-step graphs or multi-step graphs (4 per graph)."""
     from rocfm.models.deepfm import init_params
     from rocfm.parallel.emb_shard import FusedRowShard
 
     spec, hp = _cfg(opt)
     eng = FusedRowShard(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3), embedding_update=update,
-                        use_graph=mode != "eager", hot_rows=hot, staleness=staleness)
+                        use_graph=mode != "eager", hot_rows=hot, staleness=staleness, replicate_table=replicate)
     batches = _batches(128, n, 11, disjoint)
     eng.attach_pool(torch.stack([b[0] for b in batches]).cuda(), torch.stack([b[1] for b in batches]).cuda(),
                     torch.stack([b[2] for b in batches]).cuda())
@@ -199,7 +199,7 @@ def test_fused_rowshard_world1_adam_smoke():
 
 
 def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0, staleness=0, hot=0, opt="Momentum",
-            shadow=0, fault=""):
+            shadow=0, fault="", replicate=False):
     # ROCFM_DP_PUSH=1: the X4 producer push is forced on although the ranks share this GPU (small
     # batches; the default keeps the copy push there).  shadow: collective-shadowed first steps
     # (0 = off, so the equivalence tests keep their graph coverage); fault: ROCFM_FAULT
@@ -214,7 +214,8 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     spec, hp = _cfg(opt)
     B = 64
     eng = FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, 3), embedding_update=update,
-                        use_graph=spg > 0, exchange=exchange, staleness=staleness, hot_rows=hot)
+                        use_graph=spg > 0, exchange=exchange, staleness=staleness, hot_rows=hot,
+                        replicate_table=replicate)
     assert eng.exchange == exchange, eng.exchange
     assert eng.fused_push == (exchange == "p2p" and hot == 0), eng.fused_push
     fused = eng.fused_push
@@ -241,6 +242,9 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     p, _ = eng.predict_batch(ids.cuda() if rank == 0 else ids[:0].cuda(), vals.cuda() if rank == 0 else vals[:0].cuda())
     if hot:
         assert eng.n_hot == hot
+    if replicate:  # the full replica equals the owners' shards on every rank
+        full = eng.emb_full.cpu()
+        assert torch.equal(full[:, :spec.embedding_size], P["fm_v"]) and torch.equal(full[:, spec.embedding_size], P["fm_w"])
     if rank == 0:
         torch.save({"P": dict(P), "pred": p.cpu(), **status}, out_path)
     eng.close()
@@ -249,10 +253,10 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
 
 
 def _run_ranks(tmp_path, world, update, exchange, steps, spg, staleness=0, hot=0, opt="Momentum", shadow=0,
-               fault=""):
+               fault="", replicate=False):
     out = str(tmp_path / f"rs{world}.pt")
     mp.start_processes(_worker, args=(world, _free_port(), update, out, exchange, steps, spg, staleness, hot, opt,
-                                      shadow, fault), nprocs=world, join=True, start_method="spawn")
+                                      shadow, fault, replicate), nprocs=world, join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
     assert got["consistent"], got["shadow"]
     return got
@@ -392,3 +396,42 @@ def test_rowshard_hot_rows_2ranks(tmp_path, exchange, spg):
     ids, vals, _ = _batches(100, 1, 5)[0]
     pr, _ = ref.predict_batch(ids.cuda(), vals.cuda())
     torch.testing.assert_close(got["pred"], pr.cpu(), rtol=1e-4, atol=1e-6)
+
+
+# ---- owner-sharded DP (parallelism=dp_owner: replicated table, owner-sharded embedding optimizer) ----
+@pytest.mark.parametrize("mode", ["eager", "graph", "multi"])
+def test_dp_owner_world1_equals_single(mode):
+    """dp_owner at world 1: the forward reads the full replica, the owner merge broadcasts every
+    updated row (X5) and row_scatter writes it back — Momentum, every element of every variable and
+    slot within fp32 reorder bounds of the single-GPU engine; the replica equals the shard."""
+    eng = _world1("sparse", mode, replicate=True)
+    ref = _single("sparse", 11, opt="Momentum")
+    _assert_params_tight(_tables(eng), _tables(ref))
+    P = eng.parameters_tf()
+    full = eng.emb_full.cpu()
+    assert torch.equal(full[:, :10], P["fm_v"]) and torch.equal(full[:, 10], P["fm_w"])
+
+
+@pytest.mark.parametrize("world,exchange,steps,spg", [(2, "rccl", 3, 0), (2, "p2p", 3, 0), (2, "p2p", 10, 4),
+                                                     (4, "p2p", 10, 4)])
+def test_dp_owner_ranks_equal_single_gpu_union_batch(tmp_path, world, exchange, steps, spg):
+    """2 and 4 ranks on one GPU: X1 + X3 + X4 in one hand-off, the owner merge pushing its updated
+    rows into every rank's X5 slot, row_scatter into every replica — equal to the single-GPU step on
+    the union batch (Momentum, tight), replicas bit-identical (checked by the worker)."""
+    got = _run_ranks(tmp_path, world, "sparse", exchange, steps, spg, replicate=True)
+    ref = _single("sparse", steps, B=64 * world, opt="Momentum")
+    _assert_params_tight(got["P"], ref.parameters_tf())
+
+
+@pytest.mark.parametrize("fault", ["", "corrupt_push:1"])
+def test_dp_owner_shadow_exchange(tmp_path, fault):
+    """The first 8 steps shadow every p2p exchange (X1, X3, X4, X5) with the collective; a corrupt
+    word is detected and every rank falls back to RCCL; the result equals the single GPU."""
+    steps = 13
+    got = _run_ranks(tmp_path, 2, "sparse", "p2p", steps, 4, shadow=8, fault=fault, replicate=True)
+    if fault:
+        assert got["shadow"] == "mismatch" and got["exchange"] == "rccl", got["shadow"]
+    else:
+        assert got["shadow"] == "ok" and got["exchange"] == "p2p", got["shadow"]
+    ref = _single("sparse", steps, B=128, opt="Momentum")
+    _assert_params_tight(got["P"], ref.parameters_tf())

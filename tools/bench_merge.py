@@ -7,6 +7,8 @@ the map mode (scatter into W×V position maps, then apply).  Both write a dense 
 (mode 1) so repeated launches leave the inputs unchanged.
 
     python tools/bench_merge.py [--V 1000000] [--B 1024] [--iters 200]
+
+It also times the owner-sharded DP merge (parallelism=dp_owner, owner_merge below).
 """
 import argparse
 import os
@@ -116,6 +118,86 @@ def main():
             torch.cuda.synchronize()
             outs.append(dg.clone())
         assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), W
+        owner_merge(H, a, W, lists, dev)
+
+
+def owner_merge(H, a, W, lists, dev):
+    """parallelism=dp_owner: the same W batches, but owner 0 merges only the rows it owns (id % W
+    == 0) — W source lists of ≈1/W of each export, as local rows id // W — and applies the row
+    optimizer (mode 0, Adam) with a broadcast list of the updated rows (X5); then every replica
+    scatters the W owners' lists (row_scatter).  Timed like the merges above."""
+    Vs = (a.V + W - 1) // W
+    own = [torch.unique(x[x % W == 0] // W) for x in lists]
+    cap = (max(max(len(x) for x in own), 1) + 3) // 4 * 4
+    keys = torch.full((W, cap), 0xFFFFFFFF, dtype=torch.int64)
+    for r, x in enumerate(own):
+        keys[r, : len(x)] = x.cpu()
+    keys32 = torch.from_numpy(keys.numpy().astype(np.uint32).view(np.int32)).to(dev)
+    counts = torch.tensor([len(x) for x in own], dtype=torch.int32, device=dev)
+    rows = torch.randn(W, cap, a.Kp, device=dev) * 1e-3
+    emb = torch.randn(Vs, a.Kp, device=dev) * 1e-2
+    s0, s1 = torch.zeros_like(emb), torch.zeros_like(emb)
+    step = torch.ones(1, dtype=torch.int64, device=dev)
+    lrt = torch.full((1,), 1e-3, device=dev)
+    capB = W * cap
+    bc = torch.zeros(4 + capB * (1 + a.Kp), device=dev)
+    p = H.MergeParams()
+    p.keys, p.key_stride = keys32.data_ptr(), cap
+    p.rows, p.row_stride = rows.data_ptr(), cap * a.Kp
+    p.counts, p.count_stride = counts.data_ptr(), 1
+    p.W, p.cap, p.Kp, p.K1 = W, cap, a.Kp, a.Kp - 1
+    p.key_div, p.Vmap = 1, Vs
+    pos = torch.full((W * Vs,), -1, dtype=torch.int32, device=dev)
+    rep = torch.full((Vs,), W, dtype=torch.int32, device=dev)
+    p.pos, p.rep = pos.data_ptr(), rep.data_ptr()
+    p.emb, p.s0, p.s1, p.step, p.mode = emb.data_ptr(), s0.data_ptr(), s1.data_ptr(), step.data_ptr(), 0
+    o = H.OptParams()
+    o.type, o.lr, o.beta1, o.beta2, o.eps, o.lrt = 0, 1e-3, 0.9, 0.999, 1e-8, lrt.data_ptr()  # Adam
+    p.opt, p.l2, p.grad_scale = o, 1e-4, 1.0 / W
+    p.bc_count, p.bc_keys, p.bc_rows = bc.data_ptr(), bc[4:].data_ptr(), bc[4 + capB:].data_ptr()
+    p.bc_cap, p.bc_mul, p.bc_add = capB, W, 0
+    s = torch.cuda.current_stream().cuda_stream
+    uniq = sum(len(x) for x in [torch.unique(torch.cat(own))])
+    # every replica's X5 receive side: W owners' lists of ≈ the union's 1/W each
+    recv = torch.zeros(W, 4 + capB * (1 + a.Kp), device=dev)
+    table = torch.zeros(a.V, a.Kp, device=dev)
+    for r in range(W):
+        recv[r, 0] = torch.tensor([uniq], dtype=torch.int32).view(torch.float32)[0]
+        recv[r, 4:4 + uniq] = (torch.arange(uniq, device=dev, dtype=torch.int32) * W + r).view(torch.float32)
+    sp = H.RowScatterParams()
+    sp.recv, sp.slot_stride, sp.W, sp.cap, sp.Kp = recv.data_ptr(), recv.shape[1], W, capB, a.Kp
+    sp.table, sp.rows = table.data_ptr(), a.V
+    res = {}
+    for name in ("search", "maps", "scatter"):
+        def run():
+            bc[:1].zero_()
+            if name == "search":
+                p.use_maps = 0
+                H.merge_search_apply(p, None, s)
+            elif name == "maps":
+                p.use_maps = 1
+                H.merge_scatter(p, s)
+                H.merge_search_apply(p, None, s)
+            else:
+                H.row_scatter(sp, s)
+        for _ in range(10):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = e0.elapsed_time(e1) * 1000 / a.iters
+    bc[:1].zero_()
+    p.use_maps = 0
+    H.merge_search_apply(p, None, s)
+    torch.cuda.synchronize()
+    n_up = int(bc[:1].view(torch.int32).item())
+    assert n_up == uniq, (n_up, uniq)  # one broadcast row per distinct owned id
+    print(f"  dp_owner W={W}: owner lists cap={cap} entries={int(counts.sum())} updated rows={uniq}: "
+          f"search+opt {res['search']:.2f} us, maps+opt {res['maps']:.2f} us, row_scatter (W lists) "
+          f"{res['scatter']:.2f} us")
 
 
 if __name__ == "__main__":
