@@ -83,7 +83,7 @@ class P2PExchange:
     """
 
     def __init__(self, slot_floats: int, device, group=None, kind: int = KIND_UNCACHED,
-                 spin_limit: int = 1 << 30, extra_floats: int = 0):
+                 spin_limit: Optional[int] = None, extra_floats: int = 0):
         H = self.H = _hip()
         self.group = group
         self.W = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -94,7 +94,9 @@ class P2PExchange:
         self.slot = (int(slot_floats) + 3) // 4 * 4
         # local floats behind the W slots (never pushed; e.g. the row-shard hot-row replica)
         self.extra = (int(extra_floats) + 3) // 4 * 4
-        self.spin_limit = int(spin_limit)
+        # polls per wave before a wait gives up and raises the sticky error flag; ROCFM_SPIN_LIMIT
+        # lowers it for rehearsals that force producer pushes onto one shared GPU (fail fast, loud)
+        self.spin_limit = int(spin_limit if spin_limit is not None else os.environ.get("ROCFM_SPIN_LIMIT", 1 << 30))
         self.kind = kind
         self._own: List[int] = []
         self._opened: List[int] = []

@@ -119,7 +119,10 @@ def test_bench_rehearsal_2_ranks_fused_push():
     """The fused push (producers store into the peers' slots from the step tail) through bench.py
     at the reference batch, 2 ranks sharing the GPU (forced: ROCFM_DP_PUSH=1)."""
     j, log = _bench(["--gpus", "2", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
-                    {"ROCFM_BENCH_BACKEND": "gloo", "ROCFM_DP_PUSH": "1"})
+                    {"ROCFM_BENCH_BACKEND": "gloo", "ROCFM_DP_PUSH": "1",
+                     # forced producer push on a shared GPU: a starved wait ends in ≈4 s with the
+                     # sticky error flag (check() raises, bench exits non-zero) instead of hanging
+                     "ROCFM_SPIN_LIMIT": str(1 << 26)})
     assert j["n_gpus"] == 2 and j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is True, j
     assert j["value"] > 0 and "falling back" not in log, log[-2000:]
 

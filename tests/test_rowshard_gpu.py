@@ -204,7 +204,8 @@ def _worker(rank, world, port, update, out_path, exchange="rccl", steps=3, spg=0
     # batches; the default keeps the copy push there).  shadow: collective-shadowed first steps
     # (0 = off, so the equivalence tests keep their graph coverage); fault: ROCFM_FAULT
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH="1", ROCFM_SHADOW_STEPS=str(shadow),
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_DP_PUSH="1", ROCFM_SPIN_LIMIT=str(1 << 26),
+                      ROCFM_SHADOW_STEPS=str(shadow),
                       ROCFM_FAULT=fault)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
