@@ -346,3 +346,31 @@ def test_decoded_cache_epochs_equal_loader(tmp_path):
         assert len(got) == len(exp)
         assert all(all(torch.equal(a, b) for a, b in zip(x, y)) for x, y in zip(got, exp))
         assert dc.complete() and dc.num_batches() == nb
+
+
+@pytest.mark.parametrize("threads,shards", [(1, 1), (4, 1), (4, 3)])
+def test_piecewise_index_matches_decode_file(tmp_path, threads, shards):
+    """The loader indexes a file's first 2 MB as its own piece (the decoders start before the whole
+    file is walked) and the rest as a second piece: the piece boundary falls inside a record, and
+    the batches (every shard, skip, epochs) still equal the whole-file decode in record order."""
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+
+    p1, p2 = str(tmp_path / "big.tfrecords"), str(tmp_path / "small.tfrecords")
+    write_synthetic_tfrecord(p1, 9000, 50000, 39, seed=3)  # ≈2.8 MB: two pieces
+    write_synthetic_tfrecord(p2, 700, 50000, 39, seed=4)
+    assert os.path.getsize(p1) > (2 << 20)
+    Ls, Is, Vs = zip(*(T.decode_file(p, 39, 50000) for p in (p1, p2)))
+    L, I, V = torch.cat(Ls), torch.cat(Is), torch.cat(Vs)
+    for r in range(shards):
+        ds = T.TFRecordDataset([p1, p2], 39, 256, 50000, num_epochs=2, shard_count=shards, shard_index=r,
+                               num_threads=threads, pin_memory=False)
+        got = [(ids.clone(), vals.clone(), lab.clone()) for ids, vals, lab in ds]
+        sel = torch.arange(r, len(L), shards)
+        n = len(sel) // 256 * 256
+        exp_i = I[sel][:n].reshape(-1, 256, 39)
+        assert len(got) == 2 * len(exp_i)
+        for k, (ids, vals, lab) in enumerate(got):
+            e = k % len(exp_i)
+            assert torch.equal(ids, exp_i[e])
+            assert torch.equal(vals, V[sel][:n].reshape(-1, 256, 39)[e])
+            assert torch.equal(lab, L[sel][:n].reshape(-1, 256)[e])
