@@ -179,12 +179,8 @@ size_t resync(const uint8_t* buf, size_t n, size_t from, size_t limit) {
 // back to the sequential scan_records, which also produces the reference error semantics.
 // TFRecord framing is a length chain; a single thread walking it is bound by one memory latency
 // per record (≈70-90 ns), i.e. it cannot feed more than ≈12 M records/s.
-//
-// [begin, end_range): the frames whose header starts in that byte range (begin must be a frame
-// start: 0 or the `next` of the previous range); `next` returns the first frame start at or past
-// end_range (n when the range reaches the end of the file), where the following range begins.
-bool index_parallel(const uint8_t* buf, size_t n, size_t begin, size_t end_range, bool verify, bool verify_data,
-                    bool skip_bad, int parts, std::vector<RecordRef>* out, size_t* bad, size_t* next) {
+bool index_parallel(const uint8_t* buf, size_t n, bool verify, bool verify_data, bool skip_bad, int parts,
+                    std::vector<RecordRef>* out, size_t* bad) {
   struct Part {
     size_t first = 0, end = 0, bad = 0;
     bool error = false;
@@ -194,9 +190,8 @@ bool index_parallel(const uint8_t* buf, size_t n, size_t begin, size_t end_range
   std::vector<Part> P(parts);
   auto run = [&](int k) {
     Part& pt = P[k];
-    const size_t span = end_range - begin;
-    const size_t s = begin + span * k / parts, e = begin + span * (k + 1) / parts;
-    size_t p = (k == 0) ? begin : resync(buf, n, s, (size_t)16 << 20);
+    const size_t s = n * k / parts, e = n * (k + 1) / parts;
+    size_t p = (k == 0) ? 0 : resync(buf, n, s, (size_t)16 << 20);
     pt.first = p;
     pt.recs.reserve((e - s) / 256 + 16);
     while (p < e && p + 12 <= n) {
@@ -239,12 +234,9 @@ bool index_parallel(const uint8_t* buf, size_t n, size_t begin, size_t end_range
   for (auto& t : th) t.join();
   for (int k = 0; k < parts; ++k) {
     if (P[k].error) return false;
-    if (k + 1 < parts && P[k].end != P[k + 1].first) return false;
+    const size_t next = (k + 1 < parts) ? P[k + 1].first : n;
+    if (P[k].end != next) return false;
   }
-  // the last part's chain: exactly to the end of the file, or past the range into a whole frame
-  const size_t last = P[parts - 1].end;
-  if (end_range >= n ? last != n : (last < end_range || last >= n)) return false;
-  *next = last;
   size_t tot = 0;
   for (auto& pt : P) tot += pt.recs.size();
   out->reserve(out->size() + tot);
@@ -267,44 +259,27 @@ void BatchLoader::reader_main() {
       std::shared_ptr<Chunk> chunk;
       std::vector<RecordRef> recs;
       size_t bad = 0;
-      size_t next = 0;  // where the file's next piece starts (chunk->size: indexed to the end)
     };
     const int parts = std::max(1, opt_.num_threads);
     // deferred data CRCs (defer_crc_, see loader.h): the walk checks the framing (length CRCs)
     // only; each kept record's data CRC is checked by the decoder that decodes it
     const bool vdata = !defer_crc_;
-    // A file is indexed in pieces, one piece ahead of the emission: the job's first piece is
-    // short (kFirstPiece bytes, ≈6 batches of Criteo-shape records), so the decoders start after
-    // a 2 MB walk instead of a whole-file walk (measured on the box: 4-6 ms to the first group of
-    // 16 batches for 22 MB files, 13-15 ms for 170 MB files); every later piece is the rest of
-    // its file, walked by the parallel indexer while the previous piece is being decoded.
-    constexpr size_t kFirstPiece = (size_t)2 << 20;
-    auto index = [this, parts, vdata](const std::string& path, std::shared_ptr<Chunk> chunk, size_t from,
-                                      size_t limit) {
+    auto index = [this, parts, vdata](const std::string& path) {
       Indexed ix;
-      ix.chunk = chunk ? chunk : map_file(path);
+      ix.chunk = map_file(path);
       const size_t n = ix.chunk->size;
-      if (from >= n) {
-        ix.next = n;
-        return ix;
-      }
-      const size_t to = (limit >= n - from) ? n : from + limit;
-      const int np = (int)std::min<size_t>((size_t)parts, std::max<size_t>(1, (to - from) >> 22));
-      if (!index_parallel(ix.chunk->data, n, from, to, opt_.verify_crc, vdata, opt_.skip_bad, np, &ix.recs, &ix.bad,
-                          &ix.next)) {
+      const int np = (int)std::min<size_t>((size_t)parts, std::max<size_t>(1, n >> 22));
+      if (np < 2 ||
+          !index_parallel(ix.chunk->data, n, opt_.verify_crc, vdata, opt_.skip_bad, np, &ix.recs, &ix.bad)) {
         if (np >= 2) ++fallbacks_;
         ix.recs.clear();
         ix.bad = 0;
-        // the sequential walk of the rest of the file (the reference error semantics; offsets in
-        // its messages count from this piece's start)
-        scan_records(ix.chunk->data + from, n - from, opt_.verify_crc, opt_.skip_bad, &ix.recs, &ix.bad, vdata);
-        ix.next = n;
+        scan_records(ix.chunk->data, n, opt_.verify_crc, opt_.skip_bad, &ix.recs, &ix.bad, vdata);
       }
       return ix;
     };
     std::future<Indexed> pending;
-    if (!opt_.stream_mode && !opt_.files.empty())
-      pending = std::async(std::launch::async, index, opt_.files[0], nullptr, (size_t)0, kFirstPiece);
+    if (!opt_.stream_mode && !opt_.files.empty()) pending = std::async(std::launch::async, index, opt_.files[0]);
     for (int epoch = 0; opt_.num_epochs < 0 || epoch < opt_.num_epochs; ++epoch) {
       Job cur;
       cur.epoch = epoch;
@@ -369,20 +344,11 @@ void BatchLoader::reader_main() {
           }
           if (f != stdin) fclose(f);
         } else {
-          while (true) {
-            Indexed ix = pending.get();  // this piece's index (started one piece ahead)
-            const bool more = ix.next < ix.chunk->size;
-            if (more)
-              pending = std::async(std::launch::async, index, path, ix.chunk, ix.next, SIZE_MAX);
-            else if (fi + 1 < opt_.files.size() || epoch + 1 < opt_.num_epochs || opt_.num_epochs < 0)
-              pending = std::async(std::launch::async, index, opt_.files[(fi + 1) % opt_.files.size()], nullptr,
-                                   (size_t)0, SIZE_MAX);
-            bad_ += ix.bad;
-            for (auto& r : ix.recs) take(r, ix.chunk);
-            if (!more) break;
-            std::lock_guard<std::mutex> g(mu_);
-            if (stop_) return;
-          }
+          Indexed ix = pending.get();  // this file's index (started one file ahead)
+          if (fi + 1 < opt_.files.size() || epoch + 1 < opt_.num_epochs || opt_.num_epochs < 0)
+            pending = std::async(std::launch::async, index, opt_.files[(fi + 1) % opt_.files.size()]);
+          bad_ += ix.bad;
+          for (auto& r : ix.recs) take(r, ix.chunk);
         }
         ++fi;
       }
