@@ -368,11 +368,22 @@ __device__ __forceinline__ void merge_search_body(const MergeParams& p, const in
   if (W > 1) {
     if constexpr (WMAX <= 8) {
       int lo[WMAX], len[WMAX], at[WMAX];
+      // bucket directories (the sorted export's dir[b] = first position whose key ≥ b·bucket_div):
+      // each search starts inside the key's bucket — one round of directory loads, then
+      // ≈log2(bucket) instead of ≈log2(cap) dependent halvings
+      const bool use_dir = p.dirs != nullptr && p.nb > 0;
+      const int bk = use_dir ? (int)min(key / p.bucket_div, (uint32_t)p.nb - 1u) : 0;
 #pragma unroll
       for (int q = 0; q < WMAX; ++q) {
         lo[q] = 0;
         at[q] = -1;
         len[q] = (q < W && q != r) ? len_of(p, q) : 0;
+        if (use_dir && len[q] > 0) {
+          const int32_t* d = p.dirs + (size_t)q * p.dir_stride;
+          const int b0 = min(max(d[bk], 0), len[q]), b1 = min(max(d[bk + 1], 0), len[q]);
+          lo[q] = b0;
+          len[q] = max(b1 - b0, 0);
+        }
       }
       for (;;) {
         bool any = false;

@@ -90,6 +90,22 @@ def range_merge_buckets(W: int, cap: int) -> int:
     return max(64, -(-W * cap // 192))
 
 
+# With bucket directories the search merge beats the position maps up to 4 ranks
+# (tools/bench_merge.py, profiles/r3_session3_search_dir.md: W=2 7.6 vs maps 9.1 µs, W=4 9.5 vs
+# 10.3, W=8 14.6 vs 14.2), so DP keeps the sorted export + search through W = 4.
+SEARCH_DIR_MAX_W = 4
+
+
+def search_dir_buckets(W: int, V: int) -> int:
+    """Key buckets of the directory the sorted DP export writes for the SEARCH merge (2 ≤ W ≤
+    SEARCH_DIR_MAX_W): each entry's binary search in the other ranks' lists starts inside its
+    key's bucket (≈log2(bucket) halvings instead of ≈log2(cap)): 10.2 → 7.6 µs at W = 2 with 8192
+    buckets.  0 = off (ROCFM_SEARCH_DIR=0, one rank, or more than SEARCH_DIR_MAX_W ranks)."""
+    if W < 2 or W > SEARCH_DIR_MAX_W or os.environ.get("ROCFM_SEARCH_DIR", "1") == "0":
+        return 0
+    return max(64, min(8192, V // 16))
+
+
 def range_merge_enabled(W: int) -> bool:
     """The range merge (bucket directories written by the sorted export; merge.hip range mode) for
     the multi-step DP path with ≥ 2 ranks — opt-in (ROCFM_MERGE=range).  Measured against the
@@ -277,6 +293,7 @@ class FusedDataParallel:
         self.force = force_collectives()
         self.exchange = "rccl"  # DP all-gather transport (mode dp: p2p.open_exchanges may pick "p2p")
         self.range = False  # range merge (mode dp, set below)
+        self.sdir = False  # bucket directory for the search merge (mode dp, set below)
         # replicas start identical: broadcast rank 0's variables (HVD:418)
         if self.world > 1:
             from .dist import broadcast_tensors
@@ -302,9 +319,13 @@ class FusedDataParallel:
             Kp = e.Kp
             # range merge (multi-step path): the sorted export also writes a bucket directory
             self.range = range_merge_enabled(self.world) and Kp <= H.tail_max_kp()
-            self.nb = range_merge_buckets(self.world, cap) if self.range else 0
-            self.bdiv = -(-e.V // self.nb) if self.range else 0
-            ndir = (self.nb + 1 + 3) // 4 * 4 if self.range else 0
+            # search merge (W ≤ SEARCH_MAX_W, multi-step path): the directory narrows the searches
+            self.sdir = (not self.range and mode == "dp" and Kp <= H.tail_max_kp()
+                         and search_dir_buckets(self.world, e.V) > 0)
+            self.nb = (range_merge_buckets(self.world, cap) if self.range
+                       else search_dir_buckets(self.world, e.V) if self.sdir else 0)
+            self.bdiv = -(-e.V // self.nb) if self.nb else 0
+            ndir = (self.nb + 1 + 3) // 4 * 4 if self.nb else 0
             # send buffer (f32 words): [MLP grads P | pad to 4 | count (int32) + pad 3 | dir nb+1 (int32,
             # range merge) | keys cap (int32) | rows cap*Kp]  (every part from the count on 16-B aligned)
             self.off_cnt = (P + 3) // 4 * 4
@@ -589,7 +610,8 @@ class FusedDataParallel:
         self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
-        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and (self.world <= SEARCH_MAX_W or self.range)
+        self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and (self.world <= SEARCH_MAX_W or self.range
+                                                                            or self.sdir)
         e._build_multi(Smax, heads=self.m_sorted)
         e._m_pool = e.pool_ids
         S_, n = e.mS, e.n_lookup
@@ -618,7 +640,7 @@ class FusedDataParallel:
                 ex.out_cap = self.cap
                 if self.m_sorted:
                     ex.chunk_heads, ex.nch = e.m_chd[q, k * e.m_nch:].data_ptr(), e.m_nch
-                if self.range:  # + the bucket directory of the exported keys
+                if self.range or (self.sdir and self.m_sorted):  # + the bucket directory of the exported keys
                     ex.dir_nb, ex.dir_div = self.nb, self.bdiv
                     ex.out_dir, ex.push_off_dir = self.send[self.off_dir:].data_ptr(), self.off_dir
                 self._set_push(rows, wp, ex)
@@ -629,7 +651,7 @@ class FusedDataParallel:
                           "overflow", "dense_grad", "touched", "hash_slots", "hkeys", "hrep", "hpos", "tbl_bf16"):
                     setattr(mg, f, getattr(src, f))
                 mg.opt, mg.step = ep.opt, ep.step  # this step's global_step / lr_t
-                if self.range:
+                if self.range or (self.sdir and self.m_sorted):
                     mg.dirs, mg.dir_stride = self._recv_ptr + 4 * self.off_dir, self.S
                     mg.nb, mg.bucket_div = self.nb, self.bdiv
                 rows.zero_word = self.send[self.off_cnt:].data_ptr()
