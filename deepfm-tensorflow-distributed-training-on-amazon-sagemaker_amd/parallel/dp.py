@@ -103,6 +103,8 @@ def search_dir_buckets(W: int, V: int) -> int:
     buckets.  0 = off (ROCFM_SEARCH_DIR=0, one rank, or more than SEARCH_DIR_MAX_W ranks)."""
     if W < 2 or W > SEARCH_DIR_MAX_W or os.environ.get("ROCFM_SEARCH_DIR", "1") == "0":
         return 0
+    if os.environ.get("ROCFM_MERGE", "auto") != "auto":  # a forced merge (direct / hash / range) is kept
+        return 0
     return max(64, min(8192, V // 16))
 
 

@@ -109,7 +109,7 @@ def test_fused_dp_equals_single_gpu_union_batch(tmp_path, mode, exchange, steps,
 @pytest.mark.parametrize("update", ["sparse", "exact"])
 def test_fused_dp_world4_p2p_graphs(tmp_path, update):
     """4 ranks on one GPU: the p2p push fans out to 3 peers and the merge sums 4 rank lists (the
-    W>2 paths the 8-GPU node runs), through multi-step graphs."""
+    directory-narrowed search merge, SEARCH_DIR_MAX_W), through multi-step graphs."""
     _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
 
 
@@ -184,6 +184,15 @@ def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, pus
     for got, exp in zip(dp["slots"], single.emb_slots):  # the momentum accumulators too
         _assert_tight(got, exp)
     return dp
+
+
+@pytest.mark.parametrize("update", ["sparse", "exact"])
+def test_fused_dp_world4_direct_maps(tmp_path, monkeypatch, update):
+    """The position-map merge (scatter + apply launches) that DP runs beyond SEARCH_DIR_MAX_W ranks
+    (the 8-GPU node), forced at 4 ranks (ROCFM_MERGE=direct), multi-step graphs and the p2p push ≡
+    the single-GPU union batch."""
+    monkeypatch.setenv("ROCFM_MERGE", "direct")
+    _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
 
 
 @pytest.mark.parametrize("update", ["sparse", "exact"])
