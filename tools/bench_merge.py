@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--Kp", type=int, default=12)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--hash", action="store_true")
+    ap.add_argument("--sdir_buckets", type=int, default=0, help="search+dir bucket count (0: dp's default)")
+    ap.add_argument("--worlds", default="1,2,4,8")
     a = ap.parse_args()
     H = require_hip()
     dev = torch.device("cuda")
@@ -45,7 +47,7 @@ def main():
     # --hash: keys are a bijective multiplicative hash of the ids (id · odd mod 2^bits), spreading
     # the Zipf-clustered ids uniformly over the key space (what the range merge's buckets need)
     bits = max(1, (a.V - 1).bit_length())
-    for W in (1, 2, 4, 8):
+    for W in [int(x) for x in a.worlds.split(",")]:
         lists = [gen.batch(a.B, dev, g)[0].flatten().to(torch.int64) for _ in range(W)]
         if a.hash:
             lists = [(x * 0x9E3779B1) & ((1 << bits) - 1) for x in lists]
@@ -82,7 +84,7 @@ def main():
             dirs[r] = torch.searchsorted(x.cpu(), bounds).to(torch.int32)
         dirs = dirs.to(dev)
         # search+dir: the search merge's own directory (the bucket count of dp.search_dir_buckets)
-        snb = max(64, min(8192, Vk // 16))
+        snb = a.sdir_buckets or max(64, min(8192, Vk // 16))
         sdiv = (Vk + snb - 1) // snb
         sb = torch.arange(snb + 1, dtype=torch.int64) * sdiv
         sdirs = torch.stack([torch.searchsorted(x.cpu(), sb).to(torch.int32) for x in lists]).to(dev)
