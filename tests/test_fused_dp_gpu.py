@@ -186,6 +186,14 @@ def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, pus
     return dp
 
 
+def test_fused_dp_world8_rehearsal(tmp_path):
+    """Eight ranks on one GPU (the node's rank count): the push fans out to 7 peers (the copy push:
+    eight ranks' spinning producers would compete for one GPU's CUs), the merge takes the
+    position-map path DP runs beyond SEARCH_DIR_MAX_W, multi-step graphs; ≡ the single-GPU union
+    batch, replicas bit-identical."""
+    _check_dp_vs_single(tmp_path, 8, "dp", "p2p", 11, 4, "sparse", push="0")
+
+
 @pytest.mark.parametrize("update", ["sparse", "exact"])
 def test_fused_dp_world4_direct_maps(tmp_path, monkeypatch, update):
     """The position-map merge (scatter + apply launches) that DP runs beyond SEARCH_DIR_MAX_W ranks
