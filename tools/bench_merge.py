@@ -2,11 +2,12 @@
 
 W rank exports are synthesised from W synthetic Criteo-shape batches (unique ids of each batch,
 ascending — the sorted DP export), laid out like the gathered receive buffer; the two merges are
-timed on them with HIP events: the search mode (one launch, binary search in the other lists) and
-the map mode (scatter into W×V position maps, then apply).  Both write a dense gradient table
+timed on them with HIP events: the search mode (one launch, binary search in the other lists), the
+same search started inside each key's bucket of a directory (search+dir, what DP runs at 2-4
+ranks), the map mode (scatter into W×V position maps, then apply) and the range mode.  Both write a dense gradient table
 (mode 1) so repeated launches leave the inputs unchanged.
 
-    python tools/bench_merge.py [--V 1000000] [--B 1024] [--iters 200]
+    python tools/bench_merge.py [--V 1000000] [--B 1024] [--iters 200] [--worlds 1,2,4,8] [--sdir_buckets N]
 
 It also times the owner-sharded DP merge (parallelism=dp_owner, owner_merge below).
 """
