@@ -80,7 +80,9 @@ def parse():
                          "(one GPU)")
     ap.add_argument("--data_dir", default="", help="--input tfrecord: directory for the generated files (default: a "
                                                    "temporary directory, removed afterwards)")
-    ap.add_argument("--loader_threads", type=int, default=16)
+    ap.add_argument("--loader_threads", type=int, default=8)
+    ap.add_argument("--host_decode", action="store_true",
+                    help="--input tfrecord: parse the Examples on the host (default: raw payloads, parsed on the GPU)")
     ap.add_argument("--loader_hold", type=int, default=2,
                     help="--input tfrecord: decoded groups held ahead of the GPU (pinned ring of (hold+2)*S batches)")
     ap.add_argument("--json_out", default="")
@@ -287,12 +289,22 @@ def main():
         "replicas_consistent": replicas_ok,
         "shadow_exchange": (shadow.status if shadow is not None else None),
     }
+    if (world > 1 and a.engine == "fused" and hasattr(eng, "phase_windows") and not a.no_secondary):
+        try:  # per-rank device phase times of the headline's DP step (diagnostic windows, after it)
+            out["phase_ms"] = eng.phase_windows(64, a.steps_per_graph)
+        except Exception as e:  # noqa: BLE001 — a diagnostic never costs the headline
+            out["phase_ms_error"] = f"{type(e).__name__}: {e}"[:300]
+        _ctrl_barrier()
     if hasattr(eng, "close"):
         eng.close()  # graphs holding RCCL collectives must go before the process group
     if (not pg and a.engine == "fused" and a.parallelism == "auto" and not a.no_secondary
             and a.feature_size <= 20_000_000):
         del eng, run
         out.update(secondary_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels)))
+    elif world > 1 and a.engine == "fused" and a.parallelism == "auto" and not a.no_secondary:
+        del eng, run
+        out.update(multi_gpu_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels), world, rank,
+                                     backend, out))
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -302,6 +314,139 @@ def main():
     if pg:
         dist.barrier()
         dist.destroy_process_group()
+
+
+_CTRL = []
+
+
+def _ctrl_barrier():
+    """Host-side barrier on a gloo group (never queued behind GPU work)."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return
+    if not _CTRL:
+        _CTRL.append(dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else None)
+    dist.barrier(group=_CTRL[0])
+
+
+def _rank_span(dt, dev, backend):
+    """(max, min) over ranks of a timed window."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([dt, -dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0].item()), -float(t[1].item())
+
+
+def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, headline):
+    """N > 1: secondary windows beside the headline (DP over the p2p push), each on a fresh engine
+    and fenced — a window that fails or overruns becomes an error string, never a lost headline:
+
+    * ``rccl``: the same DP step with the exchange on RCCL (all-gather captured in the graphs), the
+      transport A/B of the node;
+    * ``rowshard``: config 4 — the PS-equivalent row-sharded table at 100M rows
+      (``…multiInstance.py:461-521``), p2p all-to-alls.
+    Every window reports its own replica check and p2p shadow status.  A watchdog bounds the
+    windows (ROCFM_BENCH_SECONDARY_S, default 300 s): on expiry rank 0 prints the headline with
+    the error and every rank exits."""
+    import threading
+
+    import torch
+
+    budget = float(os.environ.get("ROCFM_BENCH_SECONDARY_S", "300"))
+    state = {"window": None, "done": False}
+    out = {}
+
+    def expire():
+        if state["done"]:
+            return
+        if rank == 0:
+            h = dict(headline)
+            h.update(out)
+            h["secondary_error"] = f"watchdog: window {state['window']} overran {budget:.0f} s"
+            print(json.dumps(h), flush=True)
+            if a.json_out:
+                with open(a.json_out, "w") as f:
+                    f.write(json.dumps(h) + "\n")
+        os._exit(0)
+
+    wd = threading.Timer(budget, expire)
+    wd.daemon = True
+    wd.start()
+    S = a.steps_per_graph
+    B = a.batch_size
+
+    def run_window(name, build):
+        state["window"] = name
+        err = None
+        res = {}
+        eng = None
+        try:
+            eng = build()
+            eng.attach_pool(*pool)
+            eng.set_lr_scale(float(world))
+            eng.train_steps(a.warmup, S)
+            while getattr(eng, "shadow", None) is not None and eng.shadow.active:
+                eng.train_step()
+            eng.precapture(a.steps, S)
+            torch.cuda.synchronize()
+            _ctrl_barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.train_steps(a.steps, S)
+            torch.cuda.synchronize()
+            _ctrl_barrier()
+            dt = time.perf_counter() - t0
+            dmax, dmin = _rank_span(dt, dev, backend)
+            eng.check(replicas=False)
+            res = {"examples_per_sec": round(B * world * a.steps / dmax, 1),
+                   "ms_per_step": round(dmax / a.steps * 1e3, 4),
+                   "rank_ms_per_step_min": round(dmin / a.steps * 1e3, 4),
+                   "replicas_consistent": bool(eng.verify_replicas()),
+                   "shadow_exchange": eng.shadow.status if getattr(eng, "shadow", None) is not None else None,
+                   "exchange": getattr(eng, "exchange", None),
+                   "fused_push": bool(getattr(eng, "fused_push", False))}
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"[:300]
+        finally:
+            if eng is not None and hasattr(eng, "close"):
+                try:
+                    eng.close()
+                except Exception:  # noqa: BLE001
+                    pass
+            del eng
+            torch.cuda.empty_cache()
+        _ctrl_barrier()
+        if err is not None:
+            out[f"{name}_error"] = err
+        for k, v in res.items():
+            out[f"{name}_{k}"] = v
+
+    from rocfm.parallel.dp import FusedDataParallel, pool_exchange_capacity
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    pool_ids = pool[0]
+    cap = pool_exchange_capacity(pool_ids, 1)
+    run_window("rccl", lambda: FusedDataParallel(spec, hp, B, dev, params=params, mode="dp", seed=a.seed,
+                                                 capacity=cap, compute_dtype=a.compute_dtype, exchange="rccl"))
+    from rocfm.data.synthetic import SyntheticCriteo
+    from rocfm.models.deepfm import ModelSpec
+
+    V4 = 100_000_000
+    spec4 = ModelSpec(V4, spec.field_size, spec.embedding_size, spec.layers, spec.keep_probs, l2_reg=spec.l2_reg)
+    gen = SyntheticCriteo(V4, spec.field_size, seed=a.seed)
+    g = torch.Generator(device=dev).manual_seed(a.seed * 1000 + rank)
+    p4 = [gen.batch(B, dev, g) for _ in range(min(a.pool, 16))]
+    pool = (torch.stack([x[0] for x in p4]), torch.stack([x[1] for x in p4]), torch.stack([x[2] for x in p4]))
+    cap4 = pool_exchange_capacity(pool[0], world)
+    run_window("rowshard", lambda: FusedRowShard(spec4, hp, B, dev, params=None, seed=a.seed, capacity=cap4,
+                                                 compute_dtype=a.compute_dtype))
+    out["rowshard_feature_size"] = V4
+    state["done"] = True
+    wd.cancel()
+    return out
 
 
 def secondary_windows(a, spec, hp, params, dev, pool):
@@ -333,18 +478,52 @@ def secondary_windows(a, spec, hp, params, dev, pool):
     del eng
     gc.collect()
     torch.cuda.empty_cache()
-    # the loader-fed window streams at least 256 steps: a 20-step window is dominated by starting
-    # the decoders (measured: 4.3 M ex/s loader-alone over 20 batches vs 27-36 M over hundreds)
+    # the reference's own shapes (sparse update, same window): the notebook job (117,581 × 32,
+    # MLP 128-64-32; deepfm-sagemaker-hvd-gpu.ipynb:94-103) and the scripts' flag defaults
+    # (embedding_size 32, deep_layers 256,128,64; …multiInstance.py:52,62)
+    from rocfm.data.synthetic import SyntheticCriteo
+    from rocfm.models.deepfm import ModelSpec, init_params
+
+    for name, layers in (("notebook", [128, 64, 32]), ("refdefaults", [256, 128, 64])):
+        try:
+            sp = ModelSpec(117581, a.field_size, 32, layers, [0.5] * 3, l2_reg=spec.l2_reg)
+            gen = SyntheticCriteo(117581, a.field_size, seed=a.seed)
+            g = torch.Generator(device=dev).manual_seed(a.seed)
+            pb = [gen.batch(a.batch_size, dev, g) for _ in range(a.pool)]
+            e2 = FusedDeepFM(sp, hp, a.batch_size, dev, params=init_params(sp, a.seed), seed=a.seed,
+                             compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
+            e2.attach_pool(torch.stack([x[0] for x in pb]), torch.stack([x[1] for x in pb]),
+                           torch.stack([x[2] for x in pb]))
+            e2.train_steps(a.warmup, S)
+            e2.precapture(a.steps, S)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e2.train_steps(a.steps, S)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            e2.check()
+            out[f"{name}_examples_per_sec"] = round(a.batch_size * a.steps / dt, 1)
+            out[f"{name}_ms_per_step"] = round(dt / a.steps * 1e3, 4)
+            del e2, pb
+        except Exception as e:  # noqa: BLE001 — a secondary window never costs the headline
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
+        gc.collect()
+        torch.cuda.empty_cache()
+    # the loader-fed window: >= 2048 steps streamed from the TFRecord files (several epochs of a
+    # 512-batch file set), warm-up with the same ring and graph set, so the window holds no
+    # graph rebuild or capture; the time to the first graph is reported separately
     import copy
 
     ta = copy.copy(a)
-    ta.steps, ta.warmup, ta.steps_per_graph = max(256, a.steps), max(16, a.warmup), 16
-    t = measure_tfrecord(ta, spec, hp, params, dev)
-    out["tfrecord_steps"] = ta.steps
-    out["tfrecord_examples_per_sec"] = t["value"]
-    out["tfrecord_ms_per_step"] = t["ms_per_step"]
-    out["tfrecord_input_stall_fraction"] = t["input_stall_fraction"]
-    out["tfrecord_loader_alone_examples_per_sec"] = t["loader_alone_examples_per_sec"]
+    ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(32, a.warmup), 16
+    try:
+        t = measure_tfrecord(ta, spec, hp, params, dev)
+        out["tfrecord_steps"] = ta.steps
+        for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
+                  "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode"):
+            out["tfrecord_" + ("examples_per_sec" if k == "value" else k)] = t.get(k)
+    except Exception as e:  # a secondary window never costs the headline
+        out["tfrecord_error"] = f"{type(e).__name__}: {e}"[:400]
     return out
 
 
@@ -360,9 +539,14 @@ def bench_tfrecord(a, spec, hp, params, dev, rank):
 
 def measure_tfrecord(a, spec, hp, params, dev):
     """Loader-fed end-to-end throughput on one GPU (the reference's tf.data chain is inside its
-    training loop: PS:147-165, HVD:128-159).  Files hold exactly W + K batches; the timed region
-    is the K steps' train_stream call — it starts the C++ decoders (skipping the W warm-up batches
-    undecoded) and ends when the last step has run, so pipeline fill and input stalls count."""
+    training loop: PS:147-165, HVD:128-159): synthetic Criteo-shape TFRecord files (with their
+    record indexes) → C++ loader (frames + CRCs; raw mode copies the Example payloads, the GPU
+    parses them — ``--host_decode`` parses on the host instead) → pinned ring → HBM ring →
+    multi-step graphs.  The files hold at most 512 batches; longer windows repeat them as epochs
+    (the reference's ``repeat(num_epochs)``).  Warm-up trains W batches through the SAME ring and
+    graph set, so the timed train_stream call rebuilds nothing: it starts a fresh loader (thread
+    start, file mapping, first decode = the reported ``fill_ms``, time to the first graph launch)
+    and ends when the last step has run."""
     import shutil
     import tempfile
 
@@ -378,7 +562,8 @@ def measure_tfrecord(a, spec, hp, params, dev):
     own = not a.data_dir
     d = a.data_dir or tempfile.mkdtemp(prefix="rocfm_bench_")
     os.makedirs(d, exist_ok=True)
-    nrec = (a.warmup + a.steps) * B
+    nbat = min(512, a.warmup + a.steps)  # batches in the file set (one epoch)
+    nrec = nbat * B
     files, per = [], (nrec + 3) // 4
     t0 = time.perf_counter()
     for i in range(4):  # 4 files, like sharded S3 objects
@@ -390,20 +575,28 @@ def measure_tfrecord(a, spec, hp, params, dev):
             write_synthetic_tfrecord(p, m, a.feature_size, F, seed=a.seed + i)
         files.append(p)
     gen_s = time.perf_counter() - t0
+    raw = not getattr(a, "host_decode", False)
 
-    def dataset():
-        return TFRecordDataset(files, F, B, a.feature_size, num_threads=a.loader_threads, verify_crc=True,
-                               hold=a.loader_hold)
+    def groups(skip=0, limit=None, decode_raw=raw):
+        epochs = -(-(skip + (limit or 0)) // nbat) + 1
+        ds = TFRecordDataset(files, F, B, a.feature_size, num_threads=a.loader_threads, verify_crc=True,
+                             hold=a.loader_hold, num_epochs=epochs)
+        if decode_raw:
+            return ds.raw_groups(S, hold=a.loader_hold, skip=skip, limit=limit)
+        return ds.groups(S, hold=a.loader_hold, skip=skip, limit=limit)
 
-    # loader alone: decode every batch (CRC + Example parse into pinned memory), no GPU
-    t = time.perf_counter()
-    nb = sum(int(g[0].shape[0]) for g in dataset().groups(S, hold=a.loader_hold))
-    loader_eps = nb * B / (time.perf_counter() - t)
+    def loader_alone(decode_raw):
+        t = time.perf_counter()
+        nb = sum((g.n if decode_raw else int(g[0].shape[0])) for g in groups(0, a.steps, decode_raw))
+        return nb * B / (time.perf_counter() - t)
+
+    loader_eps = loader_alone(raw)
+    host_eps = loader_alone(False) if raw else loader_eps
 
     eng = FusedDeepFM(spec, hp, B, dev, embedding_update=a.embedding_update, params=params, seed=a.seed,
                       compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
     H = a.loader_hold
-    eng.train_stream(dataset().groups(S, hold=H, limit=a.warmup), S, hold=H)  # graphs + code objects
+    eng.train_stream(groups(0, a.warmup), S, hold=H)  # code objects + every graph of the ring
     stall = [0.0]
 
     def timed(it):
@@ -416,26 +609,27 @@ def measure_tfrecord(a, spec, hp, params, dev):
                 return
             yield x
 
+    marks = []  # (host time, event) after each graph launch
+
+    def after(first, n):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        marks.append((time.perf_counter(), ev, first + n))
+
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    done = eng.train_stream(timed(dataset().groups(S, hold=H, skip=a.warmup, limit=a.steps)), S, hold=H,
-                            ring_batches=a.steps)
+    done = eng.train_stream(timed(groups(a.warmup, a.steps)), S, hold=H, after_steps=after)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     eng.check()
     if done != a.steps:
         raise RuntimeError(f"trained {done} steps, expected {a.steps}")
-    # a second epoch over the same batches from the decoded-epoch HBM cache (the Estimator's
-    # hbm_cache: epochs >= 2 of a multi-epoch job never touch the loader) — reported separately
-    ids, vals, labels = eng.stream_ring()
-    eng.attach_pool(ids[:a.steps], vals[:a.steps], labels[:a.steps], start=(-eng.global_step()) % a.steps)
-    eng.train_steps(min(a.warmup, a.steps), S)
-    eng.precapture(a.steps, S)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    eng.train_steps(a.steps, S)
-    torch.cuda.synchronize()
-    cached_eps = B * a.steps / (time.perf_counter() - t1)
+    # steady state: GPU time between the ends of the first and the last graph
+    steady = None
+    if len(marks) > 2:
+        g0, g1 = marks[0], marks[-1]
+        ms = g0[1].elapsed_time(g1[1])
+        steady = (g1[2] - g0[2]) * B / (ms * 1e-3) if ms > 0 else None
     value = B * a.steps / dt
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "examples/sec", "n_gpus": 1, "steps": a.steps,
@@ -449,9 +643,13 @@ def measure_tfrecord(a, spec, hp, params, dev):
                             f"k={a.embedding_size}, mlp {a.deep_layers}, dropout keep {a.dropout}, {a.optimizer})",
                    "global_batch": B, "seq_len": F, "parallelism": "dp1", "engine": "fused",
                    "embedding_update": a.embedding_update, "input": "tfrecord", "steps_per_graph": S,
-                   "loader_threads": a.loader_threads, "loader_hold": a.loader_hold},
+                   "loader_threads": a.loader_threads, "loader_hold": a.loader_hold,
+                   "file_batches": nbat, "epochs": -(-(a.warmup + a.steps) // nbat)},
+        "decode": "device" if raw else "host",
+        "steady_examples_per_sec": round(steady, 1) if steady else None,
+        "fill_ms": round((marks[0][0] - t0) * 1e3, 2) if marks else None,
         "loader_alone_examples_per_sec": round(loader_eps, 1),
-        "next_epoch_from_hbm_cache_examples_per_sec": round(cached_eps, 1),
+        "host_decode_loader_alone_examples_per_sec": round(host_eps, 1),
         "input_stall_s": round(stall[0], 4),
         "input_stall_fraction": round(stall[0] / dt, 4),
         "data_gen_s": round(gen_s, 2),

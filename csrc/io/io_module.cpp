@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include "loader.h"
+#include "record_index.h"
 #include "tfrecord.h"
 
 namespace py = pybind11;
@@ -196,7 +197,8 @@ PYBIND11_MODULE(_rocfm_io, m) {
       .def(py::init([](std::vector<std::string> files, int field_size, int64_t max_id, int batch_size,
                        bool drop_remainder, int num_epochs, int shard_count, int shard_index, int num_threads,
                        int num_slots, bool verify_crc, bool skip_bad, int shuffle_buffer, uint64_t seed,
-                       bool stream_mode, int64_t skip_batches) {
+                       bool stream_mode, int64_t skip_batches, bool use_index, bool raw, int64_t raw_cap,
+                       int64_t max_batches_per_epoch) {
              LoaderOptions o;
              o.files = std::move(files);
              o.schema.field_size = field_size;
@@ -214,17 +216,27 @@ PYBIND11_MODULE(_rocfm_io, m) {
              o.seed = seed;
              o.stream_mode = stream_mode;
              o.skip_batches = skip_batches;
+             o.use_index = use_index;
+             o.raw = raw;
+             o.raw_cap = raw_cap;
+             o.max_batches_per_epoch = max_batches_per_epoch;
              return new BatchLoader(o);
            }),
            py::arg("files"), py::arg("field_size"), py::arg("max_id") = 0, py::arg("batch_size") = 1024,
            py::arg("drop_remainder") = true, py::arg("num_epochs") = 1, py::arg("shard_count") = 1,
            py::arg("shard_index") = 0, py::arg("num_threads") = 4, py::arg("num_slots") = 4,
            py::arg("verify_crc") = true, py::arg("skip_bad") = false, py::arg("shuffle_buffer") = 0,
-           py::arg("seed") = 0, py::arg("stream_mode") = false, py::arg("skip_batches") = 0)
+           py::arg("seed") = 0, py::arg("stream_mode") = false, py::arg("skip_batches") = 0,
+           py::arg("use_index") = true, py::arg("raw") = false, py::arg("raw_cap") = 0,
+           py::arg("max_batches_per_epoch") = 0)
       .def("set_slot",
            [](BatchLoader& L, int i, uintptr_t ids, uintptr_t vals, uintptr_t labels) {
              L.set_slot(i, reinterpret_cast<int32_t*>(ids), reinterpret_cast<float*>(vals),
                         reinterpret_cast<float*>(labels));
+           })
+      .def("set_raw_slot",
+           [](BatchLoader& L, int i, uintptr_t bytes, uintptr_t offs) {
+             L.set_raw_slot(i, reinterpret_cast<uint8_t*>(bytes), reinterpret_cast<int32_t*>(offs));
            })
       .def("start", &BatchLoader::start)
       .def("next",
@@ -250,5 +262,40 @@ PYBIND11_MODULE(_rocfm_io, m) {
       .def("stop", &BatchLoader::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bad_records", &BatchLoader::bad_records)
       .def_property_readonly("records_seen", &BatchLoader::records_seen)
-      .def_property_readonly("index_fallbacks", &BatchLoader::index_fallbacks);
+      .def_property_readonly("index_fallbacks", &BatchLoader::index_fallbacks)
+      .def_property_readonly("index_loads", &BatchLoader::index_loads)
+      .def_property_readonly("index_builds", &BatchLoader::index_builds);
+
+  // persistent record index (record_index.h)
+  m.def(
+      "build_index",
+      [](const std::string& path, bool verify_crc) {
+        py::gil_scoped_release nogil;
+        return build_index_file(path, verify_crc);
+      },
+      py::arg("path"), py::arg("verify_crc") = true);
+  m.def("index_path", &index_path, py::arg("path"));
+  m.def(
+      "index_info",
+      [](const std::string& path) -> py::object {
+        // (records, max payload bytes) from a valid saved index, or None
+        int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return py::none();
+        struct stat st;
+        if (fstat(fd, &st) != 0) {
+          ::close(fd);
+          return py::none();
+        }
+        const size_t size = (size_t)st.st_size;
+        void* m = size ? mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0) : nullptr;
+        ::close(fd);
+        if (size && m == MAP_FAILED) return py::none();
+        RecordIndex ix;
+        const bool ok = load_index(path, static_cast<const uint8_t*>(m), size, &ix);
+        py::object out = ok ? py::object(py::make_tuple(ix.n, ix.max_len)) : py::object(py::none());
+        ix = RecordIndex();
+        if (m) munmap(m, size);
+        return out;
+      },
+      py::arg("path"));
 }

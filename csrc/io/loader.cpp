@@ -1,8 +1,11 @@
 // rocfm host runtime: multi-threaded TFRecord batch loader (see loader.h).
 #include "loader.h"
 
+#include "record_index.h"
+
 #include <fcntl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -29,7 +32,7 @@ struct BatchLoader::Chunk {
 };
 
 namespace {
-std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path);
+std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path, bool populate = false);
 }
 
 BatchLoader::BatchLoader(const LoaderOptions& opt) : opt_(opt) {
@@ -38,7 +41,9 @@ BatchLoader::BatchLoader(const LoaderOptions& opt) : opt_(opt) {
     throw std::invalid_argument("bad shard spec");
   if (opt_.num_slots < 2) opt_.num_slots = 2;
   if (opt_.num_threads < 1) opt_.num_threads = 1;
-  defer_crc_ = opt_.verify_crc && !opt_.skip_bad && opt_.shard_count > 1 && !opt_.stream_mode;
+  if (opt_.raw && opt_.raw_cap <= 0) throw std::invalid_argument("raw mode needs raw_cap > 0");
+  if (opt_.raw && opt_.skip_bad)
+    throw std::invalid_argument("raw mode cannot skip bad records (a malformed Example is found on the GPU)");
   slots_.resize(opt_.num_slots);
   slot_state_.assign(opt_.num_slots, 0);
   slot_seq_.resize(opt_.num_slots);
@@ -54,10 +59,17 @@ void BatchLoader::set_slot(int i, int32_t* ids, float* vals, float* labels) {
   slots_[i] = Slot{ids, vals, labels};
 }
 
+void BatchLoader::set_raw_slot(int i, uint8_t* bytes, int32_t* offs) {
+  if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot");
+  slots_[i].bytes = bytes;
+  slots_[i].offs = offs;
+}
+
 void BatchLoader::start() {
   if (started_) return;
   for (auto& s : slots_)
-    if (!s.ids || !s.vals || !s.labels) throw std::runtime_error("all slots must be set before start()");
+    if (opt_.raw ? (!s.bytes || !s.offs) : (!s.ids || !s.vals || !s.labels))
+      throw std::runtime_error("all slots must be set before start()");
   started_ = true;
   reader_ = std::thread(&BatchLoader::reader_main, this);
   for (int i = 0; i < opt_.num_threads; ++i) workers_.emplace_back(&BatchLoader::worker_main, this);
@@ -96,7 +108,10 @@ void BatchLoader::push_job(Job&& j) {
 
 namespace {
 
-std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path) {
+// populate: map the page-cache pages up front (MAP_POPULATE) for files up to 1 GiB, so the decode
+// workers never take minor faults (they serialise on the mm lock) — index mode reads records
+// without a walk that would otherwise touch the pages first
+std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path, bool populate) {
   auto c = std::make_shared<BatchLoader::Chunk>();
   int fd = ::open(path.c_str(), O_RDONLY);
   if (fd < 0) throw std::runtime_error("cannot open " + path + ": " + strerror(errno));
@@ -107,7 +122,8 @@ std::shared_ptr<BatchLoader::Chunk> map_file(const std::string& path) {
   }
   c->size = (size_t)st.st_size;
   if (c->size) {
-    c->map = mmap(nullptr, c->size, PROT_READ, MAP_PRIVATE, fd, 0);
+    const bool pop = populate && c->size <= ((size_t)1 << 30) && !getenv("ROCFM_NO_POPULATE");
+    c->map = mmap(nullptr, c->size, PROT_READ, MAP_PRIVATE | (pop ? MAP_POPULATE : 0), fd, 0);
     if (c->map == MAP_FAILED) {
       ::close(fd);
       throw std::runtime_error("mmap failed for " + path);
@@ -254,19 +270,19 @@ void BatchLoader::reader_main() {
     int64_t seq = 0, skipped = 0;
     std::mt19937_64 rng(opt_.seed);
     const int B = opt_.batch_size;
-    // file mode: files are indexed (framing walk + CRC, parallel) one file ahead of the emission
+    // index mode (file mode without skip_bad): every file's record offsets come from its saved
+    // index, or from one parallel framing walk that then saves it; files are indexed one file
+    // ahead of the emission.  Legacy mode (skip_bad): the walk checks every CRC and drops bad
+    // records before sharding.
+    const bool index_mode = opt_.use_index && !opt_.skip_bad;
     struct Indexed {
       std::shared_ptr<Chunk> chunk;
-      std::vector<RecordRef> recs;
+      std::vector<RecordRef> recs;  // legacy mode: payload refs
+      RecordIndex ix;               // index mode
       size_t bad = 0;
     };
     const int parts = std::max(1, opt_.num_threads);
-    // deferred data CRCs (defer_crc_, see loader.h): the walk checks the framing (length CRCs)
-    // only; each kept record's data CRC is checked by the decoder that decodes it
-    const bool vdata = !defer_crc_;
-    auto index = [this, parts, vdata](const std::string& path) {
-      Indexed ix;
-      ix.chunk = map_file(path);
+    auto walk = [this, parts](Indexed& ix, bool vdata) {
       const size_t n = ix.chunk->size;
       const int np = (int)std::min<size_t>((size_t)parts, std::max<size_t>(1, n >> 22));
       if (np < 2 ||
@@ -276,6 +292,25 @@ void BatchLoader::reader_main() {
         ix.bad = 0;
         scan_records(ix.chunk->data, n, opt_.verify_crc, opt_.skip_bad, &ix.recs, &ix.bad, vdata);
       }
+    };
+    auto index = [this, walk, index_mode](const std::string& path) {
+      Indexed ix;
+      ix.chunk = map_file(path, index_mode);
+      if (!index_mode) {
+        walk(ix, true);
+        return ix;
+      }
+      if (load_index(path, ix.chunk->data, ix.chunk->size, &ix.ix)) {
+        ++index_loads_;
+        return ix;
+      }
+      // framing + length CRCs only: every record's data CRC is checked by whoever resolves it
+      walk(ix, false);
+      index_from_refs(ix.chunk->data, ix.recs, &ix.ix);
+      ix.recs.clear();
+      ix.recs.shrink_to_fit();
+      save_index(path, ix.ix, false);
+      ++index_builds_;
       return ix;
     };
     std::future<Indexed> pending;
@@ -283,14 +318,20 @@ void BatchLoader::reader_main() {
     for (int epoch = 0; opt_.num_epochs < 0 || epoch < opt_.num_epochs; ++epoch) {
       Job cur;
       cur.epoch = epoch;
+      cur.framed = index_mode && !opt_.stream_mode;
       std::vector<RecordRef> shuf;  // shuffle buffer
       std::vector<std::shared_ptr<Chunk>> shuf_keep;
       int64_t ridx = 0;  // record index across the concatenated file list (Dataset.shard)
+      int64_t ep_batches = 0;
+      const int64_t maxb = opt_.max_batches_per_epoch;
+      auto full = [&] { return maxb > 0 && ep_batches >= maxb; };
       cur.recs.reserve(B);
       auto emit = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
+        if (full()) return;
         if (cur.keep.empty() || cur.keep.back() != keep) cur.keep.push_back(keep);
         cur.recs.push_back(r);
         if ((int)cur.recs.size() == B) {
+          ++ep_batches;
           if (skipped < opt_.skip_batches) {  // resume: drop whole batches without decoding them
             ++skipped;
             cur.recs.clear();
@@ -298,15 +339,15 @@ void BatchLoader::reader_main() {
             return;
           }
           cur.seq = seq++;
+          const bool framed = cur.framed;
           push_job(std::move(cur));
           cur = Job();
           cur.epoch = epoch;
+          cur.framed = framed;
           cur.recs.reserve(B);
         }
       };
-      auto take = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
-        ++seen_;
-        if ((ridx++ % opt_.shard_count) != opt_.shard_index) return;
+      auto take_own = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
         if (opt_.shuffle_buffer > 0) {
           shuf.push_back(r);
           shuf_keep.push_back(keep);
@@ -322,11 +363,25 @@ void BatchLoader::reader_main() {
           emit(r, keep);
         }
       };
+      auto take = [&](const RecordRef& r, const std::shared_ptr<Chunk>& keep) {
+        ++seen_;
+        if ((ridx++ % opt_.shard_count) != opt_.shard_index) return;
+        take_own(r, keep);
+      };
       size_t fi = 0;
       for (const auto& path : opt_.files) {
         {
           std::lock_guard<std::mutex> g(mu_);
           if (stop_) return;
+        }
+        if (full() && opt_.shuffle_buffer <= 0 && !opt_.stream_mode) {
+          // this epoch's agreed batches are out: the rest of the files is not read (their
+          // indexes are still taken in order, one file ahead)
+          Indexed skip = pending.get();
+          if (fi + 1 < opt_.files.size() || epoch + 1 < opt_.num_epochs || opt_.num_epochs < 0)
+            pending = std::async(std::launch::async, index, opt_.files[(fi + 1) % opt_.files.size()]);
+          ++fi;
+          continue;
         }
         if (opt_.stream_mode) {
           FILE* f = (path == "-") ? stdin : fopen(path.c_str(), "rb");
@@ -348,7 +403,22 @@ void BatchLoader::reader_main() {
           if (fi + 1 < opt_.files.size() || epoch + 1 < opt_.num_epochs || opt_.num_epochs < 0)
             pending = std::async(std::launch::async, index, opt_.files[(fi + 1) % opt_.files.size()]);
           bad_ += ix.bad;
-          for (auto& r : ix.recs) take(r, ix.chunk);
+          if (index_mode) {
+            // only this shard's records: j ≡ shard_index − ridx (mod shard_count)
+            const int64_t P = opt_.shard_count, n = (int64_t)ix.ix.n;
+            const int64_t j0 = ((opt_.shard_index - ridx) % P + P) % P;
+            const uint8_t* base = ix.chunk->data;
+            const uint64_t size = ix.chunk->size;
+            for (int64_t j = j0; j < n && !full(); j += P) {
+              const uint64_t o = ix.ix.off[j];
+              if (o >= size) throw std::runtime_error("TFRecord index: offset beyond the end of " + path);
+              take_own(RecordRef{base + o, (uint32_t)std::min<uint64_t>(size - o, UINT32_MAX)}, ix.chunk);
+            }
+            ridx += n;
+            seen_ += (size_t)n;
+          } else {
+            for (auto& r : ix.recs) take(r, ix.chunk);
+          }
         }
         ++fi;
       }
@@ -364,6 +434,11 @@ void BatchLoader::reader_main() {
       if (!cur.recs.empty() && !opt_.drop_remainder) {
         cur.seq = seq++;
         push_job(std::move(cur));
+      } else if (!cur.recs.empty() && cur.framed && opt_.verify_crc) {
+        // the dropped remainder is never decoded, but its records are still checked (tf.data
+        // reads and checks every record before batch(drop_remainder) drops the tail)
+        std::string err = resolve(&cur.recs, -1);
+        if (!err.empty()) throw std::runtime_error(err);
       }
       if (opt_.stream_mode && opt_.num_epochs < 0) break;  // a pipe cannot be rewound
     }
@@ -375,6 +450,49 @@ void BatchLoader::reader_main() {
   } catch (const std::exception& e) {
     fail(e.what());
   }
+}
+
+std::string BatchLoader::resolve(std::vector<RecordRef>* recs, int64_t seq) const {
+  const size_t n = recs->size();
+  auto where = [seq](size_t r) {
+    return (seq >= 0 ? " in batch " + std::to_string(seq) : std::string(" in the dropped remainder")) +
+           " record " + std::to_string(r);
+  };
+  for (size_t r = 0; r < n; ++r) {
+    RecordRef& x = (*recs)[r];
+    const uint64_t left = x.len;  // bytes from the frame start to the end of the file
+    if (left < 16) return "TFRecord: truncated record" + where(r);
+    uint64_t len;
+    memcpy(&len, x.data, 8);
+    if (len > left - 16 || len > UINT32_MAX) return "TFRecord: truncated record" + where(r);
+    if (opt_.verify_crc) {
+      uint32_t lcrc;
+      memcpy(&lcrc, x.data + 8, 4);
+      if (mask_crc(crc32c(x.data, 8)) != lcrc) return "TFRecord: corrupt length CRC" + where(r);
+    }
+    x.data += 12;
+    x.len = (uint32_t)len;
+  }
+  if (opt_.verify_crc) {
+    size_t r = 0;
+    for (; r + 3 <= n; r += 3) {
+      const uint8_t* p[3] = {(*recs)[r].data, (*recs)[r + 1].data, (*recs)[r + 2].data};
+      const size_t l[3] = {(*recs)[r].len, (*recs)[r + 1].len, (*recs)[r + 2].len};
+      uint32_t c[3];
+      crc32c_x3(p, l, c);
+      for (int k = 0; k < 3; ++k) {
+        uint32_t d;
+        memcpy(&d, p[k] + l[k], 4);
+        if (mask_crc(c[k]) != d) return "TFRecord: corrupt data CRC" + where(r + k);
+      }
+    }
+    for (; r < n; ++r) {
+      uint32_t d;
+      memcpy(&d, (*recs)[r].data + (*recs)[r].len, 4);
+      if (mask_crc(crc32c((*recs)[r].data, (*recs)[r].len)) != d) return "TFRecord: corrupt data CRC" + where(r);
+    }
+  }
+  return "";
 }
 
 void BatchLoader::worker_main() {
@@ -397,25 +515,35 @@ void BatchLoader::worker_main() {
     Slot& s = slots_[slot];
     int n = (int)job.recs.size();
     std::string err;
-    for (int r = 0; r < n; ++r) {
-      if (defer_crc_) {
-        uint32_t dcrc;
-        memcpy(&dcrc, job.recs[r].data + job.recs[r].len, 4);
-        if (mask_crc(crc32c(job.recs[r].data, job.recs[r].len)) != dcrc) {
-          err = std::string("TFRecord: corrupt data CRC in batch ") + std::to_string(job.seq) + " record " +
-                std::to_string(r);
+    if (job.framed) err = resolve(&job.recs, job.seq);
+    if (err.empty() && opt_.raw) {
+      // raw mode: payloads back to back + offsets; the device decoder parses them
+      int64_t cursor = 0;
+      for (int r = 0; r < n; ++r) {
+        const RecordRef& x = job.recs[r];
+        if (cursor + (int64_t)x.len > opt_.raw_cap) {
+          err = "raw batch capacity exceeded in batch " + std::to_string(job.seq) + " (" +
+                std::to_string(opt_.raw_cap) + " bytes; records up to " + std::to_string(x.len) +
+                " bytes): use a larger raw_record_bytes or host decoding";
           break;
         }
+        s.offs[r] = (int32_t)cursor;
+        memcpy(s.bytes + cursor, x.data, x.len);
+        cursor += x.len;
       }
-      int st = decode_example(job.recs[r].data, job.recs[r].len, opt_.schema, s.labels + r,
-                              s.ids + (size_t)r * F, s.vals + (size_t)r * F, opt_.max_id);
-      if (st != kOk) {
-        static const char* names[] = {"ok", "malformed Example protobuf", "missing feature",
-                                      "wrong feature length (FixedLenFeature expects field_size values)",
-                                      "id out of range [0, feature_size)"};
-        err = std::string("decode error in batch ") + std::to_string(job.seq) + " record " + std::to_string(r) +
-              ": " + names[st];
-        break;
+      s.offs[n] = (int32_t)cursor;
+    } else if (err.empty()) {
+      for (int r = 0; r < n; ++r) {
+        int st = decode_example(job.recs[r].data, job.recs[r].len, opt_.schema, s.labels + r,
+                                s.ids + (size_t)r * F, s.vals + (size_t)r * F, opt_.max_id);
+        if (st != kOk) {
+          static const char* names[] = {"ok", "malformed Example protobuf", "missing feature",
+                                        "wrong feature length (FixedLenFeature expects field_size values)",
+                                        "id out of range [0, feature_size)"};
+          err = std::string("decode error in batch ") + std::to_string(job.seq) + " record " + std::to_string(r) +
+                ": " + names[st];
+          break;
+        }
       }
     }
     if (!err.empty()) {

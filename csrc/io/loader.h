@@ -2,18 +2,20 @@
 // reference's input_fn drives: PS:112-169, HVD:104-161).
 //
 // Pipeline (per epoch, like the reference's shard → batch(drop_remainder) → parse → repeat):
-//   reader thread : mmap file (or read a FIFO/stdin in pipe mode) → walk TFRecord framing +
-//                   CRC32C → keep every shard_count-th record starting at shard_index (record
-//                   index runs over the concatenated file list, = Dataset.shard) → optional
-//                   shuffle buffer → cut batches of batch_size (tail dropped per epoch when
-//                   drop_remainder) → job queue
-//   N workers     : decode a job's records straight into output slot (seq % num_slots)
-// A sharded loader (shard_count > 1, verify_crc, no skip_bad) checks only the framing in the walk
-// and leaves each record's data CRC to the worker that decodes it: every rank walks the whole
-// file list (record-index sharding), so a full-CRC walk made P ranks checksum every byte P times
-// and stopped the aggregate decode rate scaling with the rank count (profiles/r3_loader_aggregate.md).
-// A corrupt record still fails the job, on the rank whose shard holds it.  skip_bad keeps the full
-// walk: dropping a bad record there shifts the record index every rank shards by.
+//   reader thread : mmap file (or read a FIFO/stdin in pipe mode) → record offsets from the file's
+//                   persistent index (record_index.h; built by one framing walk and saved the
+//                   first time) → keep every shard_count-th record starting at shard_index
+//                   (record index runs over the concatenated file list, = Dataset.shard) without
+//                   touching the others → optional shuffle buffer → cut batches of batch_size
+//                   (tail dropped per epoch when drop_remainder; its records' CRCs are still
+//                   checked) → job queue
+//   N workers     : resolve a job's frames (length + length CRC), check the data CRCs (three
+//                   records interleaved) and either decode the records straight into output slot
+//                   (seq % num_slots) — host decode — or copy the raw Example payloads into the
+//                   slot's byte buffer with their offsets (raw mode: the GPU parses them,
+//                   csrc/kernels/decode.hip, so the host only moves bytes)
+// skip_bad (on_bad_record=skip) keeps the legacy full walk: dropping a corrupt record there shifts
+// the record index every rank shards by, so it must happen before sharding.
 //   consumer      : next() returns slots strictly in sequence order; release() recycles them.
 // Output slots are caller-provided host buffers (Python passes pinned torch tensors so the H2D copy
 // is a true async DMA on a side HIP stream).
@@ -49,12 +51,19 @@ struct LoaderOptions {
   uint64_t seed = 0;
   bool stream_mode = false;  // pipe mode: files are FIFOs / "-" for stdin, read sequentially
   int64_t skip_batches = 0;  // drop the first N batches undecoded (resume after a restart)
+  int64_t max_batches_per_epoch = 0;  // > 0: stop each epoch after this many batches (ranks agree
+                                      // on a common per-epoch count; the surplus is dropped)
+  bool use_index = true;     // persistent per-file offset index (file mode without skip_bad)
+  bool raw = false;          // raw mode: slots receive Example payload bytes + offsets
+  int64_t raw_cap = 0;       // raw mode: byte capacity of one slot's payload buffer
 };
 
 struct Slot {
   int32_t* ids = nullptr;
   float* vals = nullptr;
   float* labels = nullptr;
+  uint8_t* bytes = nullptr;  // raw mode: payloads of the batch, back to back
+  int32_t* offs = nullptr;   // raw mode: [batch_size + 1] payload offsets into bytes
 };
 
 class BatchLoader {
@@ -62,6 +71,7 @@ class BatchLoader {
   explicit BatchLoader(const LoaderOptions& opt);
   ~BatchLoader();
   void set_slot(int i, int32_t* ids, float* vals, float* labels);
+  void set_raw_slot(int i, uint8_t* bytes, int32_t* offs);
   void start();
   // Blocks until the next batch is decoded.  Returns slot index and fills nrows/epoch; returns -1
   // at end of data.  Throws on decode/framing errors.
@@ -76,6 +86,8 @@ class BatchLoader {
   size_t bad_records() const { return bad_.load(); }
   size_t records_seen() const { return seen_.load(); }
   size_t index_fallbacks() const { return fallbacks_.load(); }  // files indexed by the sequential walk
+  size_t index_loads() const { return index_loads_.load(); }    // files whose saved index was used
+  size_t index_builds() const { return index_builds_.load(); }  // files indexed by a walk (and saved)
 
   struct Chunk;  // owns the bytes (mmap or arena)
 
@@ -83,13 +95,17 @@ class BatchLoader {
   struct Job {
     int64_t seq;
     int epoch;
-    std::vector<RecordRef> recs;
+    std::vector<RecordRef> recs;  // framed: frame start + bytes left in the file (workers resolve)
     std::vector<std::shared_ptr<Chunk>> keep;
+    bool framed = false;
   };
   void reader_main();
   void worker_main();
   void push_job(Job&& j);
   void fail(const std::string& msg);
+  // framed refs → payload refs with every CRC checked (workers, and the reader for the dropped
+  // remainder); returns an error message or ""
+  std::string resolve(std::vector<RecordRef>* recs, int64_t seq) const;
 
   LoaderOptions opt_;
   std::vector<Slot> slots_;
@@ -105,9 +121,8 @@ class BatchLoader {
   std::string error_;
   std::thread reader_;
   std::vector<std::thread> workers_;
-  std::atomic<size_t> bad_{0}, seen_{0}, fallbacks_{0};
+  std::atomic<size_t> bad_{0}, seen_{0}, fallbacks_{0}, index_loads_{0}, index_builds_{0};
   bool started_ = false;
-  bool defer_crc_ = false;  // data CRCs checked by the decoders (see the header comment)
 };
 
 // Decode an entire TFRecord file (small files: validation sets, tests).

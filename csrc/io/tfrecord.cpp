@@ -4,6 +4,7 @@
 #include <nmmintrin.h>
 #include <string.h>
 
+#include <algorithm>
 #include <stdexcept>
 
 namespace rocfm {
@@ -28,6 +29,27 @@ uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
   }
   while (n--) c = _mm_crc32_u8((uint32_t)c, *p++);
   return ~(uint32_t)c;
+}
+
+// Three independent CRC32C streams interleaved: the crc32 instruction has a 3-cycle latency and a
+// 1-cycle issue rate, so three records checked together cost about as much as one alone.
+void crc32c_x3(const uint8_t* const p[3], const size_t n[3], uint32_t out[3]) {
+  uint64_t c0 = 0xffffffffu, c1 = 0xffffffffu, c2 = 0xffffffffu;
+  const size_t m = std::min(n[0], std::min(n[1], n[2])) & ~(size_t)7;
+  const uint8_t *a = p[0], *b = p[1], *c = p[2];
+  for (size_t i = 0; i < m; i += 8) {
+    uint64_t va, vb, vc;
+    memcpy(&va, a + i, 8);
+    memcpy(&vb, b + i, 8);
+    memcpy(&vc, c + i, 8);
+    c0 = _mm_crc32_u64(c0, va);
+    c1 = _mm_crc32_u64(c1, vb);
+    c2 = _mm_crc32_u64(c2, vc);
+  }
+  // tails continue from the raw states (crc32c() complements its argument on entry)
+  out[0] = crc32c(a + m, n[0] - m, ~(uint32_t)c0);
+  out[1] = crc32c(b + m, n[1] - m, ~(uint32_t)c1);
+  out[2] = crc32c(c + m, n[2] - m, ~(uint32_t)c2);
 }
 
 // ---------------------------------------------------------------------------------------------

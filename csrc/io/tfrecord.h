@@ -18,6 +18,8 @@ namespace rocfm {
 namespace io {
 
 uint32_t crc32c(const uint8_t* data, size_t n, uint32_t crc = 0);
+// CRC32C of three buffers at once (interleaved instruction streams).
+void crc32c_x3(const uint8_t* const p[3], const size_t n[3], uint32_t out[3]);
 inline uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 inline uint32_t unmask_crc(uint32_t m) {
   uint32_t r = m - 0xa282ead8u;

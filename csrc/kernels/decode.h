@@ -1,0 +1,31 @@
+// Device-side tf.train.Example parsing (decode.hip): the reference's vectorized
+// tf.parse_example (PS:117-126, HVD:109-118) moved off the host.  The host loader (raw mode,
+// csrc/io/loader.h) only resolves frames, checks CRCs and copies the payload bytes of each batch
+// into pinned memory; after the H2D copy this kernel parses every record into the engine's batch
+// ring (ids int32 [B,F], values f32 [B,F], label f32 [B]) on the copy stream.
+#pragma once
+#include "../common.h"
+
+namespace rocfm {
+
+constexpr int kDecodeKeyMax = 16;  // feature-name bytes compared on the device
+
+struct DecodeParams {
+  const uint8_t* bytes;   // [nb][cap] payloads of batch b back to back from bytes + b·cap
+  const int32_t* offs;    // [nb][B+1] record r of batch b = bytes[b·cap + offs[r] .. offs[r+1])
+  long long cap;          // bytes per batch row (multiple of 16)
+  int nb, B, F;
+  int32_t* ids;           // ring [R][B][F]
+  float* vals;            // ring [R][B][F]
+  float* labels;          // ring [R][B]
+  int slot0, R;           // batch b → ring slot (slot0 + b) % R
+  long long max_id;       // ids must be < max_id (0: < 2^31)
+  int batch0;             // sequence number of batch 0 (error reports)
+  int32_t* err;           // [4] sticky: status (tfrecord.h ParseStatus), batch, record, 0
+  uint8_t key[3][kDecodeKeyMax];  // label, ids, values feature names
+  int klen[3];
+};
+
+void launch_decode_examples(const DecodeParams& p, hipStream_t stream);
+
+}  // namespace rocfm

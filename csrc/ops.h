@@ -12,6 +12,7 @@
 #include "kernels/merge.h"
 #include "kernels/metrics.h"
 #include "kernels/p2p.h"
+#include "kernels/decode.h"
 
 namespace rocfm {
 

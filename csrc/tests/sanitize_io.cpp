@@ -17,7 +17,10 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/stat.h>
 #include "../io/loader.h"
+#include "../io/record_index.h"
 #include "../io/tfrecord.h"
 
 using namespace rocfm::io;
@@ -144,6 +147,48 @@ int main(int argc, char** argv) {
     }
   }
 
+  // 2b. raw mode (payload bytes + offsets) through the saved record index, every row once; the
+  //     payloads decode to the same ids as the host path
+  {
+    for (int shard = 0; shard < 2; ++shard) {
+      LoaderOptions o;
+      o.files = {path, dir + "/h2.tfrecords"};
+      o.schema.field_size = kF;
+      o.batch_size = 64;
+      o.num_epochs = 2;
+      o.shard_count = 2;
+      o.shard_index = shard;
+      o.num_threads = 3;
+      o.num_slots = 6;
+      o.raw = true;
+      o.raw_cap = 64 * 512;
+      o.max_batches_per_epoch = 5;
+      BatchLoader L(o);
+      std::vector<std::vector<uint8_t>> sb(o.num_slots, std::vector<uint8_t>(o.raw_cap));
+      std::vector<std::vector<int32_t>> so(o.num_slots, std::vector<int32_t>(65));
+      for (int i = 0; i < o.num_slots; ++i) L.set_raw_slot(i, sb[i].data(), so[i].data());
+      L.start();
+      long rows = 0;
+      int nrows = 0, epoch = 0, slot;
+      Schema s;
+      s.field_size = kF;
+      while ((slot = L.next(&nrows, &epoch)) >= 0) {
+        for (int r = 0; r < nrows; ++r) {
+          CHECK(so[slot][r] <= so[slot][r + 1] && so[slot][r + 1] <= o.raw_cap);
+          float lab;
+          int32_t ids[kF];
+          float vals[kF];
+          CHECK(decode_example(sb[slot].data() + so[slot][r], so[slot][r + 1] - so[slot][r], s, &lab, ids, vals,
+                               100000) == kOk);
+        }
+        rows += nrows;
+        L.release(slot);
+      }
+      L.stop();
+      CHECK(rows == 2L * 5 * 64);  // capped at 5 batches per epoch
+    }
+  }
+
   // 3. corrupted inputs: truncations, bit flips, forged lengths — rejected or skipped, never a
   //    wild read (ASan) or UB (UBSan)
   std::uniform_int_distribution<size_t> pos(0, buf.size() - 1);
@@ -168,6 +213,46 @@ int main(int argc, char** argv) {
     walk_and_decode(b, false, false);
     walk_and_decode(b, true, true);
     walk_and_decode(b, false, true);
+    if (it % 25 == 0) {  // and through the loader's index mode, the index taken from the intact
+      //                      file and forced to look current (same size and mtime): the workers'
+      //                      frame checks must reject whatever the corruption did
+      const std::string bad = dir + "/badix.tfrecords";
+      write_file(bad, buf);
+      build_index_file(bad, true);
+      struct stat st0;
+      stat(bad.c_str(), &st0);
+      std::string c = b;
+      c.resize(buf.size(), '\0');  // same size (truncations zero-filled)
+      write_file(bad, c);
+      struct timespec ts[2] = {st0.st_atim, st0.st_mtim};
+      utimensat(AT_FDCWD, bad.c_str(), ts, 0);
+      for (int raw = 0; raw < 2; ++raw) {
+        LoaderOptions o;
+        o.files = {bad};
+        o.schema.field_size = kF;
+        o.max_id = 100000;
+        o.batch_size = 32;
+        o.num_threads = 2;
+        o.num_slots = 4;
+        o.raw = raw;
+        o.raw_cap = 32 * 1024;
+        BatchLoader L(o);
+        std::vector<std::vector<uint8_t>> sb(4, std::vector<uint8_t>(o.raw_cap));
+        std::vector<std::vector<int32_t>> so(4, std::vector<int32_t>(33)), sid(4, std::vector<int32_t>(32 * kF));
+        std::vector<std::vector<float>> sv(4, std::vector<float>(32 * kF)), sl(4, std::vector<float>(32));
+        for (int i = 0; i < 4; ++i) {
+          L.set_slot(i, sid[i].data(), sv[i].data(), sl[i].data());
+          L.set_raw_slot(i, sb[i].data(), so[i].data());
+        }
+        try {
+          L.start();
+          int nrows = 0, epoch = 0, slot;
+          while ((slot = L.next(&nrows, &epoch)) >= 0) L.release(slot);
+        } catch (const std::exception&) {
+        }
+        L.stop();
+      }
+    }
     if (it % 50 == 0) {  // and through the file reader
       const std::string bad = dir + "/bad.tfrecords";
       write_file(bad, b);

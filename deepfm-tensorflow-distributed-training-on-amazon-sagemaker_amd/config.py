@@ -108,8 +108,10 @@ class Config:
     seed: int = 1234
     save_checkpoints_steps: int = 0  # 0 → only at end (plus save_checkpoints_secs)
     save_checkpoints_secs: int = 600  # Estimator default cadence
-    hbm_cache: bool = True  # single GPU, >1 epoch, no shuffle: keep the decoded first epoch in HBM and
-    #                         train later epochs from it (the reference re-reads + re-parses every epoch)
+    hbm_cache: bool = True  # >1 epoch, no shuffle: every rank keeps its decoded first epoch in HBM and
+    #                         trains later epochs from it (the reference re-reads + re-parses every epoch)
+    device_decode: bool = True  # fused engine streaming: the loader copies undecoded Example payloads
+    #                             and the GPU parses them (csrc/kernels/decode.hip); False = host parse
     hbm_cache_gb: float = 64.0  # budget for that cache (decoded epoch: B·(8F + 4) bytes per batch)
     # pre-decoded on-disk cache (rocfm.data.cache): each rank's first pass over its training shard is
     # written raw (int32 ids, f32 values / labels) under this directory and every later epoch — and
@@ -125,7 +127,8 @@ class Config:
     metrics_file: str = ""  # JSONL metrics output
     tensorboard: bool = True  # chief writes TF event files: model_dir (train) and model_dir/eval (utils/tensorboard.py)
     # training-data sharding over ranks: "record" = Dataset.shard (every count-th record of the
-    # concatenated file list, the reference's semantics — every rank walks every file's framing);
+    # concatenated file list, the reference's semantics — each rank reads only its own records
+    # through the files' persistent record indexes, csrc/io/record_index.h);
     # "file" = each rank reads files[index::count] only (like SageMaker's ShardedByS3Key input,
     # README:87-92), so P ranks walk each byte once; needs at least `count` files
     shard_policy: str = "record"

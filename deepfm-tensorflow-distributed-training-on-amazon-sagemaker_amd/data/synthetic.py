@@ -141,4 +141,5 @@ def write_synthetic_tfrecord(path: str, n: int, vocab: int, field_size: int = 39
         ids, vals, labels = gen_.batch(m, "cpu", g)
         io.write_tfrecord(path, labels.numpy(), ids.numpy().astype(np.int64), vals.numpy(), done > 0)
         done += m
+    io.build_index(path, True)  # the persistent record index next to the file (record_index.h)
     return done

@@ -143,6 +143,39 @@ def parse_example(payload: bytes) -> dict:
     return out
 
 
+class RawGroup:
+    """``n`` undecoded batches: ``bytes [n, cap]`` uint8 payloads and ``offs [n, B+1]`` int32
+    offsets (batch k's record r is ``bytes[k, offs[k, r]:offs[k, r+1]]``), pinned host memory."""
+
+    __slots__ = ("bytes", "offs", "n", "B")
+
+    def __init__(self, bytes_: torch.Tensor, offs: torch.Tensor, n: int, B: int):
+        self.bytes, self.offs, self.n, self.B = bytes_, offs, int(n), int(B)
+
+    def used_bytes(self) -> int:
+        """Bytes from the first batch's start to the end of the last batch's payloads."""
+        return (self.n - 1) * self.bytes.shape[1] + int(self.offs[self.n - 1, self.B])
+
+    def decode_host(self, field_size: int, feature_size: int = 0):
+        """Decode on the host (tests / CPU fallback): (ids [n,B,F], vals [n,B,F], labels [n,B])."""
+        io = _io_mod()
+        n, B, F = self.n, self.B, int(field_size)
+        ids = torch.zeros(n, B, F, dtype=torch.int32)
+        vals = torch.zeros(n, B, F, dtype=torch.float32)
+        labels = torch.zeros(n, B, dtype=torch.float32)
+        raw = self.bytes.numpy()
+        offs = self.offs.numpy()
+        for k in range(n):
+            for r in range(B):
+                st, lab, i, v = io.decode_example(raw[k, offs[k, r]:offs[k, r + 1]].tobytes(), F, int(feature_size))
+                if st != 0:
+                    raise ValueError(f"decode error {st} in batch {k} record {r}")
+                ids[k, r] = torch.from_numpy(i)
+                vals[k, r] = torch.from_numpy(v)
+                labels[k, r] = lab
+        return ids, vals, labels
+
+
 # --------------------------------------------------------------------------------------------
 # native batch loader
 # --------------------------------------------------------------------------------------------
@@ -164,7 +197,7 @@ class TFRecordDataset:
                  num_epochs: int = 1, shard_count: int = 1, shard_index: int = 0, drop_remainder: bool = True,
                  num_threads: int = 4, num_slots: int = 6, verify_crc: bool = True, skip_bad: bool = False,
                  shuffle_buffer: int = 0, seed: int = 0, stream_mode: bool = False, pin_memory: Optional[bool] = None,
-                 hold: int = 1, shard_policy: str = "record"):
+                 hold: int = 1, shard_policy: str = "record", max_batches_per_epoch: int = 0):
         self.files = list(files)
         if shard_policy not in ("record", "file"):
             raise ValueError(f"shard_policy must be record or file, got {shard_policy!r}")
@@ -183,7 +216,7 @@ class TFRecordDataset:
                        num_epochs=int(num_epochs), shard_count=int(shard_count), shard_index=int(shard_index),
                        num_threads=int(num_threads), num_slots=int(num_slots), verify_crc=verify_crc,
                        skip_bad=skip_bad, shuffle_buffer=int(shuffle_buffer), seed=int(seed),
-                       stream_mode=stream_mode)
+                       stream_mode=stream_mode, max_batches_per_epoch=int(max_batches_per_epoch))
         self.num_slots = int(num_slots)
         if pin_memory is None:
             pin_memory = torch.cuda.is_available()
@@ -259,22 +292,88 @@ class TFRecordDataset:
         finally:
             self.loader.stop()
 
+    def raw_groups(self, size: int, hold: int = 2, skip: int = 0, limit: Optional[int] = None,
+                   record_bytes: int = 0):
+        """Like ``groups`` but the batches stay undecoded: each item is a ``RawGroup`` of ``n``
+        consecutive full batches whose Example payloads sit back to back in one pinned byte ring
+        (``bytes [n, cap]``, batch k at row k) with their offsets (``offs [n, B+1]`` int32).  The
+        host only resolves frames, checks CRCs and copies bytes; the GPU parses the Examples
+        (``csrc/kernels/decode.hip``, rocfm.models.fused.FusedDeepFM.train_stream).  ``cap`` is
+        ``B × record_bytes`` (default: the longest record of the files' indexes, rounded up to
+        16 B).  Needs file mode with drop_remainder (a partial batch cannot be trained) and no
+        skip_bad (a malformed record is only found on the device)."""
+        io = _io_mod()
+        if io is None:
+            raise RuntimeError("rocfm native IO module missing; run `python build.py`")
+        if self.kw["stream_mode"] or not self.kw["drop_remainder"] or self.kw["skip_bad"]:
+            raise ValueError("raw_groups needs file mode, drop_remainder and no skip_bad")
+        size, hold = max(1, int(size)), max(1, int(hold))
+        B = self.B
+        rb = int(record_bytes) or self.max_record_bytes()
+        cap = B * ((rb + 15) // 16 * 16)
+        ns = (hold + 2) * size
+        kw = dict(self.kw, num_slots=ns, skip_batches=int(skip), raw=True, raw_cap=cap)
+        self.loader = io.BatchLoader(self.files, **kw)
+        raw = torch.zeros(ns, cap, dtype=torch.uint8, pin_memory=self.pin)
+        offs = torch.zeros(ns, B + 1, dtype=torch.int32, pin_memory=self.pin)
+        for i in range(ns):
+            self.loader.set_raw_slot(i, raw[i].data_ptr(), offs[i].data_ptr())
+        self.loader.start()
+        held = []
+        left = -1 if limit is None else int(limit)
+        try:
+            while left != 0:
+                first, n, rows, epoch = self.loader.next_group(size if left < 0 else min(size, left))
+                while len(held) >= hold or (n == 0 and held):
+                    self.loader.release_group(*held.pop(0))
+                if n == 0:
+                    break
+                held.append((first, n))
+                left -= n if left > 0 else 0
+                yield RawGroup(raw[first:first + n], offs[first:first + n], n, B)
+        finally:
+            self.loader.stop()
+
+    def max_record_bytes(self) -> int:
+        """Longest Example payload over the files (from their saved indexes; built when missing)."""
+        io = _io_mod()
+        m = 0
+        for f in self.files:
+            info = io.index_info(f)
+            if info is None:
+                io.build_index(f, bool(self.kw["verify_crc"]))
+                info = io.index_info(f)
+            if info is None:  # unwritable directory: walk the framing for the lengths
+                m = max([m] + list(io.scan_file(f, False, False)[2]))
+            else:
+                m = max(m, int(info[1]))
+        return max(m, 16)
+
     def num_batches(self) -> Optional[int]:
         """Batches this shard will yield over all epochs (file mode; None for a stream/FIFO source).
 
-        Counts records by walking the framing only (C++ ``count_records``), then applies the
-        record-index sharding and the per-epoch drop_remainder of the loader.  Upper bound when
-        ``skip_bad`` drops corrupt records."""
+        Counts records from the files' saved indexes (or by walking the framing only, C++
+        ``count_records``), then applies the record-index sharding, the per-epoch drop_remainder
+        and the per-epoch cap of the loader.  Upper bound when ``skip_bad`` drops corrupt records."""
+        if self.kw["stream_mode"]:
+            return None
+        return self.batches_per_epoch() * self.kw["num_epochs"]
+
+    def batches_per_epoch(self) -> Optional[int]:
         if self.kw["stream_mode"]:
             return None
         io = _io_mod()
         if io is None:
             raise RuntimeError("rocfm native IO module missing; run `python build.py`")
-        N = sum(int(io.count_records(f)) for f in self.files)
+        N = 0
+        for f in self.files:
+            info = io.index_info(f)
+            N += int(info[0]) if info is not None else int(io.count_records(f))
         c, i = self.kw["shard_count"], self.kw["shard_index"]
         n = (N - i + c - 1) // c if N > i else 0
         per_epoch = n // self.B if self.kw["drop_remainder"] else (n + self.B - 1) // self.B
-        return per_epoch * self.kw["num_epochs"]
+        cap = int(self.kw.get("max_batches_per_epoch", 0))
+        return min(per_epoch, cap) if cap > 0 else per_epoch
 
     @property
     def bad_records(self) -> int:

@@ -193,9 +193,14 @@ class Estimator:
         cfg = self.cfg
         S = 16
         ds = self._dataset(files, num_epochs, training=True)
-        limit = self._agreed_steps(ds)
-        if limit is not None:
-            limit = max(0, limit - skip_batches)
+        # several ranks: every step is collective, so the ranks agree on a common number of
+        # batches per epoch (the minimum of their shards'; the surplus of longer shards is dropped
+        # each epoch, like drop_remainder)
+        per_epoch = self._agreed_epoch_batches(ds)
+        limit = None
+        if per_epoch is not None:
+            ds.kw["max_batches_per_epoch"] = per_epoch
+            limit = max(0, per_epoch * num_epochs - skip_batches)
         if max_steps:
             limit = max_steps if limit is None else min(limit, max_steps)
         # fused engine + graphs: groups of S batches decoded into one pinned ring, moved by the
@@ -206,8 +211,19 @@ class Estimator:
         stream = self.engine_name == "fused" and cfg.use_hip_graph and self.device.type == "cuda" \
             and hasattr(self.eng, "train_stream") and getattr(self.eng, "graph_collectives", True) \
             and (self.world == 1 or limit is not None)
+        # device-side Example parsing: the loader hands the graphs' copy stream undecoded payloads
+        # (raw_groups) and the GPU parses them (decode.hip); the host only frames, checks CRCs and
+        # copies bytes.  Not for pipe mode, skip_bad or the decoded on-disk cache (host batches).
+        raw = stream and cfg.device_decode and not cfg.pipe_mode and cfg.on_bad_record != "skip" \
+            and not cfg.decoded_cache_dir
+
+        def groups_of(d, skip=0, lim=None):
+            if raw:
+                return d.raw_groups(S, hold=2, skip=skip, limit=lim)
+            return self._host_batches(d.groups(S, hold=2, skip=skip, limit=lim))
+
         if stream:
-            batches = self._host_batches(ds.groups(S, hold=2, skip=skip_batches, limit=limit))
+            batches = groups_of(ds, skip_batches, limit)
         else:
             batches = self._device_batches(_skip(ds, skip_batches))
             if limit is not None:
@@ -259,17 +275,20 @@ class Estimator:
             if faults:
                 faults.after_step(step)
 
-        # decoded-epoch HBM cache (single GPU, several epochs of the same files, no shuffle): epoch 1
-        # streams from the loader into an HBM ring sized for the whole epoch, epochs 2.. replay it
-        # from HBM (the reference's tf.data re-reads and re-parses every epoch, PS:147-165)
+        # decoded-epoch HBM cache (several epochs of the same files, no shuffle; every rank its own
+        # shard): epoch 1 streams from the loader into an HBM ring sized for the whole epoch,
+        # epochs 2.. replay it from HBM (the reference's tf.data re-reads and re-parses every
+        # epoch, PS:147-165).  Several ranks cache their agreed per-epoch batches.
         cache_nb = 0
         if stream and num_epochs > 1 and cfg.hbm_cache and not cfg.perform_shuffle and skip_batches == 0 \
-                and not cfg.pipe_mode and limit is None and not max_steps:
-            nb = self._dataset(files, 1, training=True).num_batches()
+                and not cfg.pipe_mode and not max_steps and (self.world == 1 or per_epoch is not None):
+            ds1 = self._dataset(files, 1, training=True)
+            if per_epoch is not None:
+                ds1.kw["max_batches_per_epoch"] = per_epoch
+            nb = ds1.num_batches()
             if nb and nb * cfg.batch_size * (8 * cfg.field_size + 4) <= cfg.hbm_cache_gb * (1 << 30):
                 cache_nb = nb
-                batches = self._host_batches(self._dataset(files, 1, training=True).groups(S, hold=2))
-                batches = _timed(batches, timer)
+                batches = _timed(groups_of(ds1), timer)
         # pre-decoded on-disk cache (rocfm.data.cache): the first pass over this rank's shard is
         # written through, every later pass (later epochs, restarted or repeated jobs) memory-maps it
         if stream and cfg.decoded_cache_dir and not cfg.perform_shuffle and not cfg.pipe_mode \
@@ -357,13 +376,14 @@ class Estimator:
             self._ctrl = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
         return self._ctrl
 
-    def _agreed_steps(self, ds) -> Optional[int]:
+    def _agreed_epoch_batches(self, ds) -> Optional[int]:
         """Every rank must run the same number of synchronous steps (each step is a collective).
-        File mode: the minimum over ranks of the shard's batch count (records counted from the
-        framing); the surplus batches of longer shards are dropped, like drop_remainder."""
+        File mode: the minimum over ranks of the shard's batches per epoch (records counted from
+        the files' indexes); the surplus batches of longer shards are dropped every epoch, like
+        drop_remainder.  None at world 1, and in pipe mode / with skip_bad (lockstep instead)."""
         if self.world == 1:
             return None
-        n = ds.num_batches() if self.cfg.on_bad_record != "skip" else None
+        n = ds.batches_per_epoch() if self.cfg.on_bad_record != "skip" else None
         t = torch.tensor([n if n is not None else -1], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctrl_group())
         return int(t.item()) if int(t.item()) >= 0 else None
@@ -507,7 +527,7 @@ class Estimator:
             return 0, 0
         per_epoch = self._dataset(files, 1, training=True).num_batches()
         if self.world > 1:
-            # train() runs the MIN over ranks of the shard batch counts (_agreed_steps); the
+            # train() runs the MIN over ranks of the shard batch counts (_agreed_epoch_batches); the
             # resume split must use that same agreed count on every rank, or ranks with one
             # more batch per epoch skip differently and run different numbers of collective steps
             t = torch.tensor([per_epoch if per_epoch is not None else -1], dtype=torch.int64)

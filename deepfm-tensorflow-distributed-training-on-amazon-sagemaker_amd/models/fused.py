@@ -32,6 +32,7 @@ from typing import Dict, List, Optional
 
 import torch
 
+from ..data.tfrecord import RawGroup
 from ..optim import OPT_ID, OptHParams, init_slots, slot_names
 from ..ops import require_hip
 from ..utils import hazard
@@ -1005,8 +1006,12 @@ class FusedDeepFM:
         batches).  A graph waits only for the copies of the batches its side chain reads, and a
         copy only for the graph that last read its slots (three graphs back), so the host, which
         stages copies and launches one graph per S steps, runs up to two graphs ahead of the GPU.
-        Items are single batches ``(ids [B,F], vals [B,F], labels [B])`` or groups of n ≤ S
-        consecutive batches stacked ``[n,B,F]`` (``TFRecordDataset.groups``: one copy per group).
+        Items are single batches ``(ids [B,F], vals [B,F], labels [B])``, groups of n ≤ S
+        consecutive batches stacked ``[n,B,F]`` (``TFRecordDataset.groups``: one copy per group),
+        or undecoded ``RawGroup``s (``TFRecordDataset.raw_groups``): their Example payload bytes
+        are copied as they are and parsed on the copy stream by the decode kernel straight into
+        the ring slots (``csrc/kernels/decode.hip``) — the host only moves bytes.  A malformed
+        record raises RuntimeError within two groups (its batch trains on zeros until then).
         The source may recycle an item's host memory once it has been advanced ``hold`` more
         times; the copy of every such item is waited for first.  Returns the number of steps
         trained; ``after_steps(first_step, n_steps)`` runs after each graph launch.
@@ -1056,6 +1061,21 @@ class FusedDeepFM:
                     b = next(it, None)
                     if b is None:
                         break
+                if isinstance(b, RawGroup):
+                    if b.B != self.B:
+                        raise ValueError(f"batch has {b.B} rows, engine built for {self.B}")
+                    n = b.n
+                    if got + n > k:  # split: the rest goes to the next graph's staging
+                        m = k - got
+                        carry[0] = RawGroup(b.bytes[m:], b.offs[m:], n - m, b.B)
+                        b, n = RawGroup(b.bytes[:m], b.offs[:m], m, b.B), m
+                    with torch.cuda.stream(copy):
+                        self._stage_raw(b, staged % R, R, staged)
+                    pending.append((mark(copy), b))
+                    staged += n
+                    got += n
+                    self._check_decode(block=False)
+                    continue
                 ids, vals, labels = b
                 if ids.dim() == 2:
                     ids, vals, labels = ids.unsqueeze(0), vals.unsqueeze(0), labels.unsqueeze(0)
@@ -1117,8 +1137,57 @@ class FusedDeepFM:
         main.wait_stream(self.sort_stream)
         for e0, _ in pending:
             e0.synchronize()
+        self._check_decode(block=True)
         self._primed = False
         return done
+
+    # ---- device-side Example parsing (raw groups) ----------------------------------------------
+    def _stage_raw(self, g, slot0: int, R: int, batch0: int) -> None:
+        """On the current (copy) stream: H2D-copy a RawGroup's payload bytes + offsets and parse
+        them into ring slots slot0 .. slot0+n-1 (mod R)."""
+        H, n, cap = self.H, g.n, int(g.bytes.shape[1])
+        st = getattr(self, "_raw_dev", None)
+        if st is None or st[0].numel() < n * cap + 64 or st[1].shape[0] < n or st[1].shape[1] != self.B + 1:
+            d_bytes = torch.empty(n * cap + 64, dtype=torch.uint8, device=self.device)  # +64: window reads
+            d_offs = torch.empty(n, self.B + 1, dtype=torch.int32, device=self.device)
+            d_err = torch.zeros(4, dtype=torch.int32, device=self.device)
+            h_err = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+            st = self._raw_dev = [d_bytes, d_offs, d_err, h_err, None]
+        d_bytes, d_offs, d_err, h_err, _ = st
+        used = g.used_bytes()
+        d_bytes[:used].copy_(g.bytes.reshape(-1)[:used], non_blocking=True)
+        d_offs[:n].copy_(g.offs, non_blocking=True)
+        p = H.DecodeParams()
+        p.bytes, p.offs, p.cap, p.nb, p.B, p.F = d_bytes.data_ptr(), d_offs.data_ptr(), cap, n, self.B, self.F
+        ring = self._stream_ring
+        p.ids, p.vals, p.labels = ring[0].data_ptr(), ring[1].data_ptr(), ring[2].data_ptr()
+        p.slot0, p.R, p.max_id, p.batch0, p.err = int(slot0), int(R), int(self.id_limit), int(batch0), d_err.data_ptr()
+        keys = getattr(self, "decode_keys", ("label", "ids", "values"))
+        p.set_keys(*keys)
+        H.decode_examples(p, torch.cuda.current_stream(self.device).cuda_stream)
+        h_err.copy_(d_err, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        st[4] = ev
+
+    def _check_decode(self, block: bool) -> None:
+        """Raise on the decode kernel's sticky error word (tfrecord.h ParseStatus codes)."""
+        st = getattr(self, "_raw_dev", None)
+        if st is None or st[4] is None:
+            return
+        if block:
+            st[4].synchronize()
+        elif not st[4].query():
+            return
+        code, batch, rec = (int(x) for x in st[3][:3])
+        if code:
+            names = {1: "malformed Example protobuf", 2: "missing feature",
+                     3: "wrong feature length (FixedLenFeature expects field_size values)",
+                     4: "id out of range [0, feature_size)", 5: "bad record offsets"}
+            st[2].zero_()
+            st[3].zero_()
+            raise RuntimeError(f"decode error in batch {batch} record {rec} (device parse): "
+                               f"{names.get(code, code)}")
 
     def stream_ring(self):
         """The HBM ring of the last train_stream call (ids, vals, labels)."""

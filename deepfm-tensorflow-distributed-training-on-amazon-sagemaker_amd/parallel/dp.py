@@ -229,6 +229,9 @@ def shadow_prefix(w, batches, after_steps=None):
     FusedDeepFM.train_stream; a group that straddles the window's end is split."""
     import itertools
 
+    from ..data.tfrecord import RawGroup
+    from ..ops.decode import PARSE_STATUS, decode_on_device
+
     shadow = getattr(w, "shadow", None)
     if shadow is None or not shadow.active:
         return batches, 0
@@ -239,6 +242,17 @@ def shadow_prefix(w, batches, after_steps=None):
         b = next(it, None)
         if b is None:
             break
+        if isinstance(b, RawGroup):  # undecoded batches: parsed on the device for the shadow steps
+            k = min(b.n, shadow.left - len(got))
+            ids, vals, labels, err = decode_on_device(b.bytes, b.offs, k, b.B, w.eng.F, dev, w.eng.id_limit,
+                                                      getattr(w.eng, "decode_keys", ("label", "ids", "values")))
+            if int(err[0]):
+                raise RuntimeError(f"decode error in batch {int(err[1])} record {int(err[2])} (device parse): "
+                                   f"{PARSE_STATUS.get(int(err[0]))}")
+            got += [(ids[i], vals[i], labels[i]) for i in range(k)]
+            if k < b.n:
+                rest.append(RawGroup(b.bytes[k:].clone(), b.offs[k:].clone(), b.n - k, b.B))
+            continue
         ids, vals, labels = b
         if ids.dim() == 2:
             ids, vals, labels = ids.unsqueeze(0), vals.unsqueeze(0), labels.unsqueeze(0)
@@ -667,11 +681,17 @@ class FusedDataParallel:
         """Main chain of one S-step DP graph (the side graph is launched by FusedDeepFM._launch_multi)."""
         e, H = self.eng, self.eng.H
         s = torch.cuda.current_stream(self.device).cuda_stream
+        v = getattr(self, "_variant", None)  # phase_windows: a truncated step (diagnostic only)
         for k in range(S):
             rows, wp, ep, da, ed, mg = self.m_dp[q][k]
             H.deepfm_rows(rows, s)  # (dp: also zeroes the export counter)
+            if v == "rows":
+                continue
             e._tail(wp, ep, None, s)
-            self._exchange()
+            if v == "compute":
+                continue
+            if v is None:
+                self._exchange()
             if self.mode == "dp" and self.range:
                 H.merge_range_apply(mg, da, s)  # bucketed row merge ‖ MLP optimizer, one launch
                 if ed is not None:
@@ -702,6 +722,58 @@ class FusedDataParallel:
             self._after_steps(e._i - S, e._i)
         torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
         e._primed = False
+
+    def phase_windows(self, steps: int = 64, steps_per_graph: int = 16) -> Dict[str, Dict[str, float]]:
+        """Per-rank device time of the multi-step DP step's phases, min / max over ranks (ms/step).
+
+        Diagnostic, run AFTER a measurement (it trains on stale exchange data and may leave the
+        replicas inconsistent): truncated variants of the step graph are replayed ``steps`` times
+        each — rows only; rows + tail (wgrad ‖ embedding export); + the merge (row merge ‖ MLP
+        optimizer) without the exchange; the full step — and the phase times are their
+        differences: rows, tail, merge, exchange (push / all-gather incl. the wait for the
+        slowest peer).  Collective: every rank must call it."""
+        e = self.eng
+        if self.mode != "dp" or not (self.graph_collectives and self.use_graph) or self.shadow.active:
+            raise RuntimeError("phase_windows needs the multi-step DP graphs (mode dp, capturable exchange)")
+        S = int(steps_per_graph)
+        if getattr(self, "_m_dp_S", None) != S or getattr(e, "_m_pool", None) is not e.pool_ids:
+            self._build_multi_dp(S)
+        if not e._m_primed:
+            e._prime_multi()
+        t = {}
+        try:
+            for v in ("rows", "compute", "merge", None):
+                self._variant = v
+                key = ("mdp", v or "full")
+                for _ in range(2):  # both parities captured outside the timed replays
+                    e._launch_multi(self._graphs, key, S, self._enqueue_multi_dp, capture_error_mode="thread_local")
+                torch.cuda.synchronize(self.device)
+                n = max(1, steps // S)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(n):
+                    e._launch_multi(self._graphs, key, S, self._enqueue_multi_dp, capture_error_mode="thread_local")
+                b.record()
+                torch.cuda.synchronize(self.device)
+                t[v or "full"] = a.elapsed_time(b) / (n * S)
+        finally:
+            self._variant = None
+            torch.cuda.current_stream(self.device).wait_stream(e.sort_stream)
+            e._primed = False
+        ph = {"rows": t["rows"], "tail": t["compute"] - t["rows"], "merge": t["merge"] - t["compute"],
+              "exchange": t["full"] - t["merge"], "step": t["full"]}
+        names = list(ph)
+        x = torch.tensor([ph[k] for k in names] + [-ph[k] for k in names], dtype=torch.float64,
+                         device=self.device if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        n = len(names)
+        out = {k: {"max": round(float(x[i]), 4), "min": round(-float(x[n + i]), 4)} for i, k in enumerate(names)}
+        out["merge_mode"] = ("range" if self.range else "search+dir" if (self.m_sorted and self.sdir)
+                             else "search" if self.m_sorted else "maps")
+        out["cap"] = int(self.cap)
+        out["push"] = "fused" if self.fused_push else ("copy" if self.p2p is not None else "collective")
+        return out
 
     def precapture(self, n: int, steps_per_graph: int = 16) -> None:
         """Capture the graphs ``train_steps(n, steps_per_graph)`` will replay (no launch)."""

@@ -42,6 +42,8 @@ def convert(input_path: str, output: str, shards: int = 1, threads: int = 8) -> 
         os.makedirs(os.path.dirname(os.path.abspath(o)), exist_ok=True)
     t0 = time.time()
     n = m.convert_libsvm_sharded(input_path, outs, threads)
+    for o in outs:  # persistent record indexes next to the shards (ranks jump to their records)
+        m.build_index(o, True)
     return {"input": input_path, "outputs": outs, "records": int(n), "seconds": round(time.time() - t0, 3)}
 
 

@@ -1,0 +1,14 @@
+# Round 4: device-side Example parsing + record index + N>1 bench windows — full GPU suite, smoke,
+# TFRecord-fed bench windows, loader aggregate over 1..8 processes (record sharding, index)
+set -e
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4a
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_decode_gpu.py -x -v --timeout 120 --timeout-method thread > $O/decode_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --loader_threads 4 > $O/tf_t4.log 2>&1
+timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --loader_threads 8 > $O/tf_t8.log 2>&1
+timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --loader_threads 16 --host_decode > $O/tf_host16.log 2>&1
+timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/b20.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputests.log 2>&1
+timeout -k 10 600 python tools/loader_aggregate.py --procs 1,2,4,8 --threads 2 --records 800000 --modes raw,tfrecord --shard_policy record --json $O/loader_agg.json > $O/loader_agg.log 2>&1

@@ -13,7 +13,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 SRCS = [os.path.join(CSRC, "tests", "sanitize_io.cpp"), os.path.join(CSRC, "io", "tfrecord.cpp"),
-        os.path.join(CSRC, "io", "loader.cpp")]
+        os.path.join(CSRC, "io", "loader.cpp"), os.path.join(CSRC, "io", "record_index.cpp")]
 
 
 def _build_and_run(tmp_path, flags, iters):

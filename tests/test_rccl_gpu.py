@@ -102,17 +102,29 @@ def _bench(args, env_extra, timeout=300):
     return json.loads(lines[0]), r.stdout + r.stderr
 
 
+@pytest.mark.timeout(600)
 def test_bench_rehearsal_4_ranks_gloo_p2p():
     """bench.py --gpus 4 relaunches itself under torch.distributed.run; 4 ranks share the GPU (gloo
     bootstrap), the DP exchange is the p2p push through multi-step graphs."""
     j, log = _bench(["--gpus", "4", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
-                    {"ROCFM_BENCH_BACKEND": "gloo"})
+                    {"ROCFM_BENCH_BACKEND": "gloo"}, timeout=600)
     assert j["n_gpus"] == 4 and j["world_size"] == 4 and j["backend"] == "gloo", j
     # ranks sharing the GPU: the copy push (the fused one is the default with one GPU per rank)
     assert j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is False, (j, log[-2000:])
     assert j["config"]["parallelism"] == "dp4" and j["config"]["global_batch"] == 4096, j
     assert j["value"] > 0 and j["rank_ms_per_step"]["max"] >= j["rank_ms_per_step"]["min"] > 0, j
     assert "falling back" not in log, log[-2000:]
+    # the node run's attribution: per-rank phase times of the headline step, what ran, and the
+    # secondary windows (collective transport A/B, config 4 at 100M rows) each with its own checks
+    ph = j["phase_ms"]
+    for k in ("rows", "tail", "merge", "exchange", "step"):
+        assert ph[k]["max"] >= ph[k]["min"], (k, ph)
+    assert ph["step"]["min"] > 0 and ph["merge_mode"] and ph["cap"] > 0 and ph["push"] == "copy", ph
+    assert not [k for k in j if k.endswith("_error")], j
+    for w in ("rccl", "rowshard"):
+        assert j[f"{w}_examples_per_sec"] > 0 and j[f"{w}_replicas_consistent"] is True, (w, j)
+    assert j["rowshard_exchange"] == "p2p" and j["rowshard_shadow_exchange"] == "ok", j
+    assert j["rowshard_feature_size"] == 100_000_000, j
 
 
 def test_bench_rehearsal_2_ranks_fused_push():

@@ -4,7 +4,8 @@
 An 8-GPU job runs one process per GPU, each decoding its own shard of the training files with the
 C++ loader (rocfm.data.tfrecord, csrc/io).  This measures what P such processes decode together on
 this host, next to the per-process rate and the rate of reading the same batches from the
-pre-decoded on-disk cache (rocfm.data.cache), so the loader's margin over P GPUs can be read off:
+pre-decoded on-disk cache (rocfm.data.cache) and of the raw mode that leaves the Example parsing to
+the GPU (csrc/kernels/decode.hip), so the loader's margin over P GPUs can be read off:
 
     python tools/loader_aggregate.py --procs 1,2,4,8 --threads 4 --records 400000 [--json out.json]
 
@@ -42,12 +43,17 @@ def _worker(files, rank, procs, threads, B, F, V, mode, cache_dir, q, bar, polic
             for _ in cache.write_through(ds.groups(16, hold=2)):
                 pass
         src = cache.groups(16, pin_memory=False)
+    elif mode == "raw":  # undecoded payloads for the GPU parser (the fused engine's streaming input)
+        src = ds.raw_groups(16, hold=2)
     else:
         src = ds.groups(16, hold=2)
     bar.wait()  # every process starts its timed pass together (cache mode: after its first pass)
     t0 = time.perf_counter()
     n = 0
     for g in src:
+        if mode == "raw":
+            n += g.n
+            continue
         n += int(g[0].shape[0]) if g[0].dim() == 3 else 1
     q.put((rank, n * B, time.perf_counter() - t0))
 
@@ -77,7 +83,8 @@ def main():
     ap.add_argument("--files", type=int, default=8)
     ap.add_argument("--batch_size", type=int, default=1024)
     ap.add_argument("--feature_size", type=int, default=1_000_000)
-    ap.add_argument("--modes", default="tfrecord,cache")
+    ap.add_argument("--modes", default="raw,tfrecord,cache",
+                    help="raw (frames + CRCs + payload copy; the GPU parses), tfrecord (host parse), cache")
     ap.add_argument("--shard_policy", default="record,file", help="record (Dataset.shard) and/or file")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
