@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 #include <hip/hip_runtime.h>
 #include "ops.h"
+#include "kernels/wgrad_body.h"  // wgrad_prepare (the wgrad_plan binding)
 
 namespace py = pybind11;
 using namespace rocfm;

@@ -122,7 +122,8 @@ struct WgradParams {
   uint16_t* Wb[kMaxHidden];
   uint16_t* WTs[kMaxHidden];  // frag_swz copies (nullable): WT as [Dout][Din], Wb as [Din][Dout]
   uint16_t* Wbs[kMaxHidden];
-  int tile_start[kMaxHidden + 1];  // prefix sums of 32×32 tiles per layer
+  int tile_start[kMaxHidden + 1];  // prefix sums of 32 × (32·tw) tiles per layer
+  int tw[kMaxHidden];              // output subtiles per tile (1, 2, 4; set by wgrad_prepare)
   int bias_start[kMaxHidden + 1];  // prefix sums of 32-column bias blocks per layer
   int fuse_opt;
   OptParams opt;
@@ -134,6 +135,8 @@ struct WgradParams {
   int bn_dmax;
   int off_gamma[kMaxHidden], off_beta[kMaxHidden];
   PushTarget push;  // DP fused push (fuse_opt == 0): gradients go straight into the W receive slots
+  int push_mirror;  // with push: also store every gradient locally (grads) — the shadow exchange
+                    // all-gathers the local buffer and compares it with what the producers pushed
   Fp8W0 w8;         // fused optimizer: refresh the fp8 input-layer copies too (f == nullptr: none)
 };
 

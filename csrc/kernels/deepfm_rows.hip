@@ -1,7 +1,8 @@
 // DeepFM fused row-tile kernel: the whole per-example part of a training step in ONE launch.
 //
-// One 512-thread workgroup (8 waves) owns 16 consecutive examples (one MFMA M-tile) and runs,
-// entirely out of LDS:
+// One 512-thread workgroup (8 waves) owns RT consecutive examples (row_tile: 8 by default — 128
+// workgroups at B = 1024; 16 = one full MFMA M-tile, 4 for small batches; profiles/r3_row_tile.md)
+// and runs, entirely out of LDS:
 //   A  gather fm_v/fm_w rows (f32, 16-B vector loads) → e = V[id]·x, h0 = bf16(e)  (PS:207-213)
 //   B  S = Σ_f e, y_v = ½Σ_k(S² − Σ_f e²), y_w = Σ_f w·x, y_lin = b + y_w + y_v    (PS:214-217)
 //   C  hidden layers: h_{l+1} = dropout(relu(h_l·W_l + c_l)) on v_mfma_f32_16x16x32_bf16
@@ -13,7 +14,8 @@
 // (mlp_wgrad.hip) and the per-lookup gradient rows for the embedding update (emb_update.hip).
 // Nothing reduces across examples, so there are no atomics and no inter-workgroup hand-offs.
 //
-// At the reference's 1024-row batches the kernel is LATENCY-bound (64 workgroups for 256 CUs):
+// At the reference's 1024-row batches the kernel is LATENCY-bound (128 workgroups for 256 CUs,
+// one wave per SIMD):
 // its time is the chain of dependent memory round trips plus each wave's serial instruction
 // stream.  So:
 //  * every phase issues all of its global loads before consuming any (flattened gather items);

@@ -286,6 +286,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
             const int v = bb <= bc ? slot : s_total;
             if (push) {
               for (int d = 0; d < p.push.W; ++d) reinterpret_cast<int32_t*>(p.push.slot[d] + p.push_off_dir)[bb] = v;
+              if (p.push_mirror && p.out_dir) p.out_dir[bb] = v;
             } else {
               p.out_dir[bb] = v;
             }
@@ -298,6 +299,10 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
               float* b = p.push.slot[d];
               reinterpret_cast<float4*>(b + p.push_off_rows)[(size_t)slot * KP4 + u4] = g[u];
               if (u4 == 0) reinterpret_cast<uint32_t*>(b + p.push_off_keys)[slot] = row_id;
+            }
+            if (p.push_mirror) {  // the shadow exchange's local reference (DP export)
+              reinterpret_cast<float4*>(p.out_rows)[(size_t)slot * KP4 + u4] = g[u];
+              if (u4 == 0) p.out_keys[slot] = row_id;
             }
           } else {
             reinterpret_cast<float4*>(p.out_rows)[(size_t)slot * KP4 + u4] = g[u];  // pad columns are 0

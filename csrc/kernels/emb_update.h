@@ -54,9 +54,10 @@ struct EmbUpdateParams {
   PushTarget push;
   int push_off_keys, push_off_rows;
   int push_seg;
-  // row-shard X3 push: also store each row gradient locally (dense_grad[rr]) — the shadow exchange
-  // (rocfm.parallel.validate) all-to-alls that local copy through RCCL and compares it bitwise
-  // with what the producers pushed into the owners' slots
+  // with push: also store each result locally — row-shard X3: every row gradient (dense_grad[rr]);
+  // DP export (mode 2): keys / rows / directory (out_keys, out_rows, out_dir).  The shadow
+  // exchange (rocfm.parallel.validate) sends that local copy through RCCL and compares it bitwise
+  // with what the producers pushed into the peers' slots
   int push_mirror;
   // nullable: the entry count is this device word (per-tile dedup: the compacted list's length,
   // written by the side chain); n is then the maximum and sizes the grid

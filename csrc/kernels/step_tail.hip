@@ -25,6 +25,15 @@ int tail_chunk_entries() {
   }();
   return n;
 }
+// compute units of the current device (the step tail sizes its roles to one dispatch round)
+static int tail_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
@@ -60,8 +69,8 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= kTailMaxKp && e.K1 <= e.Kp,
                 "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
-  const int n_wg = wgrad_prepare(w);
   const int n_emb = e.n > 0 ? cdiv(e.n, tail_chunk_entries()) : 0;
+  const int n_wg = wgrad_prepare(w, n_emb, tail_cus());  // both roles in one dispatch round
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
   const bool push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);

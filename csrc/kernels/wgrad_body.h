@@ -2,6 +2,8 @@
 #pragma once
 #include "deepfm_rows.h"
 
+#include <cstdlib>
+
 namespace rocfm {
 
 namespace {
@@ -12,6 +14,7 @@ template <bool PUSH>
 __device__ __forceinline__ void put_grad(const WgradParams& p, int idx, float g) {
   if (PUSH && p.push.W > 0) {
     for (int d = 0; d < p.push.W; ++d) p.push.slot[d][idx] = g;
+    if (p.push_mirror) p.grads[idx] = g;
   } else {
     p.grads[idx] = g;
   }
@@ -72,14 +75,124 @@ __device__ __forceinline__ float fp8_refresh(const Fp8W0& q8, int64_t step, int 
 
 }  // namespace
 
-constexpr int kWgThreads = 512;  // 8 waves: each takes 1/8 of the batch
+constexpr int kWgThreads = 512;  // 8 waves
+
+// One weight-gradient tile of layer li: 32 input rows × TW·32 output columns, dW = actᵀ·dz over the
+// batch.  TW subtiles of 32×32; the 8 waves split the batch 8/TW ways per subtile (wave w → subtile
+// w % TW, batch part w / TW), reduce through LDS, then the fused optimizer / gradient store.
+// TW > 1 (wide tiles, WgradParams::tw) cuts the workgroup count TW-fold for wide layers, so the
+// step tail's wgrad + embedding roles stay within one dispatch round on 256 CUs (the reference's
+// flag defaults, 1248 → 256: 312 32×32 tiles).
+template <bool PUSH, int TW>
+__device__ __forceinline__ void wgrad_tile(const WgradParams& p, const OptStep& st, const int bid, const int li,
+                                           const bool push, const PushSeen& push_seen, float* s_red, float* s_m8) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int Bp = p.Bp;
+  const int Din = p.dims[li], Dout = p.dims[li + 1];
+  const int local = bid - p.tile_start[li];
+  const int nto = Dout / (32 * TW);
+  const int ti = local / nto, to = local % nto;
+  const int sub = wave % TW, part = wave / TW;
+  const int oc = (to * TW + sub) * 32;  // this wave's 32 output columns
+  const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
+  const uint16_t* Bm = p.dzT[li + 1] + (size_t)(oc + (lane & 31)) * Bp + 8 * (lane >> 5);
+  const int q = Bp * TW / 8;  // batch share per wave (Bp % 128 == 0 → a multiple of 16)
+  f32x16 acc = {};
+  const int bs = part * q, be = bs + q;
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b0 = bs; b0 < be; b0 += 16 * 8) {  // 8 k-steps of loads in flight per batch
+    bf16x8 fa[8], fb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = max(bs, min(b0 + 16 * u, be - 16));
+      fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
+      fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b0 + 16 * u >= be) fa[u] = zero;
+      acc = mfma32x32x16(fa[u], fb[u], acc);
+    }
+  }
+  // every wave parks its partial tile in LDS; then all 512 threads own 2·TW tile elements each
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_red[(wave * 16 + r) * 64 + lane] = acc[r];
+  __syncthreads();
+  ROCFM_STAMP(p.stamps, 1);
+  constexpr int NE = 2 * TW;
+  float g[NE], w[NE], a[NE], b[NE];
+  int idx[NE], ii[NE], oo[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int el = t + kWgThreads * e, s = el >> 10, r = (el >> 6) & 15, ln = el & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int h = 0; h < 8 / TW; ++h) v += s_red[((h * TW + s) * 16 + r) * 64 + ln];  // fixed order
+    g[e] = v * p.grad_scale;
+    ii[e] = ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+    oo[e] = (to * TW + s) * 32 + (ln & 31);
+    idx[e] = p.offW[li] + ii[e] * Dout + oo[e];
+  }
+  if (!p.fuse_opt) {
+    if (push) push_wait_ready(p.push, push_seen);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) put_grad<PUSH>(p, idx[e], g[e]);
+    if (push) push_drain();
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    w[e] = p.params[idx[e]];
+    a[e] = p.s0 ? p.s0[idx[e]] : 0.f;
+    b[e] = p.s1 ? p.s1[idx[e]] : 0.f;
+  }
+  __syncthreads();  // s_red is reused below as the transposed bf16 tiles [TW][32][34]
+  uint16_t* s_T = reinterpret_cast<uint16_t*>(s_red);
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    opt_apply(p.opt, st, w[e], g[e], a[e], b[e]);
+    p.params[idx[e]] = w[e];
+    if (p.s0) p.s0[idx[e]] = a[e];
+    if (p.s1) p.s1[idx[e]] = b[e];
+    const uint16_t hw = f2bf(w[e]);
+    p.Wb[li][(size_t)ii[e] * Dout + oo[e]] = hw;  // 64-B runs along o
+    if (p.WTs[li]) {
+      p.WTs[li][frag_swz(oo[e], ii[e], Din)] = hw;
+      p.Wbs[li][frag_swz(ii[e], oo[e], Dout)] = hw;
+    }
+    const int el = t + kWgThreads * e;
+    s_T[(el >> 10) * (32 * 34) + (oo[e] & 31) * 34 + (ii[e] & 31)] = hw;
+  }
+  const bool q8 = li == 0 && p.w8.f;
+  if (q8) {
+    bool ok[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) ok[e] = true;
+    const float m = fp8_refresh<NE>(p.w8, p.step ? *p.step : 0, Din, Dout, ii, oo, w, ok, bid == 0 && t == 0);
+    if (lane == 0) s_m8[wave] = m;
+  }
+  __syncthreads();
+  if (q8 && p.w8.track && t == 0) {  // one atomic per workgroup
+    float m = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWgThreads / 64; ++ww) m = fmaxf(m, s_m8[ww]);
+    atomicMax(reinterpret_cast<unsigned*>(p.w8.amax + (((p.step ? *p.step : 0) + 1) & 1)), __float_as_uint(m));
+  }
+#pragma unroll
+  for (int s = 0; s < TW; ++s) {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
+    const int o = t >> 4, ip = (t & 15) * 2;
+    const uint16_t* T = s_T + s * (32 * 34);
+    const uint32_t v2 = (uint32_t)T[o * 34 + ip] | ((uint32_t)T[o * 34 + ip + 1] << 16);
+    *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)((to * TW + s) * 32 + o) * Din + ti * 32 + ip) = v2;
+  }
+  ROCFM_STAMP(p.stamps, 2);
+}
 
 // PUSH: the fused DP push variant (gradients into the W receive slots, fuse_opt == 0); a
 // compile-time switch so single-GPU tails keep their code unchanged.
 template <bool PUSH = false>
 __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) {
   __shared__ __attribute__((aligned(16))) float s_red[(kWgThreads / 64) * 16 * 64];
-  __shared__ uint16_t s_T[32 * 34];
   __shared__ float s_m8[kWgThreads / 64];  // fp8 refresh: per-wave max |w|
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n_tiles = p.tile_start[p.nl], n_bias = p.bias_start[p.nl];
@@ -94,96 +207,12 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
   if (bid < n_tiles) {
     int li = 0;
     while (bid >= p.tile_start[li + 1]) ++li;
-    const int Din = p.dims[li], Dout = p.dims[li + 1];
-    const int local = bid - p.tile_start[li];
-    const int nto = Dout >> 5;
-    const int ti = local / nto, to = local % nto;
-    const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
-    const uint16_t* Bm = p.dzT[li + 1] + (size_t)(to * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
-    const int q = Bp >> 3;  // batch eighth per wave (Bp % 64 == 0 → q % 8 == 0, a multiple of 16 for Bp >= 128)
-    f32x16 acc = {};
-    const int bs = wave * q, be = bs + q;
-    const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b0 = bs; b0 < be; b0 += 16 * 8) {  // 8 k-steps of loads in flight per batch
-      bf16x8 fa[8], fb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = max(bs, min(b0 + 16 * u, be - 16));
-        fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
-        fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (b0 + 16 * u >= be) fa[u] = zero;
-        acc = mfma32x32x16(fa[u], fb[u], acc);
-      }
-    }
-    // every wave parks its partial tile in LDS; then all 512 threads own 2 tile elements each
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s_red[(wave * 16 + r) * 64 + lane] = acc[r];
-    __syncthreads();
-    ROCFM_STAMP(p.stamps, 1);
-    float g[2], w[2], a[2], b[2];
-    int idx[2], il[2], ol[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int el = t + kWgThreads * e, r = el >> 6, ln = el & 63;
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < kWgThreads / 64; ++ww) v += s_red[(ww * 16 + r) * 64 + ln];
-      g[e] = v * p.grad_scale;
-      il[e] = (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
-      ol[e] = ln & 31;
-      idx[e] = p.offW[li] + (ti * 32 + il[e]) * Dout + to * 32 + ol[e];
-    }
-    if (!p.fuse_opt) {
-      if (push) push_wait_ready(p.push, push_seen);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) put_grad<PUSH>(p, idx[e], g[e]);
-      if (push) push_drain();
-    } else {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        w[e] = p.params[idx[e]];
-        a[e] = p.s0 ? p.s0[idx[e]] : 0.f;
-        b[e] = p.s1 ? p.s1[idx[e]] : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        opt_apply(p.opt, st, w[e], g[e], a[e], b[e]);
-        p.params[idx[e]] = w[e];
-        if (p.s0) p.s0[idx[e]] = a[e];
-        if (p.s1) p.s1[idx[e]] = b[e];
-        const uint16_t hw = f2bf(w[e]);
-        const int ii = ti * 32 + il[e], oo = to * 32 + ol[e];
-        p.Wb[li][(size_t)ii * Dout + oo] = hw;  // 64-B runs along o
-        if (p.WTs[li]) {
-          p.WTs[li][frag_swz(oo, ii, Din)] = hw;
-          p.Wbs[li][frag_swz(ii, oo, Dout)] = hw;
-        }
-        s_T[ol[e] * 34 + il[e]] = hw;
-      }
-      const bool q8 = li == 0 && p.w8.f;
-      if (q8) {
-        const int ii[2] = {ti * 32 + il[0], ti * 32 + il[1]}, oo[2] = {to * 32 + ol[0], to * 32 + ol[1]};
-        const bool ok[2] = {true, true};
-        const float m = fp8_refresh<2>(p.w8, p.step ? *p.step : 0, Din, Dout, ii, oo, w, ok, bid == 0 && t == 0);
-        if (lane == 0) s_m8[wave] = m;
-      }
-      __syncthreads();
-      if (q8 && p.w8.track && t == 0) {  // one atomic per workgroup
-        float m = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < kWgThreads / 64; ++ww) m = fmaxf(m, s_m8[ww]);
-        atomicMax(reinterpret_cast<unsigned*>(p.w8.amax + (((p.step ? *p.step : 0) + 1) & 1)), __float_as_uint(m));
-      }
-      {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
-        const int o = t >> 4, ip = (t & 15) * 2;
-        const uint32_t v2 = (uint32_t)s_T[o * 34 + ip] | ((uint32_t)s_T[o * 34 + ip + 1] << 16);
-        *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)(to * 32 + o) * Din + ti * 32 + ip) = v2;
-      }
-    }
-    ROCFM_STAMP(p.stamps, 2);
+    if (p.tw[li] == 4)
+      wgrad_tile<PUSH, 4>(p, st, bid, li, push, push_seen, s_red, s_m8);
+    else if (p.tw[li] == 2)
+      wgrad_tile<PUSH, 2>(p, st, bid, li, push, push_seen, s_red, s_m8);
+    else
+      wgrad_tile<PUSH, 1>(p, st, bid, li, push, push_seen, s_red, s_m8);
     return;
   }
   // column reductions over the batch: 16 threads per column, 8 chunks (64 rows) in flight each
@@ -315,20 +344,49 @@ __device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, cons
 
 
 // Fills the per-layer tile / bias workgroup offsets; returns the grid size.
-inline int wgrad_prepare(WgradParams& p) {
+// ``co_resident`` (step tail): workgroups of the launch's other role; the tile widths are widened
+// (WgradParams::tw, largest layers first, up to 4 subtiles) until tiles + bias blocks + 1 + the
+// other role fit ``max_wg`` (one dispatch round).  0: plain 32×32 tiles (standalone mlp_wgrad).
+inline int wgrad_prepare(WgradParams& p, int co_resident = -1, int max_wg = 256) {
   ROCFM_REQUIRE(p.Bp % 128 == 0, "mlp_wgrad: Bp must be a multiple of 128");
-  p.tile_start[0] = 0;
-  p.bias_start[0] = 0;
-  for (int l = 0; l < p.nl; ++l) {
-    ROCFM_REQUIRE(p.dims[l] % 32 == 0 && p.dims[l + 1] % 32 == 0, "mlp_wgrad: dims must be padded to 32");
-    p.tile_start[l + 1] = p.tile_start[l] + (p.dims[l] / 32) * (p.dims[l + 1] / 32);
-    p.bias_start[l + 1] = p.bias_start[l] + p.dims[l + 1] / 32;
+  for (int l = 0; l < kMaxHidden; ++l) p.tw[l] = 1;
+  auto fill = [&p] {
+    p.tile_start[0] = 0;
+    p.bias_start[0] = 0;
+    for (int l = 0; l < p.nl; ++l) {
+      ROCFM_REQUIRE(p.dims[l] % 32 == 0 && p.dims[l + 1] % 32 == 0, "mlp_wgrad: dims must be padded to 32");
+      p.tile_start[l + 1] = p.tile_start[l] + (p.dims[l] / 32) * (p.dims[l + 1] / (32 * p.tw[l]));
+      p.bias_start[l + 1] = p.bias_start[l] + p.dims[l + 1] / 32;
+    }
+    for (int l = p.nl + 1; l <= kMaxHidden; ++l) {
+      p.tile_start[l] = p.tile_start[p.nl];
+      p.bias_start[l] = p.bias_start[p.nl];
+    }
+    return p.tile_start[p.nl] + p.bias_start[p.nl] + 1;
+  };
+  int n = fill();
+  if (co_resident < 0) return n;
+  const char* env = getenv("ROCFM_WGRAD_TW");  // A/B: force a width on every layer it divides
+  if (env && *env) {
+    const int f = atoi(env);
+    for (int l = 0; l < p.nl; ++l)
+      if ((f == 2 || f == 4) && p.dims[l + 1] % (32 * f) == 0) p.tw[l] = f;
+    return fill();
   }
-  for (int l = p.nl + 1; l <= kMaxHidden; ++l) {
-    p.tile_start[l] = p.tile_start[p.nl];
-    p.bias_start[l] = p.bias_start[p.nl];
+  while (n + co_resident > max_wg) {  // widen the layer with the most tiles that can still widen
+    int best = -1, bt = 0;
+    for (int l = 0; l < p.nl; ++l) {
+      const int nt = p.tile_start[l + 1] - p.tile_start[l];
+      if (p.tw[l] < 4 && p.dims[l + 1] % (64 * p.tw[l]) == 0 && nt > bt) {
+        best = l;
+        bt = nt;
+      }
+    }
+    if (best < 0) break;
+    p.tw[best] *= 2;
+    n = fill();
   }
-  return p.tile_start[p.nl] + p.bias_start[p.nl] + 1;
+  return n;
 }
 
 }  // namespace rocfm

@@ -81,7 +81,7 @@ def _all_reduce(t: torch.Tensor) -> None:
 # beyond it a scatter into position maps + apply is faster (tools/bench_merge.py on one MI355X,
 # 7.5k keys per rank: W=1 3.9 vs 8.9 µs, W=2 9.8 vs 10.0, W=4 12.8 vs 10.0, W=8 20.6 vs 13.7)
 SEARCH_MAX_W = 2
-MERGE_MAP_BUDGET = 512 << 20
+MERGE_MAP_BUDGET = 512 << 20  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
 
 
 def range_merge_buckets(W: int, cap: int) -> int:
@@ -114,7 +114,7 @@ def range_merge_enabled(W: int) -> bool:
     search / maps merges (profiles/r3_merge_range.md): no gain on Criteo-shape ids, whose
     field-clustered Zipf ids crowd a few key buckets; 8.6 vs 10.6 µs at W = 4 only when the keys
     are first spread by a bijective hash."""
-    return W >= 2 and os.environ.get("ROCFM_MERGE", "auto") == "range"  # bytes of direct-addressing merge maps ((W + 1) × V int32) before hashing
+    return W >= 2 and os.environ.get("ROCFM_MERGE", "auto") == "range"
 
 
 class MergeMaps:
@@ -430,6 +430,7 @@ class FusedDataParallel:
 
         self.shadow = Shadow(e.device, steps=None if (self.p2p is not None and self.world > 1) else 0)
         self.shadow.corrupt = fault_rank("corrupt_push", self.rank)
+        self._set_mirror(self.shadow.active)
         self._shadow_buf = torch.zeros(self.world * self.S, dtype=torch.float32, device=e.device) \
             if self.shadow.active else None
         self._corrupt_replica = fault_rank("corrupt_replica", self.rank)
@@ -555,14 +556,26 @@ class FusedDataParallel:
         self._after_steps(e._i - 1, e._i)
 
     # ---- self-validation (rocfm.parallel.validate) ----------------------------------------------
+    def _set_mirror(self, on: bool) -> None:
+        """Fused push: while the shadow window is open the producers also write their results to
+        the local send buffer (MLP gradients, exported keys / rows / directory), so the shadow's
+        reference is what each producer computed, not what landed in a receive slot."""
+        m = 1 if (on and self.fused_push) else 0
+        for p in range(2):
+            self.eng.wgrad_params[p].push_mirror = m
+            if self.mode == "dp":
+                self.export_params[p].push_mirror = m
+
     def _shadow_exchange(self) -> None:
-        """The p2p all-gather just delivered every rank's slot: gather this rank's own slot through
-        the collective as well, compare bitwise, and let the merge consume the collective's copy."""
+        """The p2p all-gather just delivered every rank's slot: all-gather every rank's LOCAL send
+        buffer (what its producers computed: the copy push's source, or the fused push's mirror)
+        through the collective as well, compare bitwise, and let the merge consume the
+        collective's copy.  A producer that pushed wrong bytes to every slot — a wrong offset, a
+        wrong directory value — therefore mismatches too, not only a transfer that corrupted one
+        receiver's copy."""
         got = self.p2p.recv_tensor(torch.float32, (self.world * self.S,))
-        # this rank's own slot is the reference it contributes: copied before a (test) fault lands
-        own = got[self.rank * self.S:(self.rank + 1) * self.S].clone()
         self.shadow.corrupt_(got)
-        _all_gather_flat(self._shadow_buf, own)
+        _all_gather_flat(self._shadow_buf, self.send)
         self.shadow.compare(got, self._shadow_buf)
 
     def _shadow_finish(self) -> None:
@@ -576,6 +589,7 @@ class FusedDataParallel:
                 print(f"[rocfm] {msg}", flush=True)
             self._fallback_to_collective()
         self._shadow_buf = None
+        self._set_mirror(False)
 
     def _fallback_to_collective(self) -> None:
         """Agreed switch from the p2p push to the process group's all-gather (every rank)."""

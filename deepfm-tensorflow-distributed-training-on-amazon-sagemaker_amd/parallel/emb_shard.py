@@ -573,9 +573,11 @@ class FusedRowShard:
         self._set_mirror(self.shadow.active)
 
     def _set_mirror(self, on: bool) -> None:
-        """X3 producer push: also keep each row gradient in grad_stage (the shadow's local copy)."""
+        """Producer pushes: also keep each result locally while the shadow window is open — X3 row
+        gradients in grad_stage, X4 MLP gradients in the MLP bucket (the shadow's local copies)."""
         for p in range(2):
             self.eng.emb_params[p].push_mirror = 1 if (on and self.grad_push is not None) else 0
+            self.eng.wgrad_params[p].push_mirror = 1 if (on and self.mlp_push is not None) else 0
 
     def _bind_exchange(self, exs) -> None:
         """Receive-side buffers of the X1-X4 exchanges: the peer-mapped p2p slots (``exs``), the
@@ -745,7 +747,9 @@ class FusedRowShard:
             if prm is None:
                 prm = self._p2p_params["x5"] = self.x_bc.params(self.x5_send.data_ptr(), 4)
             self.x_bc.push(prm)
-            if self.shadow.active:  # an all-gather: this rank's own slot holds its list
+            if self.shadow.active:  # an all-gather: this rank's own slot holds its list (the merge
+                # pushes the rows straight into the slots and keeps no local copy, so this check
+                # covers the transfer and the receivers' agreement, not the owner's row values)
                 from .dp import _all_gather_flat
 
                 sl = self.bc_slot
@@ -1083,15 +1087,16 @@ class FusedRowShard:
         if self.exchange == "p2p":
             _, prm = self._mlp_prm()
             self.x_mlp.push(prm)
-            if self.shadow.active:  # X4 is an all-gather: this rank's own slot holds its payload
-                from .dp import _all_gather_flat
+            if self.shadow.active:  # X4 is an all-gather of every rank's local MLP bucket (the copy
+                from .dp import _all_gather_flat  # push's source, or the fused push's mirror)
 
                 got = self.x_mlp.recv_tensor(torch.float32, (self.W * self.x_mlp.slot,))
                 sl = self.x_mlp.slot
-                own = got[self.rank * sl:(self.rank + 1) * sl].clone()  # (before a fault hits the copy)
+                loc = torch.zeros(sl, dtype=torch.float32, device=self.device)
+                loc[:self.PX].copy_(self.mlp_bucket)
                 self.shadow.corrupt_(got)
                 want = torch.empty_like(got)
-                _all_gather_flat(want, own)
+                _all_gather_flat(want, loc)
                 self.shadow.compare(got, want)
         elif self.W > 1 or self.force:
             all_reduce_(self.mlp_bucket)  # MLP grads + replicated-row sums, one collective
@@ -1176,6 +1181,10 @@ class FusedRowShard:
         if self.shadow.finish():
             msg = (f"row-shard exchange: p2p results differed from the collective in the first "
                    f"{self.shadow.compared} validated exchanges on some rank; falling back to RCCL")
+            if self.replicate:  # the collective X5 gathers every owner's whole list each step
+                msg += (f"; dp_owner's X5 row broadcast then all-gathers {self.W * self.S5 * 4 / 2**20:.1f} MiB "
+                        f"per rank per step (W x the {self.S5 * 4 / 2**20:.1f} MiB list capacity, however few "
+                        f"rows changed)")
             log.warning(msg)
             if self.rank == 0:
                 print(f"[rocfm] {msg}", flush=True)

@@ -12,8 +12,11 @@ run checks itself:
   gathered rank segments in rank order), so ANY difference is a bug.  Engines run it in ``check()``.
 * **Shadow exchange** (``Shadow``): for the first ``ROCFM_SHADOW_STEPS`` (default 8) steps of a p2p
   run, every exchange is ALSO done through the process group's collective (RCCL) from the data
-  each rank holds locally; the two results are compared bitwise and the collective's result is
-  what the step consumes.  After the window the ranks agree: any mismatch anywhere → every rank
+  each rank holds locally — its send buffer, which producer-side pushes mirror during the window
+  (DP export + MLP gradients, row-shard X3 / X4); the dp_owner X5 row broadcast has no local
+  copy and is checked from the owner's own receive slot, i.e. for transfer and receiver
+  agreement only — the two results are compared bitwise and the collective's result is what the
+  step consumes.  After the window the ranks agree: any mismatch anywhere → every rank
   falls back to RCCL (replicas stay consistent, because the validated steps used RCCL's data).
 
 ``ROCFM_FAULT=corrupt_push:R`` makes rank R flip one received word of every shadowed p2p exchange

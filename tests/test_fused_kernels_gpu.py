@@ -39,11 +39,15 @@ def _ref_inputs(eng: FusedDeepFM, spec: ModelSpec, step: int, keeps):
     return emb, layers, w_out, b_out, fmb, masks
 
 
-@pytest.mark.parametrize("K,layers,generic", [(10, [128, 64, 32], False), (10, [128, 64, 32], True),
-                                              (32, [256, 128, 64], False), (8, [48, 16], False),
-                                              (10, [64, 32], False), (32, [128, 64, 32], False),
-                                              (32, [128, 64, 32], True), (32, [256, 128, 64], True)])
-def test_fused_step_gradients_match_oracle(K, layers, generic):
+@pytest.mark.parametrize("K,layers,generic,tw", [
+    (10, [128, 64, 32], False, 0), (10, [128, 64, 32], True, 0), (32, [256, 128, 64], False, 0), (8, [48, 16], False, 0),
+    (10, [64, 32], False, 0), (32, [128, 64, 32], False, 0), (32, [128, 64, 32], True, 0), (32, [256, 128, 64], True, 0),
+    # wide weight-gradient tiles (32 × 64 / 32 × 128: the step tail's one-dispatch-round layout for
+    # wide layers, forced here on every layer they divide)
+    (32, [256, 128, 64], False, 4), (10, [128, 64, 32], False, 2), (32, [128, 64, 32], True, 4)])
+def test_fused_step_gradients_match_oracle(K, layers, generic, tw, monkeypatch):
+    if tw:
+        monkeypatch.setenv("ROCFM_WGRAD_TW", str(tw))
     torch.manual_seed(0)
     dev = torch.device("cuda")
     V, F, B = 5000, 39, 192

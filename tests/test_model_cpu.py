@@ -200,3 +200,30 @@ def test_fused_reference_batch_norm_vs_autograd(monkeypatch, exact):
     # the oracle's probabilities match the model's training-mode forward
     ptol = dict(rtol=1e-5, atol=1e-6) if exact else dict(rtol=2e-2, atol=2e-3)
     torch.testing.assert_close(ref["prob"], torch.sigmoid(y.detach()), **ptol)
+
+
+def test_step_tail_wgrad_plan_fits_one_dispatch_round():
+    """The step tail widens the weight-gradient tiles of wide layers until its two roles fit the
+    256 CUs in one round (as far as 32 × 128 tiles go) (csrc/kernels/wgrad_body.h wgrad_prepare): the reference's flag defaults
+    (39·32 → 256-128-64) and the notebook MLP go from two rounds to one; the bench shape keeps its
+    32×32 tiles."""
+    import os
+
+    import pytest
+
+    from rocfm.ops import hip
+
+    H = hip()
+    if H is None or not hasattr(H, "wgrad_plan"):
+        pytest.skip("rocfm._rocfm_hip not built")
+    os.environ.pop("ROCFM_WGRAD_TW", None)
+    emb = lambda F, B=1024: -(-B * F // H.tail_chunk())  # noqa: E731 — embedding workgroups
+    n, tw = H.wgrad_plan([416, 128, 64, 32], 1024, emb(39), 256)  # 39·10 → 128-64-32 (padded to 32)
+    assert tw == [1, 1, 1] and n + emb(39) <= 256
+    # (the widest tiles are 32 × 128; a few bias / output workgroups may spill past the round)
+    n, tw = H.wgrad_plan([1248, 256, 128, 64], 1024, emb(39), 256)
+    assert n + emb(39) <= 256 + 8 and tw == [4, 4, 2], (n, tw)
+    n, tw = H.wgrad_plan([1248, 128, 64, 32], 1024, emb(39), 256)
+    assert n + emb(39) <= 256 and tw[0] >= 2, (n, tw)
+    n0, tw = H.wgrad_plan([1248, 256, 128, 64], 1024, -1, 256)  # standalone launch: plain tiles
+    assert tw == [1, 1, 1] and n0 == 39 * 8 + 8 * 4 + 4 * 2 + (256 + 128 + 64) // 32 + 1

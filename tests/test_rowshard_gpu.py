@@ -436,3 +436,59 @@ def test_dp_owner_shadow_exchange(tmp_path, fault):
         assert got["shadow"] == "ok" and got["exchange"] == "p2p", got["shadow"]
     ref = _single("sparse", steps, B=128, opt="Momentum")
     _assert_params_tight(got["P"], ref.parameters_tf())
+
+
+def _owner_restore_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), ROCFM_SPIN_LIMIT=str(1 << 26), ROCFM_SHADOW_STEPS="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from rocfm.models.deepfm import init_params
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    spec, hp = _cfg("Momentum")
+    B, n1, n2 = 64, 6, 5
+    batches = _batches(world * B, n1 + n2, 11)
+    pool = [torch.stack([b[i][rank * B:(rank + 1) * B] for b in batches]).cuda() for i in range(3)]
+
+    def make(seed):
+        return FusedRowShard(spec, hp, B, torch.device("cuda", 0), params=init_params(spec, seed), use_graph=True,
+                             exchange="p2p", replicate_table=True)
+
+    a = make(3)
+    a.attach_pool(*pool)
+    a.train_steps(n1, 4)
+    torch.cuda.synchronize()
+    sd = {k: v.clone() for k, v in a.state_dict().items()}
+    b = make(99)  # other initial weights: everything must come from the checkpoint
+    b.load_state_dict(sd)
+    b.attach_pool(*pool)
+    torch.cuda.synchronize()
+    # the restored replica is the gathered owners' shards, on every rank (a stale replica would pass
+    # verify_replicas — every rank equally stale — and silently feed the forward old rows)
+    Pb = b.parameters_tf()
+    full = b.emb_full.cpu()
+    restored = (torch.equal(full[:, :spec.embedding_size], Pb["fm_v"]) and
+                torch.equal(full[:, spec.embedding_size], Pb["fm_w"]) and torch.equal(full, a.emb_full.cpu()))
+    for e in (a, b):
+        e.train_steps(n2, 4)
+        torch.cuda.synchronize()
+        e.check()
+    Pa, Pb = a.parameters_tf(), b.parameters_tf()
+    same = all(torch.equal(Pa[k], Pb[k]) for k in Pa) and torch.equal(a.emb_full, b.emb_full)
+    if rank == 0:
+        torch.save({"restored": restored, "same": same, "step": b.global_step()}, out_path)
+    a.close()
+    b.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_owner_checkpoint_restore_2ranks(tmp_path):
+    """dp_owner restore: load_state_dict rebuilds every rank's full replica from the
+    owners' shards (_sync_full); training on from the restored engine equals the uninterrupted run,
+    bitwise."""
+    out = str(tmp_path / "own.pt")
+    mp.start_processes(_owner_restore_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    assert got["restored"] and got["same"] and got["step"] == 11, got

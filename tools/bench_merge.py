@@ -8,6 +8,13 @@ ranks), the map mode (scatter into W×V position maps, then apply) and the range
 (mode 1) so repeated launches leave the inputs unchanged.
 
     python tools/bench_merge.py [--V 1000000] [--B 1024] [--iters 200] [--worlds 1,2,4,8] [--sdir_buckets N]
+                                [--memory cached,uncached] [--cap N]
+
+``--memory uncached`` places the gathered lists (keys, counts, rows, directories) in a
+hipDeviceMallocUncached buffer — the memory type of the engine's p2p receive slots (p2p.py), which
+the merge reads on the node — instead of cached torch tensors.  ``--cap N`` sizes the lists' slots
+at N rows (the production default is batch_size · field_size) to show whether a merge's cost
+follows the slot capacity or the live row counts.
 
 It also times the owner-sharded DP merge (parallelism=dp_owner, owner_merge below).
 """
@@ -40,6 +47,9 @@ def main():
     ap.add_argument("--hash", action="store_true")
     ap.add_argument("--sdir_buckets", type=int, default=0, help="search+dir bucket count (0: dp's default)")
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--memory", default="cached", help="cached and/or uncached (the p2p receive slots' type)")
+    ap.add_argument("--cap", type=int, default=0, help="slot capacity in rows (0: the largest list)")
+    ap.add_argument("--skip_owner", action="store_true")
     a = ap.parse_args()
     H = require_hip()
     dev = torch.device("cuda")
@@ -54,7 +64,7 @@ def main():
             lists = [(x * 0x9E3779B1) & ((1 << bits) - 1) for x in lists]
         lists = [torch.unique(x) for x in lists]
         Vk = (1 << bits) if a.hash else a.V
-        cap = (max(len(x) for x in lists) + 3) // 4 * 4
+        cap = (max(max(len(x) for x in lists), a.cap) + 3) // 4 * 4
         keys = torch.full((W, cap), 0xFFFFFFFF, dtype=torch.int64)
         for r, x in enumerate(lists):
             keys[r, : len(x)] = x.cpu()
@@ -89,38 +99,50 @@ def main():
         sdiv = (Vk + snb - 1) // snb
         sb = torch.arange(snb + 1, dtype=torch.int64) * sdiv
         sdirs = torch.stack([torch.searchsorted(x.cpu(), sb).to(torch.int32) for x in lists]).to(dev)
-        dir_of = {"range": (dirs.data_ptr(), nb + 1, nb, div), "search+dir": (sdirs.data_ptr(), snb + 1, snb, sdiv)}
         s = torch.cuda.current_stream().cuda_stream
-        res = {}
         names = ("search", "search+dir", "maps", "range")
-        for name in names:
-            p.dirs, p.dir_stride, p.nb, p.bucket_div = dir_of.get(name, (0, 0, 0, 1))
-
-            def run():
-                if name in ("search", "search+dir"):
-                    H.merge_search_apply(p, None, s)
-                elif name == "range":
-                    H.merge_range_apply(p, None, s)
-                else:
-                    H.merge_scatter(p, s)
-                    H.merge_apply(p, s)
-            for _ in range(10):
-                run()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                run()
-            e1.record()
+        for mem in a.memory.split(","):
+            src = (keys32, counts, rows, dirs, sdirs)
+            raw = None
+            if mem == "uncached":  # one uncached allocation holding every list, like a receive buffer
+                sizes = [t.numel() for t in src]
+                raw = H.p2p_malloc(4 * (sum(sizes) + 64), 0)
+                views, off = [], 0
+                for t, n in zip(src, sizes):
+                    v = _uncached_view(raw + 4 * off, t.shape, t.dtype, dev)
+                    v.copy_(t)
+                    views.append(v)
+                    off += (n + 3) // 4 * 4
+                src = tuple(views)
+            k_, c_, r_, d_, sd_ = src
+            p.keys, p.rows, p.counts = k_.data_ptr(), r_.data_ptr(), c_.data_ptr()
+            dir_of = {"range": (d_.data_ptr(), nb + 1, nb, div), "search+dir": (sd_.data_ptr(), snb + 1, snb, sdiv)}
+            _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, sum(len(x) for x in lists))
             torch.cuda.synchronize()
-            res[name] = e0.elapsed_time(e1) * 1000 / a.iters
-        print(f"W={W} cap={cap} entries={W * cap} buckets={nb}: search {res['search']:.2f} us, "
-              f"search+dir ({snb} buckets) {res['search+dir']:.2f} us, "
-              f"maps {res['maps']:.2f} us, range {res['range']:.2f} us", flush=True)
-        # the merges write the same dense gradient rows
-        outs = []
-        for name in names:
-            p.dirs, p.dir_stride, p.nb, p.bucket_div = dir_of.get(name, (0, 0, 0, 1))
-            dg.zero_()
+            if raw is not None:
+                del src, k_, c_, r_, d_, sd_
+                H.p2p_free(raw)
+        if not a.hash and not a.skip_owner:  # (hashed keys exceed the owner table's rows)
+            owner_merge(H, a, W, lists, dev)
+
+
+def _uncached_view(ptr, shape, dtype, dev):
+    class _Raw:
+        pass
+
+    raw = _Raw()
+    n = int(np.prod(shape))
+    raw.__cuda_array_interface__ = {"shape": (n,), "typestr": {torch.float32: "<f4", torch.int32: "<i4"}[dtype],
+                                    "data": (ptr, False), "version": 3, "strides": None}
+    return torch.as_tensor(raw, device=dev).view(*shape)
+
+
+def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live):
+    res = {}
+    for name in names:
+        p.dirs, p.dir_stride, p.nb, p.bucket_div = dir_of.get(name, (0, 0, 0, 1))
+
+        def run():
             if name in ("search", "search+dir"):
                 H.merge_search_apply(p, None, s)
             elif name == "range":
@@ -128,11 +150,33 @@ def main():
             else:
                 H.merge_scatter(p, s)
                 H.merge_apply(p, s)
-            torch.cuda.synchronize()
-            outs.append(dg.clone())
-        assert all(torch.equal(outs[0], o) for o in outs[1:]), W
-        if not a.hash:  # (hashed keys exceed the owner table's rows)
-            owner_merge(H, a, W, lists, dev)
+        for _ in range(10):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = e0.elapsed_time(e1) * 1000 / a.iters
+    print(f"W={W} {mem} cap={cap} live rows={live} buckets={nb}: search {res['search']:.2f} us, "
+          f"search+dir ({snb} buckets) {res['search+dir']:.2f} us, "
+          f"maps {res['maps']:.2f} us, range {res['range']:.2f} us", flush=True)
+    # the merges write the same dense gradient rows
+    outs = []
+    for name in names:
+        p.dirs, p.dir_stride, p.nb, p.bucket_div = dir_of.get(name, (0, 0, 0, 1))
+        dg.zero_()
+        if name in ("search", "search+dir"):
+            H.merge_search_apply(p, None, s)
+        elif name == "range":
+            H.merge_range_apply(p, None, s)
+        else:
+            H.merge_scatter(p, s)
+            H.merge_apply(p, s)
+        torch.cuda.synchronize()
+        outs.append(dg.clone())
+    assert all(torch.equal(outs[0], o) for o in outs[1:]), W
 
 
 def owner_merge(H, a, W, lists, dev):
