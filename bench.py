@@ -289,7 +289,11 @@ def main():
         "replicas_consistent": replicas_ok,
         "shadow_exchange": (shadow.status if shadow is not None else None),
     }
+    wd = None
+    if world > 1 and a.engine == "fused" and not a.no_secondary:
+        wd = _Watchdog(out, rank, a.json_out)  # bounds everything after the headline
     if (world > 1 and a.engine == "fused" and hasattr(eng, "phase_windows") and not a.no_secondary):
+        wd.window = "phase_ms"
         try:  # per-rank device phase times of the headline's DP step (diagnostic windows, after it)
             out["phase_ms"] = eng.phase_windows(64, a.steps_per_graph)
         except Exception as e:  # noqa: BLE001 — a diagnostic never costs the headline
@@ -303,8 +307,10 @@ def main():
         out.update(secondary_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels)))
     elif world > 1 and a.engine == "fused" and a.parallelism == "auto" and not a.no_secondary:
         del eng, run
-        out.update(multi_gpu_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels), world, rank,
-                                     backend, out))
+        multi_gpu_windows(a, spec, hp, params, dev, (pool_ids, pool_vals, pool_labels), world, rank, backend, out,
+                          wd)
+    if wd is not None:
+        wd.cancel()
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -340,46 +346,54 @@ def _rank_span(dt, dev, backend):
     return float(t[0].item()), -float(t[1].item())
 
 
-def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, headline):
+class _Watchdog:
+    """N > 1: bounds the work after the headline (phase windows, secondary windows) — on expiry
+    (ROCFM_BENCH_SECONDARY_S, default 300 s) rank 0 prints the JSON gathered so far with the name
+    of the window that overran, and every rank exits, so a hung secondary never loses the headline."""
+
+    def __init__(self, out, rank, json_out):
+        import threading
+
+        self.out, self.rank, self.json_out, self.window, self.done = out, rank, json_out, None, False
+        self.budget = float(os.environ.get("ROCFM_BENCH_SECONDARY_S", "300"))
+        self.t = threading.Timer(self.budget, self._expire)
+        self.t.daemon = True
+        self.t.start()
+
+    def _expire(self):
+        if self.done:
+            return
+        if self.rank == 0:
+            h = dict(self.out)
+            h["secondary_error"] = f"watchdog: window {self.window} overran {self.budget:.0f} s"
+            print(json.dumps(h), flush=True)
+            if self.json_out:
+                with open(self.json_out, "w") as f:
+                    f.write(json.dumps(h) + "\n")
+        os._exit(0)
+
+    def cancel(self):
+        self.done = True
+        self.t.cancel()
+
+
+def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out, wd):
     """N > 1: secondary windows beside the headline (DP over the p2p push), each on a fresh engine
-    and fenced — a window that fails or overruns becomes an error string, never a lost headline:
+    and fenced — a window that fails becomes an error string in ``out``, one that overruns trips
+    the watchdog; either way the headline is printed:
 
     * ``rccl``: the same DP step with the exchange on RCCL (all-gather captured in the graphs), the
       transport A/B of the node;
     * ``rowshard``: config 4 — the PS-equivalent row-sharded table at 100M rows
       (``…multiInstance.py:461-521``), p2p all-to-alls.
-    Every window reports its own replica check and p2p shadow status.  A watchdog bounds the
-    windows (ROCFM_BENCH_SECONDARY_S, default 300 s): on expiry rank 0 prints the headline with
-    the error and every rank exits."""
-    import threading
-
+    Every window reports its own replica check and p2p shadow status."""
     import torch
 
-    budget = float(os.environ.get("ROCFM_BENCH_SECONDARY_S", "300"))
-    state = {"window": None, "done": False}
-    out = {}
-
-    def expire():
-        if state["done"]:
-            return
-        if rank == 0:
-            h = dict(headline)
-            h.update(out)
-            h["secondary_error"] = f"watchdog: window {state['window']} overran {budget:.0f} s"
-            print(json.dumps(h), flush=True)
-            if a.json_out:
-                with open(a.json_out, "w") as f:
-                    f.write(json.dumps(h) + "\n")
-        os._exit(0)
-
-    wd = threading.Timer(budget, expire)
-    wd.daemon = True
-    wd.start()
     S = a.steps_per_graph
     B = a.batch_size
 
     def run_window(name, build):
-        state["window"] = name
+        wd.window = name
         err = None
         res = {}
         eng = None
@@ -444,9 +458,6 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, head
     run_window("rowshard", lambda: FusedRowShard(spec4, hp, B, dev, params=None, seed=a.seed, capacity=cap4,
                                                  compute_dtype=a.compute_dtype))
     out["rowshard_feature_size"] = V4
-    state["done"] = True
-    wd.cancel()
-    return out
 
 
 def secondary_windows(a, spec, hp, params, dev, pool):

@@ -1,5 +1,5 @@
-# Round 4: device-side Example parsing + record index + N>1 bench windows — full GPU suite, smoke,
-# TFRecord-fed bench windows, loader aggregate over 1..8 processes (record sharding, index)
+# Round 4 (a): device-side Example parsing, TFRecord-fed bench windows, headline + secondaries,
+# merge on uncached memory, k=32 shapes (dedup x wide wgrad tiles A/B)
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4a
@@ -10,12 +10,9 @@ timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --lo
 timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --loader_threads 8 > $O/tf_t8.log 2>&1
 timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 32 --loader_threads 16 --host_decode > $O/tf_host16.log 2>&1
 timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/b20.log 2>&1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputests.log 2>&1
-timeout -k 10 600 python tools/loader_aggregate.py --procs 1,2,4,8 --threads 2 --records 800000 --modes raw,tfrecord --shard_policy record --json $O/loader_agg.json > $O/loader_agg.log 2>&1
 timeout -k 10 300 python tools/bench_merge.py --worlds 2,4,8 --memory cached,uncached --skip_owner --iters 100 > $O/merge_mem.log 2>&1
 timeout -k 10 300 python tools/bench_merge.py --worlds 8 --memory cached,uncached --cap 39936 --skip_owner --iters 100 > $O/merge_cap.log 2>&1
 for D in 0 1; do for L in 128,64,32 256,128,64; do for T in auto 1; do
 if [ $T = auto ]; then unset ROCFM_WGRAD_TW; else export ROCFM_WGRAD_TW=$T; fi
 ROCFM_DEDUP=$D timeout -k 10 200 python bench.py --steps 200 --warmup 20 --embedding_size 32 --deep_layers $L --feature_size 117581 --no_secondary > $O/k32_${L//,/-}_dedup${D}_tw$T.log 2>&1
 done; done; done
-unset ROCFM_WGRAD_TW

@@ -1,0 +1,8 @@
+# Round 4 (b): the full GPU suite, then the loader aggregate over 1..8 processes (record sharding
+# through the record index; raw payloads vs host parse)
+set -e
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4b
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputests.log 2>&1
+timeout -k 10 600 python tools/loader_aggregate.py --procs 1,2,4,8 --threads 2 --records 800000 --modes raw,tfrecord --shard_policy record --json $O/loader_agg.json > $O/loader_agg.log 2>&1

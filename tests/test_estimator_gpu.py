@@ -123,3 +123,69 @@ def test_hbm_epoch_cache_equals_streaming(data_dir, tmp_path):
     assert [r["global_step"] for r in logs if r.get("event") == "train"][-1] == 48
     for e in (a, b):
         e.close()
+
+
+def test_device_decode_equals_host_decode(data_dir, tmp_path):
+    """device_decode (default): the loader hands the graphs' copy stream undecoded Example payloads
+    and the GPU parses them (csrc/kernels/decode.hip) — bit-identical training to host parsing."""
+    from rocfm.estimator import Estimator
+
+    tr = [os.path.join(data_dir, "tr.tfrecords")]
+    a = Estimator(_cfg(data_dir, "", device_decode="true", hbm_cache="false"))
+    b = Estimator(_cfg(data_dir, "", device_decode="false", hbm_cache="false"))
+    assert a.train(tr, num_epochs=2)["steps"] == b.train(tr, num_epochs=2)["steps"] == 32
+    sa, sb = a.eng.state_dict(), b.eng.state_dict()
+    assert not [k for k in sa if not torch.equal(sa[k], sb[k])]
+    for e in (a, b):
+        e.close()
+
+
+def _two_rank_cache_worker(rank, world, port, data_dir, out_path):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), ROCFM_SHADOW_STEPS="3")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from rocfm.estimator import Estimator
+
+    tr = [os.path.join(data_dir, "tr2.tfrecords")]
+    res = {}
+    for cache in ("true", "false"):
+        est = Estimator(_cfg(data_dir, "", hbm_cache=cache, parallelism="dp", batch_size=512),
+                        device=torch.device("cuda", 0))  # (both ranks share the box's one GPU)
+        out = est.train(tr, num_epochs=3)
+        torch.cuda.synchronize()
+        sd = est.eng.state_dict()
+        res[cache] = (out["steps"], {k: v.cpu() for k, v in sd.items()}, est.eng.shadow.status)
+        est.close()
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_hbm_epoch_cache_equals_streaming(tmp_path):
+    """World 2 (ranks sharing the GPU, p2p DP, device-side parsing, a 3-step shadow window): the
+    ranks agree on a per-epoch batch count (rank 0's shard holds one batch more, dropped every
+    epoch), epoch 1 streams into each rank's HBM cache and epochs 2-3 replay it — bit-identical to
+    streaming all three epochs from the loader."""
+    import torch.multiprocessing as mp
+
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+
+    d = tmp_path / "data2"
+    d.mkdir()
+    write_synthetic_tfrecord(str(d / "tr2.tfrecords"), 9215, 5000, seed=5)  # shards 4608 / 4607 → 9 / 8 batches
+    out = str(tmp_path / "cache2.pt")
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_two_rank_cache_worker, args=(2, port, str(d), out), nprocs=2, join=True, start_method="spawn")
+    r = torch.load(out, weights_only=True)
+    (na, sa, sha), (nb, sb, shb) = r["true"], r["false"]
+    assert na == nb == 3 * 8 and sha == shb == "ok", (na, nb, sha, shb)
+    assert not [k for k in sa if not torch.equal(sa[k], sb[k])]
