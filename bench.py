@@ -458,6 +458,88 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
     run_window("rowshard", lambda: FusedRowShard(spec4, hp, B, dev, params=None, seed=a.seed, capacity=cap4,
                                                  compute_dtype=a.compute_dtype))
     out["rowshard_feature_size"] = V4
+    del pool, p4
+    torch.cuda.empty_cache()
+    tfrecord_window(a, spec, hp, params, dev, world, rank, backend, out, wd)
+
+
+def tfrecord_window(a, spec, hp, params, dev, world, rank, backend, out, wd):
+    """N > 1, TFRecord-fed DP under the reference's default record sharding
+    (``dataset.shard(hvd.size(), hvd.rank())``, HVD:132-133): every rank writes one synthetic
+    Criteo-shape file (with its record index) in parallel, then reads every P-th record of the
+    concatenated file list — only its own records, through the index — as undecoded payloads that
+    its GPU parses (raw loader mode + decode.hip), streamed through the DP multi-step graphs with the
+    exchange inline.  The files hold 256 batches per rank; the window repeats them as epochs."""
+    import shutil
+    import tempfile
+
+    import torch
+    import torch.distributed as dist
+
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.data.tfrecord import TFRecordDataset
+    from rocfm.parallel.dp import FusedDataParallel
+
+    wd.window = "tfrecord"
+    B, F, S = a.batch_size, spec.field_size, 16
+    nb = 256  # batches per rank per epoch
+    steps, warm = max(1024, a.steps), 64
+    obj = [tempfile.mkdtemp(prefix="rocfm_bench_mtf_") if rank == 0 else None]
+    _ctrl_barrier()
+    dist.broadcast_object_list(obj, src=0, group=_CTRL[0] if _CTRL and _CTRL[0] is not None else None)
+    d = obj[0]
+    err, res, eng = None, {}, None
+    try:
+        t0 = time.perf_counter()
+        write_synthetic_tfrecord(os.path.join(d, f"tr{rank}.tfrecords"), nb * B, spec.feature_size, F,
+                                 seed=a.seed + 17 * rank)
+        gen_s = time.perf_counter() - t0
+        _ctrl_barrier()
+        files = [os.path.join(d, f"tr{r}.tfrecords") for r in range(world)]
+
+        def groups(skip, limit):
+            ds = TFRecordDataset(files, F, B, spec.feature_size, num_epochs=-(-(skip + limit) // nb) + 1,
+                                 shard_count=world, shard_index=rank, num_threads=4, hold=2)
+            return ds.raw_groups(S, hold=2, skip=skip, limit=limit)
+
+        eng = FusedDataParallel(spec, hp, B, dev, params=params, mode="dp", seed=a.seed,
+                                compute_dtype=a.compute_dtype)
+        eng.set_lr_scale(float(world))
+        eng.train_stream(groups(0, warm), S, hold=2)  # shadow window + graph captures
+        torch.cuda.synchronize()
+        _ctrl_barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        done = eng.train_stream(groups(warm, steps), S, hold=2)
+        torch.cuda.synchronize()
+        _ctrl_barrier()
+        dt = time.perf_counter() - t0
+        dmax, dmin = _rank_span(dt, dev, backend)
+        eng.check(replicas=False)
+        if done != steps:
+            raise RuntimeError(f"trained {done} steps, expected {steps}")
+        res = {"examples_per_sec": round(B * world * steps / dmax, 1), "ms_per_step": round(dmax / steps * 1e3, 4),
+               "rank_ms_per_step_min": round(dmin / steps * 1e3, 4), "steps": steps,
+               "replicas_consistent": bool(eng.verify_replicas()), "shadow_exchange": eng.shadow.status,
+               "exchange": eng.exchange, "shard": "record (Dataset.shard(P, rank), record index)",
+               "decode": "device", "data_gen_s": round(gen_s, 2)}
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        if eng is not None:
+            try:
+                eng.close()
+            except Exception:  # noqa: BLE001
+                pass
+        del eng
+        torch.cuda.empty_cache()
+    _ctrl_barrier()
+    if rank == 0:
+        shutil.rmtree(d, ignore_errors=True)
+    if err is not None:
+        out["tfrecord_error"] = err
+    for k, v in res.items():
+        out[f"tfrecord_{k}"] = v
 
 
 def secondary_windows(a, spec, hp, params, dev, pool):
@@ -526,7 +608,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
     import copy
 
     ta = copy.copy(a)
-    ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(32, a.warmup), 16
+    # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
+    ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(64, a.warmup), 16
     try:
         t = measure_tfrecord(ta, spec, hp, params, dev)
         out["tfrecord_steps"] = ta.steps

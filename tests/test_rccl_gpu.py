@@ -125,6 +125,10 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
         assert j[f"{w}_examples_per_sec"] > 0 and j[f"{w}_replicas_consistent"] is True, (w, j)
     assert j["rowshard_exchange"] == "p2p" and j["rowshard_shadow_exchange"] == "ok", j
     assert j["rowshard_feature_size"] == 100_000_000, j
+    # TFRecord-fed DP under the reference's record sharding (each rank reads its records through
+    # the record index; the GPU parses the payloads)
+    assert j["tfrecord_examples_per_sec"] > 0 and j["tfrecord_replicas_consistent"] is True, j
+    assert j["tfrecord_shadow_exchange"] == "ok" and j["tfrecord_decode"] == "device", j
 
 
 def test_bench_rehearsal_2_ranks_fused_push():
