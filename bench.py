@@ -710,11 +710,18 @@ def measure_tfrecord(a, spec, hp, params, dev):
         ev.record()
         marks.append((time.perf_counter(), ev, first + n))
 
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    done = eng.train_stream(timed(groups(a.warmup, a.steps)), S, hold=H, after_steps=after)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    import gc
+
+    gc.collect()
+    gc.disable()  # a collector pass over the process's objects must not stall the launch loop
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        done = eng.train_stream(timed(groups(a.warmup, a.steps)), S, hold=H, after_steps=after)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        gc.enable()
     eng.check()
     if done != a.steps:
         raise RuntimeError(f"trained {done} steps, expected {a.steps}")

@@ -10,6 +10,7 @@
 #include "wgrad_body.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace rocfm {
 
@@ -70,7 +71,9 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
                 "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
   const int n_emb = e.n > 0 ? cdiv(e.n, tail_chunk_entries()) : 0;
-  const int n_wg = wgrad_prepare(w, n_emb, tail_cus());  // both roles in one dispatch round
+  const char* tw = std::getenv("ROCFM_WGRAD_TW");  // auto: widen to one dispatch round; 2|4: forced
+  const bool widen = tw && *tw && std::strcmp(tw, "1") != 0;
+  const int n_wg = wgrad_prepare(w, widen ? n_emb : -1, tail_cus());
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
   const bool push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);

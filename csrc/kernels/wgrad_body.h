@@ -344,9 +344,11 @@ __device__ __forceinline__ void dense_apply_body(const DenseApplyParams& p, cons
 
 
 // Fills the per-layer tile / bias workgroup offsets; returns the grid size.
-// ``co_resident`` (step tail): workgroups of the launch's other role; the tile widths are widened
-// (WgradParams::tw, largest layers first, up to 4 subtiles) until tiles + bias blocks + 1 + the
-// other role fit ``max_wg`` (one dispatch round).  0: plain 32×32 tiles (standalone mlp_wgrad).
+// ``co_resident`` ≥ 0 (step tail, ROCFM_WGRAD_TW=auto): workgroups of the launch's other role; the
+// tile widths are widened (WgradParams::tw, largest layers first, up to 4 subtiles) until tiles +
+// bias blocks + 1 + the other role fit ``max_wg`` (one dispatch round).  Measured no faster at the
+// reference's k = 32 shapes (profiles/r4_k32_tail_ab.md), so the step tail keeps 32×32 tiles
+// unless asked; ROCFM_WGRAD_TW=2|4 forces a width.  < 0: plain 32×32 tiles.
 inline int wgrad_prepare(WgradParams& p, int co_resident = -1, int max_wg = 256) {
   ROCFM_REQUIRE(p.Bp % 128 == 0, "mlp_wgrad: Bp must be a multiple of 128");
   for (int l = 0; l < kMaxHidden; ++l) p.tw[l] = 1;

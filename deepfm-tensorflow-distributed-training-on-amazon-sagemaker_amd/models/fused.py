@@ -998,7 +998,7 @@ class FusedDeepFM:
             self._precapture_multi(self._m_graphs, ("m",), n, self._multi_body)
 
     def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
-                     ring_batches: int = 0, build=None, run=None) -> int:
+                     ring_batches: int = 0, build=None, run=None, prefix=None) -> int:
         """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
 
         Batches are copied host → HBM on a copy stream into a device ring of 4·S batch slots, two
@@ -1021,9 +1021,14 @@ class FusedDeepFM:
         ``build(S)`` / ``run(n)`` (the distributed wrappers, rocfm.parallel): (re)build the
         multi-step structures for the attached ring, and launch one n-step graph with the step's
         exchange inline; default: this engine's single-GPU graphs.
+        ``prefix`` = device batches ``(ids [n,B,F], vals, labels)`` ALREADY trained just before this
+        call (the distributed wrappers' shadow-validation steps): they take ring slots 0..n-1 so
+        that the ring holds the stream's batches in order from its first one (``ring_batches``
+        counts them too).
         """
         S = self._multi_S(int(steps_per_graph))[1]
-        R = max(4 * S, (int(ring_batches) + S - 1) // S * S)
+        npre = 0 if prefix is None else int(prefix[0].shape[0])
+        R = max(4 * S + npre, (int(ring_batches) + S - 1) // S * S)
         hold = max(1, int(hold))
         dev = self.device
         ring = getattr(self, "_stream_ring", None)
@@ -1033,13 +1038,16 @@ class FusedDeepFM:
                     torch.zeros(R, self.B, dtype=torch.float32, device=dev))
             self._stream_ring = ring
         i0 = self._i
-        # pool batch index of global step i = (start + i) % R  with start ≡ −i0 (mod R) → slot i − i0
-        self.attach_pool(*ring, start=(R - i0 % R) % R)
+        # pool batch index of global step i = (start + i) % R  with start ≡ −(i0 − npre) (mod R) →
+        # slot i − i0 + npre: the prefix (steps i0 − npre .. i0 − 1) in slots 0 .. npre − 1
+        self.attach_pool(*ring, start=(R - (i0 - npre) % R) % R)
+        if npre:
+            for k in range(3):
+                ring[k][:npre].copy_(prefix[k])
         self._ring_mode_stream = True
         copy = getattr(self, "_copy_stream", None) or torch.cuda.Stream(device=dev)
         self._copy_stream = copy
         it = iter(batches)
-        staged = 0  # batches copied into the ring so far
 
         def mark(stream):
             e = torch.cuda.Event()
@@ -1048,6 +1056,7 @@ class FusedDeepFM:
 
         pending = []  # (event, host batch) kept alive until its copy has completed
         carry = [None]  # the part of a group that did not fit the previous graph (same host memory)
+        staged = npre  # ring slots filled so far (the prefix first)
 
         def stage(k):  # copy up to k more batches; returns how many were available
             nonlocal staged
@@ -1104,6 +1113,7 @@ class FusedDeepFM:
         avail = stage(2 * S)
         if avail == 0:
             return 0
+        staged_new = lambda: staged - npre  # noqa: E731 — batches of this call's stream
         cevs = [mark(copy)]  # cevs[j]: copies read by graph j's side chain (graph j+1's batches)
         main.wait_event(cevs[0])
         if build is not None:
@@ -1115,8 +1125,8 @@ class FusedDeepFM:
         prime_ev = mark(main)
         sevs = []  # sevs[j]: end of graph j's side chain (side graph, sort stream)
         done, j = 0, 0
-        while done < staged:
-            n = min(S, staged - done)
+        while done < staged_new():
+            n = min(S, staged_new() - done)
             # stage graph j+2's batches; their ring slots held graph j-2's batches, last read by
             # graph j-3's side chain (or by the prime)
             copy.wait_event(sevs[j - 3] if j >= 3 else prime_ev)

@@ -222,11 +222,14 @@ def attach_torch_dp(eng, embedding_update: str = "sparse") -> None:
         eng.exchange_rows = exchange_rows
 
 
-def shadow_prefix(w, batches, after_steps=None):
+def shadow_prefix(w, batches, after_steps=None, with_prefix: bool = False):
     """Train the shadow-validation window of a distributed fused engine ``w`` (its first p2p steps,
     per step with the collective shadow) from the head of a host batch stream.  Returns (the rest
-    of the stream, steps trained).  Items are single batches or stacked groups, as in
-    FusedDeepFM.train_stream; a group that straddles the window's end is split."""
+    of the stream, steps trained) — and, ``with_prefix``, the trained batches as device tensors
+    ``(ids [n,B,F], vals, labels)`` or None, which ``FusedDeepFM.train_stream(prefix=…)`` puts at
+    the head of its HBM ring (so the ring of an epoch holds the whole epoch: the HBM epoch cache).
+    Items are single batches, stacked groups or RawGroups, as in FusedDeepFM.train_stream; a group
+    that straddles the window's end is split."""
     import itertools
 
     from ..data.tfrecord import RawGroup
@@ -234,7 +237,7 @@ def shadow_prefix(w, batches, after_steps=None):
 
     shadow = getattr(w, "shadow", None)
     if shadow is None or not shadow.active:
-        return batches, 0
+        return (batches, 0, None) if with_prefix else (batches, 0)
     it = iter(batches)
     dev = w.eng.device
     got, rest = [], []
@@ -262,15 +265,17 @@ def shadow_prefix(w, batches, after_steps=None):
         if k < ids.shape[0]:  # the rest of this group is trained by the stream (own host copy)
             rest.append((ids[k:].clone(), vals[k:].clone(), labels[k:].clone()))
     if not got:
-        return itertools.chain(rest, it), 0
+        return (itertools.chain(rest, it), 0, None) if with_prefix else (itertools.chain(rest, it), 0)
     e = w.eng
     i0 = e._i
-    w.attach_pool(torch.stack([g[0] for g in got]), torch.stack([g[1] for g in got]),
-                  torch.stack([g[2] for g in got]), start=(-i0) % len(got))
+    pre = (torch.stack([g[0] for g in got]), torch.stack([g[1] for g in got]), torch.stack([g[2] for g in got]))
+    w.attach_pool(*pre, start=(-i0) % len(got))
     for _ in got:
         w.train_step()
     if after_steps is not None:
         after_steps(i0, len(got))
+    if with_prefix:
+        return itertools.chain(rest, it), len(got), pre
     return itertools.chain(rest, it), len(got)
 
 
@@ -830,9 +835,9 @@ class FusedDataParallel:
         steps) trains per step first.  Every rank must stream the same number of batches."""
         if not (self.graph_collectives and self.use_graph):
             raise RuntimeError("train_stream needs capturable exchanges (p2p, or RCCL with graphs)")
-        batches, done = shadow_prefix(self, batches, after_steps)
+        batches, done, pre = shadow_prefix(self, batches, after_steps, with_prefix=True)
         n = self.eng.train_stream(batches, steps_per_graph, after_steps, hold, ring_batches,
-                                  build=self._stream_build, run=self._stream_run)
+                                  build=self._stream_build, run=self._stream_run, prefix=pre)
         return done + n
 
     def close(self) -> None:

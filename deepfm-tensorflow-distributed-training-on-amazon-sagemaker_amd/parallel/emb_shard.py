@@ -1424,18 +1424,27 @@ class FusedRowShard:
             raise RuntimeError("train_stream needs capturable exchanges (p2p, or RCCL with graphs)")
         from .dp import shadow_prefix
 
-        batches, done = shadow_prefix(self, batches, after_steps)
+        batches, done, pre = shadow_prefix(self, batches, after_steps, with_prefix=True)
         if self.NH and self.hot_ids is None:  # replicated ids from the stream's first group
             first = next(iter(batches), None)
             if first is None:
                 return done
-            ids = first[0] if first[0].dim() == 3 else first[0].unsqueeze(0)
+            from ..data.tfrecord import RawGroup
+
+            if isinstance(first, RawGroup):  # undecoded: parse a copy of its first batches
+                from ..ops.decode import decode_on_device
+
+                k = min(first.n, 8)
+                ids = decode_on_device(first.bytes, first.offs, k, first.B, self.eng.F, self.device,
+                                       self.eng.id_limit)[0]
+            else:
+                ids = first[0] if first[0].dim() == 3 else first[0].unsqueeze(0)
             self._choose_hot(ids[: min(len(ids), 8)].to(self.device))
             import itertools
 
             batches = itertools.chain([first], batches)
         n = self.eng.train_stream(batches, steps_per_graph, after_steps, hold, ring_batches,
-                                  build=self._stream_build, run=self._stream_run)
+                                  build=self._stream_build, run=self._stream_run, prefix=pre)
         self._pre_served = False
         return done + n
 
