@@ -554,6 +554,32 @@ def secondary_windows(a, spec, hp, params, dev, pool):
     from rocfm.models.fused import FusedDeepFM
 
     out = {}
+
+    def tf_window():
+        # the loader-fed window: >= 2048 steps streamed from the TFRecord files (several epochs of a
+        # 512-batch file set), warm-up with the same ring and graph set, so the window holds no
+        # graph rebuild or capture; the time to the first graph is reported separately
+        import copy
+
+        ta = copy.copy(a)
+        # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
+        # (32 steps per graph: the side chain sorts ≥ 1M keys on rocPRIM's onesweep path,
+        # profiles/r4_radix_ab.md)
+        ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(128, a.warmup), 32
+        try:
+            t = measure_tfrecord(ta, spec, hp, params, dev)
+            out["tfrecord_steps"] = ta.steps
+            for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
+                      "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode"):
+                out["tfrecord_" + ("examples_per_sec" if k == "value" else k)] = t.get(k)
+        except Exception as e:  # a secondary window never costs the headline
+            out["tfrecord_error"] = f"{type(e).__name__}: {e}"[:400]
+
+    # the TFRecord window runs first: after the other windows it measured 20 % slower than in a
+    # process of its own (profiles/r4_radix_ab.md); ROCFM_BENCH_TF_FIRST=0 restores the old order
+    tf_first = os.environ.get("ROCFM_BENCH_TF_FIRST", "1") == "1"
+    if tf_first:
+        tf_window()
     eng = FusedDeepFM(spec, hp, a.batch_size, dev, embedding_update="exact", params=params, seed=a.seed,
                       compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
     eng.attach_pool(*pool)
@@ -602,22 +628,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
             out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
         gc.collect()
         torch.cuda.empty_cache()
-    # the loader-fed window: >= 2048 steps streamed from the TFRecord files (several epochs of a
-    # 512-batch file set), warm-up with the same ring and graph set, so the window holds no
-    # graph rebuild or capture; the time to the first graph is reported separately
-    import copy
-
-    ta = copy.copy(a)
-    # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
-    ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(64, a.warmup), 16
-    try:
-        t = measure_tfrecord(ta, spec, hp, params, dev)
-        out["tfrecord_steps"] = ta.steps
-        for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
-                  "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode"):
-            out["tfrecord_" + ("examples_per_sec" if k == "value" else k)] = t.get(k)
-    except Exception as e:  # a secondary window never costs the headline
-        out["tfrecord_error"] = f"{type(e).__name__}: {e}"[:400]
+    if not tf_first:
+        tf_window()
     return out
 
 
@@ -652,7 +664,12 @@ def measure_tfrecord(a, spec, hp, params, dev):
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--input tfrecord measures one GPU (use the Estimator / rocfm.cli for multi-GPU runs)")
-    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 16)
+    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 32)
+    if a.warmup < 4 * S:  # both parities' graphs captured before the window (the first launch is eager)
+        import copy
+
+        a = copy.copy(a)
+        a.warmup = 4 * S
     own = not a.data_dir
     d = a.data_dir or tempfile.mkdtemp(prefix="rocfm_bench_")
     os.makedirs(d, exist_ok=True)

@@ -22,8 +22,8 @@ struct DecodeParams {
   long long max_id;       // ids must be < max_id (0: < 2^31)
   int batch0;             // sequence number of batch 0 (error reports)
   int32_t* err;           // [4] sticky: status (tfrecord.h ParseStatus), batch, record, 0
-  uint8_t key[3][kDecodeKeyMax];  // label, ids, values feature names
-  int klen[3];
+  unsigned long long keyw[3][2];  // label, ids, values feature names: ≤ 16 bytes each, little-endian
+  int klen[3];                     //   words (zero-padded), compared 8 bytes at a time
 };
 
 void launch_decode_examples(const DecodeParams& p, hipStream_t stream);

@@ -68,6 +68,18 @@ template <bool L>
 __device__ __forceinline__ bool varint(const Src<L>& m, int& p, int end, uint64_t& v) {
   const int avail = end - p;
   if (avail <= 0) return false;
+  {  // ≤ 4-byte varints (every tag and length, ids < 2^28): one 32-bit window, 32-bit arithmetic
+    uint32_t x = m.ld32(p);
+    uint32_t t = ~x & 0x80808080u;
+    if (avail < 4) t &= (1u << (8 * avail)) - 1u;
+    if (t) {
+      const int nb = (__builtin_ctz(t) >> 3) + 1;
+      if (nb < 4) x &= (1u << (8 * nb)) - 1u;
+      v = (x & 0x7fu) | ((x >> 1) & (0x7fu << 7)) | ((x >> 2) & (0x7fu << 14)) | ((x >> 3) & (0x7fu << 21));
+      p += nb;
+      return true;
+    }
+  }
   uint64_t x = m.win8(p);
   uint64_t t = ~x & 0x8080808080808080ull;
   if (avail < 8) t &= (1ull << (8 * avail)) - 1;
@@ -186,11 +198,8 @@ __device__ __forceinline__ int int64_list(const Src<L>& m, int p, int end, int32
 template <bool L>
 __device__ __forceinline__ bool key_is(const Src<L>& m, int kp, int kl, const DecodeParams& P, int w) {
   if (kl != P.klen[w]) return false;
-  uint64_t a = 0, b = 0, ka = 0, kb = 0;
-  for (int i = 0; i < 8; ++i) {
-    ka |= (uint64_t)P.key[w][i] << (8 * i);
-    kb |= (uint64_t)P.key[w][8 + i] << (8 * i);
-  }
+  uint64_t a = 0, b = 0;
+  const uint64_t ka = P.keyw[w][0], kb = P.keyw[w][1];
   if (kl > 0) a = m.win8(kp);
   if (kl > 8) b = m.win8(kp + 8);
   const uint64_t ma = kl >= 8 ? ~0ull : ((1ull << (8 * kl)) - 1);

@@ -15,3 +15,7 @@ timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/b20.log 2>&1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 ROCFM_RADIX=onesweep timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_os -o os -- python bench.py --steps 200 --warmup 20 --no_secondary > $O/prof_os.log 2>&1
 timeout -k 10 600 python tools/loader_aggregate.py --procs 1,8 --threads 2 --records 6400000 --modes raw --shard_policy record --json $O/loader_agg.json > $O/loader_agg.log 2>&1
+timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 64 --loader_threads 4 > $O/tf_t4.log 2>&1
+ROCFM_RADIX=onesweep timeout -k 10 300 python bench.py --input tfrecord --steps 2048 --warmup 64 --loader_threads 4 > $O/tf_t4_onesweep.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tf -o tf -- python bench.py --input tfrecord --steps 2048 --warmup 64 --loader_threads 4 > $O/prof_tf.log 2>&1
