@@ -201,27 +201,35 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const int last_end = s_last_end;
   const bool cont = last_end > cend && !(p.max_key && s_hkey[nh - 1] >= p.max_key);
   if (cont) {
+    // every thread sums its own entries of the following chunks (two chunks' loads in flight per
+    // round, no cross-lane work inside the loop), then ONE butterfly per float4 column: the hot
+    // runs (ids present in every example: 1,024-entry runs) cost two load latencies, not a
+    // reduction per 512 entries
     float4 tot[KP4];
 #pragma unroll
     for (int u = 0; u < KP4; ++u) tot[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k0 = cend; k0 < last_end; k0 += kChunk) {
-      const int j = k0 + t;
-      float4 w[KP4];
-      if (j < last_end) {
-        const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)j * p.Kp)
-                                             : contrib_row4(p, p.svals[j] - p.val_base);
+    for (int k0 = cend; k0 < last_end; k0 += 2 * kChunk) {
+      float4 w[2][KP4];
 #pragma unroll
-        for (int u = 0; u < KP4; ++u) w[u] = src[u];
-      } else {
+      for (int h = 0; h < 2; ++h) {
+        const int j = k0 + h * kChunk + t;
+        if (j < last_end) {
+          const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)j * p.Kp)
+                                               : contrib_row4(p, p.svals[j] - p.val_base);
 #pragma unroll
-        for (int u = 0; u < KP4; ++u) w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int u = 0; u < KP4; ++u) w[h][u] = src[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < KP4; ++u) w[h][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
 #pragma unroll
-      for (int u = 0; u < KP4; ++u) {
+      for (int u = 0; u < KP4; ++u) tot[u] = f4add(tot[u], f4add(w[0][u], w[1][u]));
+    }
 #pragma unroll
-        for (int d = 32; d > 0; d >>= 1) w[u] = f4add(w[u], f4shfl_xor(w[u], d));
-        tot[u] = f4add(tot[u], w[u]);
-      }
+    for (int u = 0; u < KP4; ++u) {
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) tot[u] = f4add(tot[u], f4shfl_xor(tot[u], d));
     }
     if (lane == 0) {
 #pragma unroll
