@@ -563,9 +563,7 @@ def secondary_windows(a, spec, hp, params, dev, pool):
 
         ta = copy.copy(a)
         # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
-        # (32 steps per graph: the side chain sorts ≥ 1M keys on rocPRIM's onesweep path,
-        # profiles/r4_radix_ab.md)
-        ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(128, a.warmup), 32
+        ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(64, a.warmup), 16
         try:
             t = measure_tfrecord(ta, spec, hp, params, dev)
             out["tfrecord_steps"] = ta.steps
@@ -664,7 +662,7 @@ def measure_tfrecord(a, spec, hp, params, dev):
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--input tfrecord measures one GPU (use the Estimator / rocfm.cli for multi-GPU runs)")
-    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 32)
+    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 16)
     if a.warmup < 4 * S:  # both parities' graphs captured before the window (the first launch is eager)
         import copy
 

@@ -39,6 +39,11 @@ int tail_chunk_entries();  // sorted entries per embedding workgroup of the fuse
 size_t sort_pairs_temp_bytes(int n, int end_bit);
 void sort_pairs_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_out,
                      int n, int end_bit, hipStream_t stream, uint32_t first_val = 0);
+// seg_sort.hip: stable LSD radix sort of (key, first_val + index) over nseg segments of seg_len
+// keys each, by key bits [0, bits) (every segment sorted on its own; keys keep their other bits)
+size_t seg_sort_temp_bytes(int nseg, int seg_len, int bits);
+void seg_sort_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_out,
+                   int nseg, int seg_len, int bits, hipStream_t stream, uint32_t first_val = 0);
 size_t sort_pairs64_temp_bytes(int n, int end_bit);
 void sort_pairs64_iota(void* temp, size_t temp_bytes, const uint64_t* keys_in, uint64_t* keys_out, uint32_t* vals_out,
                        int n, int end_bit, hipStream_t stream);

@@ -39,6 +39,31 @@ from ..utils import hazard
 from .deepfm import ModelSpec, init_params, mlp_names
 
 
+def sort_lib() -> str:
+    """The (key, index) sort behind every embedding-gradient aggregation: ``rocfm`` (default) — the
+    segmented stable radix sort of csrc/kernels/seg_sort.hip; ``rocprim`` (ROCFM_SORT_LIB=rocprim)
+    — rocPRIM's device radix sort over the composite keys (A/B; profiles/r4_seg_sort.md)."""
+    return "rocprim" if os.environ.get("ROCFM_SORT_LIB", "") == "rocprim" else "rocfm"
+
+
+def iota_sort_temp_bytes(H, n: int, bits: int, nseg: int = 1, seg_bits: int = 0) -> int:
+    """Temporary bytes of ``iota_sort`` over ``nseg`` segments of ``n`` keys."""
+    if sort_lib() == "rocprim":
+        return H.sort_pairs_temp_bytes(nseg * n, bits + seg_bits)
+    return H.seg_sort_temp_bytes(nseg, n, bits)
+
+
+def iota_sort(H, temp, kin: int, kout: int, vout: int, n: int, bits: int, stream: int, nseg: int = 1,
+              seg_bits: int = 0) -> None:
+    """Stable sort of ``nseg`` segments of ``n`` keys each by key bits [0, bits), values = global
+    index.  Segment k's keys must carry k in bits [bits, bits + seg_bits) when nseg > 1 (the
+    composite keys of the multi-step side chain): rocPRIM sorts them as ONE array on those bits."""
+    if sort_lib() == "rocprim":
+        H.sort_pairs_iota(temp.data_ptr(), temp.numel(), kin, kout, vout, nseg * n, bits + seg_bits, stream)
+    else:
+        H.seg_sort_iota(temp.data_ptr(), temp.numel(), kin, kout, vout, nseg, n, bits, stream)
+
+
 def _r32(x: int) -> int:
     return (x + 31) // 32 * 32
 
@@ -234,7 +259,7 @@ class FusedDeepFM:
         self.end_bit = max(1, math.ceil(math.log2(max(self.V, 2))))
         self.skeys = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
         self.svals = [torch.zeros(self.n_lookup, dtype=torch.int32, device=dev) for _ in range(2)]
-        tb = self.H.sort_pairs_temp_bytes(self.n_lookup, self.end_bit)
+        tb = iota_sort_temp_bytes(self.H, self.n_lookup, self.end_bit)
         self.sort_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
         if self.dedup:  # per parity: group index / next member by lookup, compacted keys, count, run ends
             n, nch = self.n_lookup, (self.n_lookup + self.H.tail_chunk() - 1) // self.H.tail_chunk()
@@ -589,9 +614,8 @@ class FusedDeepFM:
             self._set_w8(dp, 1)
 
     def _sort(self, q: int, stream) -> None:
-        self.H.sort_pairs_iota(self.sort_temp.data_ptr(), self.sort_temp.numel(), self.slot_ids[q].data_ptr(),
-                               self.skeys[q].data_ptr(), self.svals[q].data_ptr(), self.n_lookup, self.end_bit,
-                               stream.cuda_stream)
+        iota_sort(self.H, self.sort_temp, self.slot_ids[q].data_ptr(), self.skeys[q].data_ptr(),
+                  self.svals[q].data_ptr(), self.n_lookup, self.end_bit, stream.cuda_stream)
         if self.dedup:
             d = self.H.DedupParams()
             d.skeys, d.svals, d.n, d.S, d.F, d.rt = (self.skeys[q].data_ptr(), self.svals[q].data_ptr(),
@@ -746,7 +770,7 @@ class FusedDeepFM:
         self.m_sk = torch.zeros(2, Smax * n, **i32)
         self.m_sv = torch.zeros(2, Smax * n, **i32)
         if self.m_composite:
-            tb = H.sort_pairs_temp_bytes(Smax * n, self.m_bits)
+            tb = iota_sort_temp_bytes(H, n, idbits, Smax, sbits)
             self.m_keys64 = None
         else:  # 64-bit keys in / out (the sorted ids land in m_sk via sort_aux)
             tb = H.sort_pairs64_temp_bytes(Smax * n, self.m_bits)
@@ -821,9 +845,8 @@ class FusedDeepFM:
         H = self.H
         H.fetch_multi(self._fetch_multi_params(q, advance), stream.cuda_stream)
         if self.m_composite:  # all S batches in one sort
-            H.sort_pairs_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys.data_ptr(),
-                              self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
-                              self.m_bits, stream.cuda_stream)
+            iota_sort(H, self.m_temp, self.m_keys.data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(),
+                      self.n_lookup, self.m_idbits, stream.cuda_stream, nseg=self.mS, seg_bits=self.m_bits - self.m_idbits)
         else:  # one sort of 64-bit composite keys
             H.sort_pairs64_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys64[0].data_ptr(),
                                 self.m_keys64[1].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,

@@ -511,7 +511,9 @@ class FusedRowShard:
         self.overflow = torch.zeros(1, **i32)
         self.bad = torch.zeros(1, **i32)
         self.route_scratch = torch.zeros(H.route_scratch_ints(n), **i32)
-        self.route_temp = torch.zeros(max(H.sort_pairs_temp_bytes(n, self.route_bits), 16), dtype=torch.uint8,
+        from ..models.fused import iota_sort_temp_bytes
+
+        self.route_temp = torch.zeros(max(iota_sort_temp_bytes(H, n, self.route_bits), 16), dtype=torch.uint8,
                                       device=dev)
         # ---- exchange buffers ----
         f32 = dict(dtype=torch.float32, device=dev)
@@ -930,8 +932,9 @@ class FusedRowShard:
         H, s = self.H, stream.cuda_stream
         if n > 0:
             H.shard_keys(kp, s)
-            H.sort_pairs_iota(self.route_temp.data_ptr(), self.route_temp.numel(), self.rkeys.data_ptr(),
-                              self.rsk.data_ptr(), rp.svals, n, self.route_bits, s)
+            from ..models.fused import iota_sort
+
+            iota_sort(H, self.route_temp, self.rkeys.data_ptr(), self.rsk.data_ptr(), rp.svals, n, self.route_bits, s)
         H.shard_route(rp, s)
 
     def prime(self) -> None:
