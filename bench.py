@@ -563,7 +563,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
 
         ta = copy.copy(a)
         # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
-        ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(64, a.warmup), 16
+        # (32 steps per graph: 27.9-29.9 M ex/s vs 26.7-28.0 M at 16, profiles/r4_seg_sort.md)
+        ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(128, a.warmup), 32
         try:
             t = measure_tfrecord(ta, spec, hp, params, dev)
             out["tfrecord_steps"] = ta.steps
@@ -662,7 +663,7 @@ def measure_tfrecord(a, spec, hp, params, dev):
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--input tfrecord measures one GPU (use the Estimator / rocfm.cli for multi-GPU runs)")
-    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 16)
+    B, F, S = a.batch_size, a.field_size, (a.steps_per_graph if a.steps_per_graph > 0 else 32)
     if a.warmup < 4 * S:  # both parities' graphs captured before the window (the first launch is eager)
         import copy
 
