@@ -38,6 +38,10 @@ def run(cfg: Config) -> dict:
     from .estimator import Estimator
     from .parallel.dist import init_distributed
 
+    if cfg.parallelism == "async_ps":  # PS / worker roles over RPC, no process group
+        from .parallel.async_ps import run_job
+
+        return run_job(cfg)
     info = init_distributed("cuda" if torch.cuda.is_available() else "cpu", cfg.dist_timeout_s)
     if cfg.clear_existing_model and info.is_chief:
         clear_model_dir(cfg.effective_model_dir)  # HVD:372-378

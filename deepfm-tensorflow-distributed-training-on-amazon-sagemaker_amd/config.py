@@ -102,6 +102,8 @@ class Config:
     embedding_update: str = "sparse"  # sparse (lazy L2 + row optimizer) | exact (dense, faithful Q1)
     parallelism: str = "auto"  # auto | dp (replicated table) | rowshard (PS-equivalent) | dense_dp
     #                            | dp_owner (replicated table, owner-sharded embedding optimizer)
+    #                            | async_ps (asynchronous parameter servers over RPC, PS:461-521)
+    num_ps: int = 1  # async_ps: ranks 0 .. num_ps-1 are parameter servers, the rest workers
     lr_scaling: str = "linear"  # linear (lr × world, HVD:171) | none
     compute_dtype: str = "bf16"  # bf16 | fp8: MLP MFMA operands in the fused engine (fp8: the input
     #                              layer's forward GEMM on e4m3 with dynamic per-row/per-column scales)
@@ -195,7 +197,11 @@ class Config:
             raise ValueError(f"unknown embedding_update {self.embedding_update!r}")
         if self.compute_dtype not in ("bf16", "fp8"):
             raise ValueError(f"compute_dtype must be bf16 or fp8, got {self.compute_dtype!r}")
-        if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard", "dp_owner"):
+        if self.num_ps < 1:
+            raise ValueError("num_ps must be >= 1")
+        if self.parallelism == "async_ps" and (self.embedding_update != "sparse" or self.batch_norm):
+            raise ValueError("async_ps trains with embedding_update=sparse and without batch_norm")
+        if self.parallelism not in ("auto", "dp", "dense_dp", "rowshard", "dp_owner", "async_ps"):
             raise ValueError(f"unknown parallelism {self.parallelism!r}")
         if self.engine not in ("auto", "fused", "torch"):
             raise ValueError(f"unknown engine {self.engine!r}")

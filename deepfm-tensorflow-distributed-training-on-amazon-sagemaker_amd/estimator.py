@@ -57,7 +57,7 @@ class Estimator:
         self.world = _world()
         self.hp = OptHParams(name=cfg.optimizer, lr=cfg.learning_rate)
         self.engine_name = self._pick_engine()
-        if params is None and cfg.parallelism not in ("rowshard", "dp_owner"):
+        if params is None and cfg.parallelism not in ("rowshard", "dp_owner", "async_ps"):
             params = init_params(self.spec, cfg.seed)
         P = params  # row-shard: None → every rank initialises only its own rows
         self.eng = self._build_engine(P)
@@ -80,6 +80,8 @@ class Estimator:
     # ---- construction -------------------------------------------------------------------------
     def _pick_engine(self) -> str:
         e = self.cfg.engine
+        if self.cfg.parallelism == "async_ps":  # the eager step against the parameter servers
+            return "torch"
         if e == "auto":
             # batch_norm runs fused while the batch's row-kernel grid fits on the chip at once (its
             # moments are reduced with grid barriers): ≤ 4096 rows per GPU
@@ -94,6 +96,11 @@ class Estimator:
     def _build_engine(self, P):
         cfg = self.cfg
         cap = cfg.exchange_capacity or None
+        if cfg.parallelism == "async_ps":  # (RPC initialised by rocfm.parallel.async_ps.run_job)
+            from .parallel.async_ps import AsyncPSWorker
+
+            return AsyncPSWorker(self.spec, self.hp, cfg.num_ps, self.device, embedding_update=cfg.embedding_update,
+                                 dropout_seed=cfg.seed + 7919 * self.info.rank)
         if cfg.parallelism in ("rowshard", "dp_owner"):
             from .parallel.emb_shard import FusedRowShard, TorchRowShard
 
