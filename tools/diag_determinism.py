@@ -23,14 +23,13 @@ def main():
     vals = torch.rand(8, B, 39, generator=g)
     labels = (torch.rand(8, B, generator=g) < 0.3).float()
     out = {}
-    for S in (16, 1):
-        for rep in range(2):
-            eng = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 1), seed=3)
-            eng.attach_pool(ids.to(dev), vals.to(dev), labels.to(dev))
-            n = int(os.environ.get("STEPS", "40"))
-            eng.train_steps(n, S)
-            torch.cuda.synchronize()
-            out[(S, rep)] = {k: v.detach().cpu().clone() for k, v in eng.parameters_tf().items()}
+    runs = [(16, 0), (16, 1), (1, 0), (1, 1)]
+    for S, rep in runs:
+        eng = FusedDeepFM(spec, hp, B, dev, params=init_params(spec, 1), seed=3)
+        eng.attach_pool(ids.to(dev), vals.to(dev), labels.to(dev))
+        eng.train_steps(int(os.environ.get("STEPS", "40")), S)
+        torch.cuda.synchronize()
+        out[(S, rep)] = {k: v.detach().cpu().clone() for k, v in eng.parameters_tf().items()}
     keys = list(out)
     for i in range(len(keys)):
         for j in range(i + 1, len(keys)):
