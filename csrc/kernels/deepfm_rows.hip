@@ -1258,13 +1258,13 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
     }
     const bool diag = p.stamps != nullptr || p.ablate != 0;
     if (diag) {
-      if constexpr (SH::F == 39 && (SH::K == 10 || SH::kWide) && SH::nl == 3 && !BT) {
+      if constexpr (SH::F == 39 && (SH::K == 10 || SH::K == 32) && SH::nl == 3 && !BT) {
         ROCFM_REQUIRE(!p.fp8 && p.train, "deepfm_rows: diagnostics are built for the bf16 training kernel only");
         launch_rows_impl<KP4, SH, false, kTrain, true, false, RT>(p, stream);
         return;
       } else {
-        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need the 39x10 128-64-32 or "
-                                    "39x32 256-128-64 shape and an f32 table");
+        throw std::invalid_argument("deepfm_rows: diagnostics (stamps/ablate) need a 39-field k=10 or k=32 "
+                                    "3-layer shape and an f32 table");
       }
     }
     if (p.fp8) {
