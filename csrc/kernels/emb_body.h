@@ -32,6 +32,47 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
   return make_float4(__shfl_xor(v.x, d, 64), __shfl_xor(v.y, d, 64), __shfl_xor(v.z, d, 64), __shfl_xor(v.w, d, 64));
 }
 
+// DPP lane moves (VALU, no LDS traffic; __shfl_* compile to ds_bpermute, which shares the LDS
+// pipe with the chunk's row staging): bound_ctrl → lanes without a source read 0
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, true));
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void dpp_add4(float4& v, bool take) {
+  const float x = dppf<CTRL, ROW_MASK>(v.x), y = dppf<CTRL, ROW_MASK>(v.y), z = dppf<CTRL, ROW_MASK>(v.z),
+              w = dppf<CTRL, ROW_MASK>(v.w);
+  v.x += take ? x : 0.f;
+  v.y += take ? y : 0.f;
+  v.z += take ? z : 0.f;
+  v.w += take ? w : 0.f;
+}
+
+// Inclusive segmented scan over the 64 lanes: v[lane] = Σ v[seg .. lane] (seg = the first lane of
+// this lane's segment, ≤ lane).  Rows of 16 lanes first (row_shr 1, 2, 4, 8), then row 0's last
+// lane into row 1 and row 2's into row 3 (row_bcast:15), then lane 31 into rows 2-3
+// (row_bcast:31) — each step only where the segment reaches back that far.  seg = 0 everywhere:
+// lane 63 holds the wave's total.
+template <int N>
+__device__ __forceinline__ void seg_scan_dpp(float4 (&v)[N], int lane, int seg) {
+  const int rl = lane & 15, row = lane >> 4;
+  const bool t1 = rl >= 1 && lane - 1 >= seg, t2 = rl >= 2 && lane - 2 >= seg;
+  const bool t4 = rl >= 4 && lane - 4 >= seg, t8 = rl >= 8 && lane - 8 >= seg;
+  const bool t15 = (row & 1) && seg < (lane & ~15), t31 = row >= 2 && seg <= 31;
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x111, 0xf>(v[u], t1);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x112, 0xf>(v[u], t2);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x114, 0xf>(v[u], t4);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x118, 0xf>(v[u], t8);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x142, 0xa>(v[u], t15);
+#pragma unroll
+  for (int u = 0; u < N; ++u) dpp_add4<0x143, 0xc>(v[u], t31);
+}
+
 }  // namespace
 
 // One workgroup per 256 consecutive sorted entries.  Every thread loads ONE entry's gradient row
@@ -106,14 +147,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     const unsigned long long hm = __ballot(head || lane == 0 || !live);
     const unsigned long long below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const int seg = 63 - __clzll(hm & below);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-      for (int u = 0; u < KP4; ++u) {
-        const float4 o = f4shfl_up(v[u], d);
-        if (lane - d >= seg) v[u] = f4add(v[u], o);
-      }
-    }
+    seg_scan_dpp(v, lane, seg);
     if (t < kE) {  // (wave-uniform: kE is a multiple of 64)
 #pragma unroll
       for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
@@ -226,12 +260,8 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
 #pragma unroll
       for (int u = 0; u < KP4; ++u) tot[u] = f4add(tot[u], f4add(w[0][u], w[1][u]));
     }
-#pragma unroll
-    for (int u = 0; u < KP4; ++u) {
-#pragma unroll
-      for (int d = 32; d > 0; d >>= 1) tot[u] = f4add(tot[u], f4shfl_xor(tot[u], d));
-    }
-    if (lane == 0) {
+    seg_scan_dpp(tot, lane, 0);  // lane 63: the wave's total
+    if (lane == 63) {
 #pragma unroll
       for (int u = 0; u < KP4; ++u) s_cont[wave * KP4 + u] = tot[u];
     }
