@@ -167,6 +167,7 @@ void seg_sort_iota(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint3
   const Layout L = layout(nseg, seg_len);
   ROCFM_REQUIRE(temp != nullptr && temp_bytes >= L.total, "seg_sort: temporary storage too small");
   ROCFM_REQUIRE(keys_in && keys_out && vals_out, "seg_sort: null pointer");
+  ROCFM_REQUIRE(keys_in != keys_out, "seg_sort: keys_out must not alias keys_in (the last pass scatters into it)");
   uint8_t* tb = static_cast<uint8_t*>(temp);
   uint32_t* K[2] = {reinterpret_cast<uint32_t*>(tb + L.keys[0]), reinterpret_cast<uint32_t*>(tb + L.keys[1])};
   uint32_t* V[2] = {reinterpret_cast<uint32_t*>(tb + L.vals[0]), reinterpret_cast<uint32_t*>(tb + L.vals[1])};

@@ -141,6 +141,7 @@ def _applies():
 
 
 _DONE = [0]  # ps0: workers that finished training
+_DONE_LOCK = threading.Lock()  # (RPC requests run on the agent's thread pool)
 
 
 def _set_ready():
@@ -148,8 +149,9 @@ def _set_ready():
 
 
 def _worker_done():
-    _DONE[0] += 1  # (RPC calls run on the agent's thread pool; += on a list slot under the GIL)
-    return _DONE[0]
+    with _DONE_LOCK:
+        _DONE[0] += 1
+        return _DONE[0]
 
 
 def _done_count():
