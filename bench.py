@@ -264,6 +264,9 @@ def main():
         # in-house PyTorch-eager engine of the same model is reported separately for context
         "vs_baseline": None,
         "vs_eager_pytorch": (round(value / (base * world), 3) if base else None),
+        # (relative to a STORED constant: the eager engine's rate measured once, EAGER_BASELINE above,
+        # not re-measured in this run)
+        "vs_eager_pytorch_basis": "stored constant (EAGER_BASELINE, bench.py --engine torch, one MI355X)",
         "dtype": a.compute_dtype if a.engine == "fused" else "fp32",
         "data": "synthetic Criteo-shape (39 fields, Zipf ids, HBM-resident batch pool), random-init weights",
         "config": {
@@ -629,6 +632,100 @@ def secondary_windows(a, spec, hp, params, dev, pool):
         torch.cuda.empty_cache()
     if not tf_first:
         tf_window()
+    out.update(scale_windows(a, spec, hp, dev))
+    return out
+
+
+def scale_windows(a, spec, hp, dev):
+    """One GPU, the bench config's model at the vocabulary scales of BASELINE.json configs 4 and 5,
+    each window fenced (a failure becomes ``<name>_error``) and timed like the headline (same
+    warm-up, steps, steps per graph; full optimisation steps):
+
+    * ``rowshard100m``: config 4's PS-equivalent row-sharded table at 100M rows (the owner-routed
+      lookup / gradient exchange at world 1, ``…multiInstance.py:461-521``);
+    * ``capacity``: config 5 — the largest table with f32 Adam slots that fits this GPU's HBM next to
+      the step's buffers (≈90 %: 1.8B rows × (k+1 → 12 floats) × {table, m, v} ≈ 259 GB on a
+      288 GB MI355X), with the fp8-e4m3 MFMA MLP input layer; reports the rows and the bytes
+      resident."""
+    import gc
+
+    import torch
+
+    from rocfm.data.synthetic import SyntheticCriteo
+    from rocfm.models.deepfm import ModelSpec
+
+    out = {}
+    S = a.steps_per_graph
+    B = a.batch_size
+
+    def pool_for(V, n):
+        gen = SyntheticCriteo(V, spec.field_size, seed=a.seed)
+        g = torch.Generator(device=dev).manual_seed(a.seed)
+        pb = [gen.batch(B, dev, g) for _ in range(n)]
+        return tuple(torch.stack([x[i] for x in pb]) for i in range(3))
+
+    def window(name, V, build, **extra):
+        eng, pool = None, None
+        try:
+            t0 = time.perf_counter()
+            sp = ModelSpec(V, spec.field_size, spec.embedding_size, spec.layers, spec.keep_probs, l2_reg=spec.l2_reg)
+            pool = pool_for(V, min(a.pool, 16))
+            eng = build(sp, pool)
+            torch.cuda.synchronize()
+            build_s = time.perf_counter() - t0
+            resident = torch.cuda.memory_allocated(dev)
+            eng.attach_pool(*pool)
+            eng.train_steps(a.warmup, S)
+            eng.precapture(a.steps, S)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.train_steps(a.steps, S)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            eng.check() if not hasattr(eng, "verify_replicas") else eng.check(replicas=False)
+            out[f"{name}_examples_per_sec"] = round(B * a.steps / dt, 1)
+            out[f"{name}_ms_per_step"] = round(dt / a.steps * 1e3, 4)
+            out[f"{name}_feature_size"] = V
+            out[f"{name}_bytes_resident"] = int(resident)
+            out[f"{name}_build_s"] = round(build_s, 2)
+            out.update({f"{name}_{k}": v for k, v in extra.items()})
+        except Exception as e:  # noqa: BLE001 — a secondary window never costs the headline
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
+        finally:
+            if eng is not None and hasattr(eng, "close"):
+                try:
+                    eng.close()
+                except Exception:  # noqa: BLE001
+                    pass
+            del eng, pool
+            gc.collect()
+            torch.cuda.empty_cache()
+
+    from rocfm.parallel.dp import pool_exchange_capacity
+    from rocfm.parallel.emb_shard import FusedRowShard
+
+    def rowshard(sp, pool):
+        return FusedRowShard(sp, hp, B, dev, params=None, seed=a.seed, capacity=pool_exchange_capacity(pool[0], 1),
+                             compute_dtype=a.compute_dtype)
+
+    window("rowshard100m", 100_000_000, rowshard, parallelism="rowshard1")
+
+    from rocfm.models.fused import FusedDeepFM
+
+    free, total = torch.cuda.mem_get_info(dev)
+    kp = (spec.embedding_size + 1 + 3) // 4 * 4
+    per_row = kp * 4 * 3  # f32 table + Adam m, v
+    # ≈90 % of the device for the table + slots, ids < 2^31, at most what is free now minus 6 GB
+    rows = min(int(0.9 * total) // per_row, (free - (6 << 30)) // per_row, (1 << 31) - 1)
+    rows = rows // 1_000_000 * 1_000_000
+
+    def capacity(sp, pool):
+        return FusedDeepFM(sp, hp, B, dev, params=None, seed=a.seed, compute_dtype="fp8")
+
+    if rows >= 1_000_000:
+        window("capacity", rows, capacity, table_bytes=rows * per_row, hbm_total_bytes=int(total),
+               hbm_fraction=round(rows * per_row / total, 3), compute_dtype="fp8", table_dtype="f32",
+               optimizer_slots="f32 Adam m, v")
     return out
 
 

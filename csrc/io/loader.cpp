@@ -465,11 +465,13 @@ std::string BatchLoader::resolve(std::vector<RecordRef>* recs, int64_t seq) cons
     uint64_t len;
     memcpy(&len, x.data, 8);
     if (len > left - 16 || len > UINT32_MAX) return "TFRecord: truncated record" + where(r);
-    if (opt_.verify_crc) {
-      uint32_t lcrc;
-      memcpy(&lcrc, x.data + 8, 4);
-      if (mask_crc(crc32c(x.data, 8)) != lcrc) return "TFRecord: corrupt length CRC" + where(r);
-    }
+    // the length CRC is checked even with verify_crc off (8 bytes per record): a frame offset taken
+    // from a sidecar index (record_index.h) is trusted only through (size, mtime, both ends), so a
+    // file rewritten in place with the same size and a coarse mtime would otherwise decode garbage
+    uint32_t lcrc;
+    memcpy(&lcrc, x.data + 8, 4);
+    if (mask_crc(crc32c(x.data, 8)) != lcrc)
+      return std::string("TFRecord: corrupt length CRC") + (opt_.verify_crc ? "" : " (stale record index?)") + where(r);
     x.data += 12;
     x.len = (uint32_t)len;
   }

@@ -54,7 +54,11 @@ struct FetchMultiParams {
   uint32_t* keys;   // [S][B*F] composite sort keys (nullable): step k's keys are k << id_bits | id
   int id_bits;
   unsigned long long* keys64;  // [S][B*F] (nullable; instead of keys): k << id_bits | id as 64-bit
-                               // keys — vocabularies too wide for S << id_bits to fit 32 bits
+                               // keys — vocabularies too wide for S << id_bits to fit 32 bits, sorted
+                               // by rocPRIM (ROCFM_SORT_LIB=rocprim A/B only)
+  int plain_keys;   // 1: keys holds the plain id keys of each batch (no k << id_bits): the segmented
+                    // sort (seg_sort.hip) orders every batch on its own id bits, so the 100M-1B-row
+                    // vocabularies need no 64-bit composite keys
   int shard_W;      // > 0: keys are owner-major row-shard keys (id % W)·Vs + id / W (shard.hip)
   uint32_t shard_Vs;
   const uint32_t* shard_hot;  // replicated ids (ascending; shard_key in shard.h), nullable
@@ -65,6 +69,8 @@ struct FetchMultiParams {
   int opt_type;
   int32_t* bad_ids;  // nullable: device-side id guard, as in FetchParams
   uint32_t max_id;
+  const int32_t* halt;  // nullable: the input pipeline's sticky error word (decode.hip); non-zero →
+                        // every prepared step carries kHaltStepBit (optim.h: its updates are skipped)
 };
 
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream);

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
   int32_t* di = p.ids + (long long)k * p.Bp * p.F;
   float* dv = p.vals + (long long)k * p.Bp * p.F;
   uint32_t* dk = p.keys ? p.keys + (long long)k * n : nullptr;
-  const uint32_t kb = p.keys64 ? 0u : (uint32_t)k << p.id_bits;
+  const uint32_t kb = (p.keys64 || p.plain_keys) ? 0u : (uint32_t)k << p.id_bits;
   unsigned long long* dk64 = p.keys64 ? p.keys64 + (long long)k * n : nullptr;
   const unsigned long long kb64 = (unsigned long long)k << p.id_bits;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void fetch_multi_kernel(const FetchMultiParams
     p.labels[(long long)k * p.Bp + i] = p.labels_pool[b * p.B + i];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t st = *p.step_src + p.advance + k;
-    p.steps[k] = st;
+    p.steps[k] = (p.halt != nullptr && *p.halt != 0) ? (st | kHaltStepBit) : st;
     p.lrt[k] = p.opt_type == kAdam ? adam_lr_t(p.lr, p.beta1, p.beta2, st) : p.lr;
     if (k == 0) {
       *p.cur_dst = start;
@@ -293,8 +293,9 @@ void launch_dedup(const DedupParams& p, hipStream_t stream) {
 void launch_fetch_multi(const FetchMultiParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.pool_batches > 0 && p.S > 0, "fetch_multi: empty pool / S");
   ROCFM_REQUIRE(p.cur_dst != p.cur_src && p.step_dst != p.step_src, "fetch_multi: counters must differ");
-  ROCFM_REQUIRE(p.keys == nullptr || ((unsigned long long)p.S << p.id_bits) <= (1ull << 32),
-                "fetch_multi: S << id_bits must fit in 32 bits (use 64-bit keys)");
+  ROCFM_REQUIRE(p.keys == nullptr || p.plain_keys || ((unsigned long long)p.S << p.id_bits) <= (1ull << 32),
+                "fetch_multi: S << id_bits must fit in 32 bits (use plain per-batch keys)");
+  ROCFM_REQUIRE(!p.plain_keys || (p.keys != nullptr && p.keys64 == nullptr), "fetch_multi: plain_keys needs keys");
   ROCFM_REQUIRE(p.keys64 == nullptr || p.id_bits <= 32, "fetch_multi: ids wider than 32 bits");
   const long long n = (long long)p.B * p.F;
   const int gx = (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 64));

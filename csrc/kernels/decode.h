@@ -27,5 +27,7 @@ struct DecodeParams {
 };
 
 void launch_decode_examples(const DecodeParams& p, hipStream_t stream);
+size_t decode_lds_bytes(int F);  // dynamic LDS of one decode workgroup
+bool decode_fits(int F);         // F ≤ 192 and that LDS fits the current device (opt-in limit)
 
 }  // namespace rocfm

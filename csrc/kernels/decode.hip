@@ -362,14 +362,32 @@ __global__ __launch_bounds__(kDecRecs) void decode_examples_kernel(DecodeParams 
 
 }  // namespace
 
+size_t decode_lds_bytes(int F) { return (size_t)kStageWords * 4 + (size_t)kDecRecs * F * 8 + kDecRecs * 8; }
+
+bool decode_fits(int F) {
+  static int max_lds = -1;
+  if (max_lds < 0) {
+    int dev = 0, v = 0;
+    ROCFM_HIP_CHECK(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 0)
+      ROCFM_HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+    max_lds = v;
+  }
+  return F >= 1 && F <= 192 && decode_lds_bytes(F) <= (size_t)max_lds;
+}
+
 void launch_decode_examples(const DecodeParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.B > 0 && p.F > 0 && p.F <= 192 && p.nb >= 0 && p.R > 0 && p.cap % 16 == 0,
                 "decode_examples: bad shape");
   ROCFM_REQUIRE(p.bytes && p.offs && p.ids && p.vals && p.labels && p.err, "decode_examples: null pointer");
   for (int w = 0; w < 3; ++w) ROCFM_REQUIRE(p.klen[w] >= 0 && p.klen[w] <= kDecodeKeyMax, "decode: key too long");
   if (p.nb == 0) return;
-  const size_t lds = (size_t)kStageWords * 4 + (size_t)kDecRecs * p.F * 8 + kDecRecs * 8;
+  const size_t lds = decode_lds_bytes(p.F);
   const int blocks = p.nb * cdiv(p.B, kDecRecs);
+  // the device's opt-in LDS limit (160 KiB per workgroup on gfx950): a wider schema is refused here,
+  // before any launch, and the Estimator parses on the host instead (decode_fits)
+  ROCFM_REQUIRE(decode_fits(p.F), "decode_examples: field_size " + std::to_string(p.F) + " needs " +
+                                      std::to_string(lds) + " B of LDS, more than this device allows");
   if (lds > 65536) {  // beyond the default dynamic-LDS limit (160 KiB per CU on gfx950)
     ROCFM_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(decode_examples_kernel),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -729,7 +729,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           }
           ST[c] = mean;
           ST[Dout + c] = rsqrtf(m2 / (float)p.B + p.bn_eps);
-          if (blockIdx.x == 0) {  // moving averages; the variance one is unbiased (TF fused BN)
+          if (blockIdx.x == 0 && !(p.step && (*p.step & kHaltStepBit))) {  // moving averages (not in a
+            // halted step, optim.h); the variance one is unbiased (TF fused BN)
             p.bn_mean[l][c] = p.bn_mean[l][c] * p.bn_decay + mean * (1.f - p.bn_decay);
             p.bn_var[l][c] = p.bn_var[l][c] * p.bn_decay + (m2 / (float)max(p.B - 1, 1)) * (1.f - p.bn_decay);
           }

@@ -16,9 +16,17 @@ struct OptParams {
   const float* lrt = nullptr;  // precomputed step-dependent lr_t (written by fetch_batch), or null
 };
 
+// Halted step: the side chain's batch preparation sets this bit in a step's device global_step when
+// the input pipeline has flagged an error (a malformed record parsed on the GPU, decode.hip): every
+// optimizer update of that step is skipped, so a bad batch never reaches the parameters, the slots or
+// a checkpoint (tf.data's parse_example fails before the batch is used, PS:117-132).  The low 32 bits
+// (dropout keys, tags) are unchanged.
+constexpr int64_t kHaltStepBit = 1ll << 62;
+
 // Step-dependent scalars, computed once per thread from the device step counter (t = step+1).
 struct OptStep {
   float lr_t;  // Adam: lr·√(1−β2ᵗ)/(1−β1ᵗ); others: lr
+  bool skip;   // halted step (kHaltStepBit): no update
 };
 
 __host__ __device__ inline float adam_lr_t(float lr, float beta1, float beta2, int64_t step) {
@@ -28,6 +36,7 @@ __host__ __device__ inline float adam_lr_t(float lr, float beta1, float beta2, i
 
 __device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
   OptStep s;
+  s.skip = (step & kHaltStepBit) != 0;
   if (o.lrt) {
     s.lr_t = *o.lrt;
   } else if (o.type == kAdam) {
@@ -41,6 +50,7 @@ __device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
 // In-place update of param p and slots s0/s1 with gradient g.
 __device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st, float& p, float g, float& s0,
                                           float& s1) {
+  if (st.skip) return;
   switch (o.type) {
     case kAdam: {
       s0 = o.beta1 * s0 + (1.f - o.beta1) * g;

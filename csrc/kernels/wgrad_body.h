@@ -368,11 +368,13 @@ inline int wgrad_prepare(WgradParams& p, int co_resident = -1, int max_wg = 256)
   };
   int n = fill();
   if (co_resident < 0) return n;
-  const char* env = getenv("ROCFM_WGRAD_TW");  // A/B: force a width on every layer it divides
-  if (env && *env) {
-    const int f = atoi(env);
+  // A/B: ROCFM_WGRAD_TW=2|4 forces a width on every layer it divides; any other value (auto) widens
+  // automatically below
+  const char* env = getenv("ROCFM_WGRAD_TW");
+  const int forced = env ? atoi(env) : 0;
+  if (forced == 2 || forced == 4) {
     for (int l = 0; l < p.nl; ++l)
-      if ((f == 2 || f == 4) && p.dims[l + 1] % (32 * f) == 0) p.tw[l] = f;
+      if (p.dims[l + 1] % (32 * forced) == 0) p.tw[l] = forced;
     return fill();
   }
   while (n + co_resident > max_wg) {  // widen the layer with the most tiles that can still widen

@@ -222,7 +222,7 @@ class Estimator:
         # (raw_groups) and the GPU parses them (decode.hip); the host only frames, checks CRCs and
         # copies bytes.  Not for pipe mode, skip_bad or the decoded on-disk cache (host batches).
         raw = stream and cfg.device_decode and not cfg.pipe_mode and cfg.on_bad_record != "skip" \
-            and not cfg.decoded_cache_dir
+            and not cfg.decoded_cache_dir and self._device_decode_fits()
 
         def groups_of(d, skip=0, lim=None):
             if raw:
@@ -382,6 +382,14 @@ class Estimator:
         if getattr(self, "_ctrl", None) is None:
             self._ctrl = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
         return self._ctrl
+
+    def _device_decode_fits(self) -> bool:
+        """The device Example parser's LDS stage fits this schema on this GPU (decode.hip
+        decode_fits: ≤ 192 fields and the opt-in LDS limit); otherwise the host parses."""
+        from .ops import hip
+
+        H = hip()
+        return H is not None and hasattr(H, "decode_fits") and bool(H.decode_fits(self.cfg.field_size))
 
     def _agreed_epoch_batches(self, ds) -> Optional[int]:
         """Every rank must run the same number of synchronous steps (each step is a collective).

@@ -293,6 +293,10 @@ class FusedDeepFM:
         self.id_guard = ids_check_enabled()
         self.id_limit = self.V
         self.bad_ids = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the device Example parser's sticky error word [code, batch, record, -] (decode.hip); the
+        # side chain's batch preparation reads it, and once it is set every prepared step is halted
+        # (optim.h kHaltStepBit: no optimizer update), so a malformed record never trains
+        self.halt_word = torch.zeros(4, dtype=torch.int32, device=dev)
         # default batch source: a 2-slot ring fed by push_batch()
         self._ring = True
         self._set_pool(torch.zeros(2, B, F, dtype=torch.int32, device=dev),
@@ -737,14 +741,15 @@ class FusedDeepFM:
     # One graph replays S steps whose main stream is strictly serial (rows → wgrad → emb_update per
     # step: cross-stream waits inside a graph cost more than the concurrency they buy — measured
     # 47 vs 55 µs/step); ONE side chain per graph prepares the NEXT graph's S batches (one copy
-    # kernel) and sorts all S·B·F lookups at once (composite key batch << id_bits | id), joined
-    # at the graph's end.
+    # kernel) and sorts all S·B·F lookups at once (S segments of one batch each), joined at the
+    # graph's end.
     def _multi_S(self, Smax: int, shard: Optional[tuple] = None):
-        """(id bits, steps per graph).  Graphs of S steps sort all S·B·F lookups at once on the
-        composite 32-bit key ``k << id_bits | id`` while S << id_bits fits (vocabularies up to
-        2^26 rows at S = 64); wider vocabularies (100M-1B rows) keep S and sort 64-bit composite
-        keys, whose ids the side chain then hands on as plain per-batch 32-bit keys
-        (``m_composite`` False)."""
+        """(id bits, steps per graph).  Graphs of S steps sort all S·B·F lookups at once as S
+        segments (seg_sort.hip: each batch on its own id bits).  While S << id_bits fits 32 bits
+        (vocabularies up to 2^26 rows at S = 64) the keys carry their batch, ``k << id_bits | id``
+        (``m_composite``: what rocPRIM's one-array sort needs, kept as the A/B); wider vocabularies
+        (100M-1B rows) sort plain per-batch id keys (``m_plain``) — no 64-bit keys unless the
+        rocPRIM A/B is asked for (ROCFM_SORT_LIB=rocprim: 64-bit composite keys)."""
         key_range = self.V if shard is None else (shard[0] + (len(shard) > 2)) * shard[1]  # + hot owner
         idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
         return idbits, max(1, int(Smax))
@@ -760,6 +765,7 @@ class FusedDeepFM:
         idbits, Smax = self._multi_S(Smax, shard)
         sbits = math.ceil(math.log2(Smax)) if Smax > 1 else 0
         self.m_composite = (Smax << idbits) <= (1 << 32) and os.environ.get("ROCFM_SORT", "") != "wide"
+        self.m_plain = not self.m_composite and sort_lib() == "rocfm"  # per-batch 32-bit id keys
         self.mS, self.m_idbits = Smax, idbits
         self.m_bits = idbits + sbits
         i32 = dict(dtype=torch.int32, device=dev)
@@ -769,10 +775,10 @@ class FusedDeepFM:
         self.m_keys = torch.zeros(Smax * n, **i32)
         self.m_sk = torch.zeros(2, Smax * n, **i32)
         self.m_sv = torch.zeros(2, Smax * n, **i32)
-        if self.m_composite:
-            tb = iota_sort_temp_bytes(H, n, idbits, Smax, sbits)
+        if self.m_composite or self.m_plain:
+            tb = iota_sort_temp_bytes(H, n, idbits, Smax, sbits if self.m_composite else 0)
             self.m_keys64 = None
-        else:  # 64-bit keys in / out (the sorted ids land in m_sk via sort_aux)
+        else:  # rocPRIM A/B: 64-bit keys in / out (the sorted ids land in m_sk via sort_aux)
             tb = H.sort_pairs64_temp_bytes(Smax * n, self.m_bits)
             self.m_keys64 = torch.zeros(2, Smax * n, dtype=torch.int64, device=dev)
         self.m_temp = torch.zeros(max(tb, 16), dtype=torch.uint8, device=dev)
@@ -829,7 +835,9 @@ class FusedDeepFM:
         f.ids, f.vals, f.labels = (self.m_ids[1 - q].data_ptr(), self.m_vals[1 - q].data_ptr(),
                                    self.m_labels[1 - q].data_ptr())
         f.keys, f.id_bits = self.m_keys.data_ptr(), self.m_idbits
-        if not self.m_composite:
+        if self.m_plain:
+            f.plain_keys = 1
+        elif not self.m_composite:
             f.keys, f.keys64 = 0, self.m_keys64[0].data_ptr()
         if getattr(self, "_m_shard", None) is not None:
             f.shard_W, f.shard_Vs = self._m_shard[:2]
@@ -838,16 +846,18 @@ class FusedDeepFM:
         f.steps, f.lrt = self.m_steps[1 - q].data_ptr(), self.m_lrt[1 - q].data_ptr()
         f.lr, f.beta1, f.beta2 = self.hp.lr * self.lr_scale, self.hp.beta1, self.hp.beta2
         f.opt_type = OPT_ID[self.hp.name]
+        f.halt = self.halt_word.data_ptr()
         self._guard(f)
         return f
 
     def _prepare_multi(self, q: int, advance: int, stream) -> None:
         H = self.H
         H.fetch_multi(self._fetch_multi_params(q, advance), stream.cuda_stream)
-        if self.m_composite:  # all S batches in one sort
+        if self.m_composite or self.m_plain:  # all S batches in one (segmented) sort
             iota_sort(H, self.m_temp, self.m_keys.data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_sv[1 - q].data_ptr(),
-                      self.n_lookup, self.m_idbits, stream.cuda_stream, nseg=self.mS, seg_bits=self.m_bits - self.m_idbits)
-        else:  # one sort of 64-bit composite keys
+                      self.n_lookup, self.m_idbits, stream.cuda_stream, nseg=self.mS,
+                      seg_bits=(self.m_bits - self.m_idbits) if self.m_composite else 0)
+        else:  # rocPRIM A/B: one sort of 64-bit composite keys
             H.sort_pairs64_iota(self.m_temp.data_ptr(), self.m_temp.numel(), self.m_keys64[0].data_ptr(),
                                 self.m_keys64[1].data_ptr(), self.m_sv[1 - q].data_ptr(), self.mS * self.n_lookup,
                                 self.m_bits, stream.cuda_stream)
@@ -857,11 +867,11 @@ class FusedDeepFM:
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
         if self.m_chd is not None:
             a.chunk_heads = self.m_chd[1 - q].data_ptr()
-        if not self.m_composite:  # sorted 64-bit keys → plain per-batch ids in m_sk
+        if self.m_keys64 is not None:  # sorted 64-bit keys → plain per-batch ids in m_sk
             a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
         if self.m_dedup:  # positions / run ends / run heads come from the dedup over the compacted list
             a.chunk_end = a.chunk_heads = 0
-        if not (self.m_dedup and self.m_composite):  # (64-bit keys: sort_aux writes the plain ids)
+        if not (self.m_dedup and self.m_keys64 is None):  # (64-bit keys: sort_aux writes the plain ids)
             H.sort_aux(a, stream.cuda_stream)
         if self.m_dedup:
             d = H.DedupParams()
@@ -883,6 +893,8 @@ class FusedDeepFM:
         self.m_cur[1] = base + self._i
         self.m_step[1] = self._i
         self._prepare_multi(1, 0, torch.cuda.current_stream(self.device))  # → parity-0 buffers
+        self._pl_op("main", f"prime steps {self._i}+", self._pl_ring(self._i, self.mS, False)
+                    + [("m_batches", 0, 1, True)])
         self._m_side_ev = None  # the prime ran on the main stream
         self._mq = 0
         self._m_primed = True
@@ -935,20 +947,30 @@ class FusedDeepFM:
                 graphs[key + (q, S, "side")], graphs[key + (q, S, "main")] = gs, gm
         if capture_only:
             return
+        # (ROCFM_HAZARD stream plan: the side graph reads the ring slots of the next graph's steps
+        # and writes the parity 1-q batch buffers; the main graph reads parity q)
+        side_rng = ((self._pl_ring(self._i + S, self.mS, False) if getattr(self, "_ring_mode_stream", False) else [])
+                    + [("m_batches", 1 - q, 2 - q, True)])
+        main_rng = [("m_batches", q, q + 1, False)]
         if eager:
             rec = self._hazard
             if rec is not None:
                 rec.begin("side")
             side.wait_stream(main)
+            if getattr(self, "_plan", None) is not None:
+                self._plan.wait_stream("side", "main")
             with torch.cuda.stream(side):
                 self._prepare_multi(q, S, side)
-            ev = torch.cuda.Event()
+            self._pl_op("side", f"side graph @{self._i} (eager)", side_rng)
+            ev = self._pl_mark(torch.cuda.Event(), "side")
             ev.record(side)
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
+                self._pl_wait("main", self._m_side_ev)
             if rec is not None:
                 rec.begin("main")
             body(q, S)
+            self._pl_op("main", f"main graph @{self._i} (eager)", main_rng)
             if rec is not None:
                 rec.end()
                 rec.check(f"eager {key + (q, S)}")
@@ -956,15 +978,19 @@ class FusedDeepFM:
             # main graph submitted first: its kernels start while the host is still submitting the
             # side graph (a timed window otherwise begins with the side graph's whole submission);
             # the side graph still waits only for the main work queued BEFORE this main graph
-            before = torch.cuda.Event()
+            before = self._pl_mark(torch.cuda.Event(), "main")
             before.record(main)
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
+                self._pl_wait("main", self._m_side_ev)
             gm.replay()
+            self._pl_op("main", f"main graph @{self._i}", main_rng)
             side.wait_event(before)
+            self._pl_wait("side", before)
             with torch.cuda.stream(side):
                 gs.replay()
-            ev = torch.cuda.Event()
+            self._pl_op("side", f"side graph @{self._i}", side_rng)
+            ev = self._pl_mark(torch.cuda.Event(), "side")
             ev.record(side)
         self._m_side_ev = ev
         self._m_warm += 1
@@ -985,6 +1011,40 @@ class FusedDeepFM:
                 n -= S
         finally:
             self._mq = q0
+
+    # ---- ROCFM_HAZARD: the streamed loop's three-stream plan (utils/hazard.py StreamPlan) --------
+    def _pl_tok(self, ev):
+        return getattr(ev, "_hz_tok", 0)
+
+    def _pl_mark(self, ev, stream: str):
+        """Note that ``ev`` was just recorded on ``stream`` (plan token on the event)."""
+        pl = getattr(self, "_plan", None)
+        if pl is not None and ev is not None:
+            ev._hz_tok = pl.record(stream)
+        return ev
+
+    def _pl_wait(self, stream: str, ev) -> None:
+        pl = getattr(self, "_plan", None)
+        if pl is not None and ev is not None:
+            pl.wait(stream, self._pl_tok(ev))
+
+    def _pl_ring(self, first_step: int, count: int, write: bool, slot0: Optional[int] = None):
+        """Ring-slot ranges of ``count`` batches from global step ``first_step`` (or from slot
+        ``slot0``), split at the ring's end."""
+        R = int(self.pool_ids.shape[0])
+        s0 = (getattr(self, "_start_batch", 0) + first_step) % R if slot0 is None else slot0 % R
+        out, left = [], count
+        while left > 0:
+            m = min(left, R - s0)
+            out.append(("ring", s0, s0 + m, write))
+            left -= m
+            s0 = 0
+        return out
+
+    def _pl_op(self, stream: str, label: str, ranges=()) -> None:
+        pl = getattr(self, "_plan", None)
+        if pl is not None:
+            pl.op(stream, label, ranges)
 
     def _tail(self, wp, ep, ed, s: int) -> None:
         """MLP weight gradients + embedding update: one launch (step_tail.hip) when the rows fit."""
@@ -1034,7 +1094,10 @@ class FusedDeepFM:
         or undecoded ``RawGroup``s (``TFRecordDataset.raw_groups``): their Example payload bytes
         are copied as they are and parsed on the copy stream by the decode kernel straight into
         the ring slots (``csrc/kernels/decode.hip``) — the host only moves bytes.  A malformed
-        record raises RuntimeError within two groups (its batch trains on zeros until then).
+        record sets the parser's sticky error word: every step the side chain prepares from then on
+        is halted on the device (no optimizer update — the bad batch, and any batch after it, never
+        trains), and RuntimeError is raised within two groups, by ``check()`` and so before any
+        checkpoint (``state_dict``).
         The source may recycle an item's host memory once it has been advanced ``hold`` more
         times; the copy of every such item is waited for first.  Returns the number of steps
         trained; ``after_steps(first_step, n_steps)`` runs after each graph launch.
@@ -1071,11 +1134,20 @@ class FusedDeepFM:
         copy = getattr(self, "_copy_stream", None) or torch.cuda.Stream(device=dev)
         self._copy_stream = copy
         it = iter(batches)
+        # ROCFM_HAZARD=1: every copy / side / main operation of this loop and its event waits go
+        # into a happens-before plan, checked after each graph launch (utils/hazard.py StreamPlan)
+        self._plan = hazard.StreamPlan() if self._hazard is not None else None
+        names = {}  # stream handle → plan stream name
+        if self._plan is not None:
+            names = {copy.cuda_stream: "copy", self.sort_stream.cuda_stream: "side",
+                     torch.cuda.current_stream(dev).cuda_stream: "main"}
+            if npre:
+                self._pl_op("main", "prefix", self._pl_ring(0, npre, True, slot0=0))
 
         def mark(stream):
             e = torch.cuda.Event()
             e.record(stream)
-            return e
+            return self._pl_mark(e, names.get(stream.cuda_stream, "?"))
 
         pending = []  # (event, host batch) kept alive until its copy has completed
         carry = [None]  # the part of a group that did not fit the previous graph (same host memory)
@@ -1103,6 +1175,8 @@ class FusedDeepFM:
                         b, n = RawGroup(b.bytes[:m], b.offs[:m], m, b.B), m
                     with torch.cuda.stream(copy):
                         self._stage_raw(b, staged % R, R, staged)
+                    self._pl_op("copy", f"raw stage of batches {staged}..{staged + n - 1}",
+                                self._pl_ring(0, n, True, slot0=staged % R) + [("raw_stage", 0, 1, True)])
                     pending.append((mark(copy), b))
                     staged += n
                     got += n
@@ -1127,6 +1201,8 @@ class FusedDeepFM:
                         ring[1][slot:slot + m].copy_(vals[o:o + m], non_blocking=True)
                         ring[2][slot:slot + m].copy_(labels[o:o + m], non_blocking=True)
                         o += m
+                self._pl_op("copy", f"copy of batches {staged}..{staged + n - 1}",
+                            self._pl_ring(0, n, True, slot0=staged % R))
                 pending.append((mark(copy), b))
                 staged += n
                 got += n
@@ -1139,6 +1215,7 @@ class FusedDeepFM:
         staged_new = lambda: staged - npre  # noqa: E731 — batches of this call's stream
         cevs = [mark(copy)]  # cevs[j]: copies read by graph j's side chain (graph j+1's batches)
         main.wait_event(cevs[0])
+        self._pl_wait("main", cevs[0])
         if build is not None:
             build(S)
         elif getattr(self, "m_req", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
@@ -1147,20 +1224,28 @@ class FusedDeepFM:
         self._prime_multi()  # prepares steps i0 .. i0+S-1 from the ring
         prime_ev = mark(main)
         sevs = []  # sevs[j]: end of graph j's side chain (side graph, sort stream)
+        inject = self._plan is not None and os.environ.get("ROCFM_HAZARD_INJECT", "") == "ring"
         done, j = 0, 0
         while done < staged_new():
             n = min(S, staged_new() - done)
             # stage graph j+2's batches; their ring slots held graph j-2's batches, last read by
             # graph j-3's side chain (or by the prime)
-            copy.wait_event(sevs[j - 3] if j >= 3 else prime_ev)
+            wait_ev = sevs[j - 3] if j >= 3 else prime_ev
+            if inject and j >= 3:  # (hazard test only) the refill waits one side graph too early
+                wait_ev = sevs[j - 4] if j >= 4 else prime_ev
+            copy.wait_event(wait_ev)
+            self._pl_wait("copy", wait_ev)
             more = stage(S)
             cevs.append(mark(copy))
             self.sort_stream.wait_event(cevs[j])
+            self._pl_wait("side", cevs[j])
             if run is not None:
                 run(n)
             else:
                 self._run_multi_graph(n)
             sevs.append(self._m_side_ev)
+            if self._plan is not None:
+                self._plan.check(f"train_stream graph {j}")
             if after_steps is not None:
                 after_steps(i0 + done, n)
             done += n
@@ -1170,6 +1255,7 @@ class FusedDeepFM:
         main.wait_stream(self.sort_stream)
         for e0, _ in pending:
             e0.synchronize()
+        self._plan = None
         self._check_decode(block=True)
         self._primed = False
         return done
@@ -1183,7 +1269,7 @@ class FusedDeepFM:
         if st is None or st[0].numel() < n * cap + 64 or st[1].shape[0] < n or st[1].shape[1] != self.B + 1:
             d_bytes = torch.empty(n * cap + 64, dtype=torch.uint8, device=self.device)  # +64: window reads
             d_offs = torch.empty(n, self.B + 1, dtype=torch.int32, device=self.device)
-            d_err = torch.zeros(4, dtype=torch.int32, device=self.device)
+            d_err = self.halt_word  # (the error word the step preparation halts on)
             h_err = torch.zeros(4, dtype=torch.int32, pin_memory=True)
             st = self._raw_dev = [d_bytes, d_offs, d_err, h_err, None]
         d_bytes, d_offs, d_err, h_err, _ = st
@@ -1397,7 +1483,9 @@ class FusedDeepFM:
 
     def check(self) -> None:
         """Raise if a batch-norm grid barrier of the row kernel timed out (the step's moments are
-        then invalid; a sticky device flag, read with one small copy)."""
+        then invalid; a sticky device flag, read with one small copy), or if the device Example
+        parser flagged a malformed record (its steps were halted, never trained)."""
+        self._check_decode(block=True)
         if self.bn and int(self.bn_error[0].item()) != 0:
             raise RuntimeError("deepfm_rows: a batch_norm grid barrier timed out (not every workgroup was resident)")
         if self.id_guard and int(self.bad_ids.item()) != 0:

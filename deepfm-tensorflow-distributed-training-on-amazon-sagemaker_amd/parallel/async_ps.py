@@ -162,6 +162,33 @@ def _is_ready():
     return _READY.is_set()
 
 
+_FAILED = [0]  # ps0: workers that raised (their peers stop waiting for them)
+
+
+def _worker_failed():
+    with _DONE_LOCK:
+        _FAILED[0] += 1
+        return _FAILED[0]
+
+
+def _failed_count():
+    return _FAILED[0]
+
+
+def _wait_ps0(pred, what: str, timeout_s: float) -> None:
+    """Poll ps0 until ``pred()`` (an RPC) holds; raise if a worker has reported a failure or after
+    ``timeout_s`` — a dead peer must fail the job, not hang it (then rpc.shutdown hangs too)."""
+    from torch.distributed import rpc
+
+    deadline = time.time() + max(1.0, float(timeout_s))
+    while not pred():
+        if rpc.rpc_sync(ps_name(0), _failed_count) > 0:
+            raise RuntimeError(f"async PS: a worker failed while this worker waited for {what}")
+        if time.time() > deadline:
+            raise TimeoutError(f"async PS: waited {timeout_s:.0f} s for {what} (dist_timeout_s)")
+        time.sleep(0.05)
+
+
 class AsyncPSWorker:
     """Worker-side engine: the eager sparse step against the parameter servers (duck-types
     rocfm.models.torch_engine.TorchDeepFM for the Estimator)."""
@@ -401,14 +428,19 @@ def run_job(cfg, task_fn=None) -> dict:
             est = Estimator(cfg, device=device, rank_info=info)  # restores model_dir into the PS
             rpc.rpc_sync(ps_name(0), _set_ready)
         else:
-            while not rpc.rpc_sync(ps_name(0), _is_ready):
-                time.sleep(0.05)
+            _wait_ps0(lambda: rpc.rpc_sync(ps_name(0), _is_ready), "the chief's restore", cfg.dist_timeout_s)
             est = Estimator(cfg, device=device, rank_info=info, restore=False)
         out = (task_fn or _default_task)(est, w, nw)
         est.eng.flush()
         est.close()
         out["role"] = worker_name(w)
         return out
+    except BaseException:
+        try:  # tell ps0, so the chief / the other workers stop waiting for this one
+            rpc.rpc_sync(ps_name(0), _worker_failed)
+        except Exception:  # noqa: BLE001 — ps0 itself may be gone
+            pass
+        raise
     finally:
         rpc.shutdown()
 
@@ -432,8 +464,8 @@ def _default_task(est, w: int, nw: int) -> dict:
 
         rpc.rpc_sync(ps_name(0), _worker_done)
         if w == 0:  # the final checkpoint holds every worker's updates; evaluation reads all files
-            while rpc.rpc_sync(ps_name(0), _done_count) < nw:
-                time.sleep(0.05)
+            _wait_ps0(lambda: rpc.rpc_sync(ps_name(0), _done_count) >= nw, "every worker to finish training",
+                      cfg.dist_timeout_s)
             est.info = RankInfo(rank=0, world=1)
             if va_files:
                 out["eval"] = est.evaluate(va_files)

@@ -235,3 +235,83 @@ class HipProxy:
             return attr(*args, **kwargs)
 
         return call
+
+
+# ---- three-stream plan of the streamed training loop ---------------------------------------------
+class StreamPlan:
+    """Happens-before checker over the operations of ``FusedDeepFM.train_stream`` on its three
+    streams: the copy stream (H2D copies of host batches / raw payloads + the device Example parser
+    writing the HBM batch ring), the side stream (each multi-step graph's fetch + sort of the NEXT
+    graph's batches — the ring's readers) and the compute stream (the prime, the main graphs).
+
+    The loop records every ``Event.record`` / ``wait_event`` it issues here (``record`` returns a
+    token, ``wait`` queues it for the stream's next operation) and every operation with the ring
+    slots (or other named ranges) it reads and writes.  Operations on one stream are ordered; across
+    streams only through the recorded waits (transitively).  ``check`` raises HazardError for two
+    unordered operations whose ranges overlap with at least one write — e.g. a copy that refills a
+    ring slot a side graph may still be reading (the event plan's ``copy.wait_event(sevs[j - 3])``).
+    """
+
+    def __init__(self):
+        self.ops: List[Tuple[str, str, List[Tuple[str, int, int, bool]], int]] = []  # stream, label, ranges, deps
+        self._last: Dict[str, int] = {}
+        self._waits: Dict[str, int] = defaultdict(int)  # stream → bitmask of ops its next op waits for
+
+    def record(self, stream: str) -> int:
+        """Token of everything issued on ``stream`` so far (an event recorded there)."""
+        i = self._last.get(stream)
+        return 0 if i is None else (1 << i)
+
+    def wait(self, stream: str, token: Optional[int]) -> None:
+        if token:
+            self._waits[stream] |= token
+
+    def wait_stream(self, stream: str, other: str) -> None:
+        self.wait(stream, self.record(other))
+
+    def op(self, stream: str, label: str, ranges=()) -> int:
+        """One operation on ``stream``; ``ranges`` = [(name, lo, hi, write)] (half-open)."""
+        deps = self._waits.pop(stream, 0)
+        if stream in self._last:
+            deps |= 1 << self._last[stream]
+        i = len(self.ops)
+        self.ops.append((stream, label, list(ranges), deps))
+        self._last[stream] = i
+        return i
+
+    def conflicts(self) -> List[Tuple[str, str, str]]:
+        # transitive happens-before: hb[i] = bitmask of every op ordered before op i
+        hb: List[int] = []
+        for _, _, _, deps in self.ops:
+            m = deps
+            d = deps
+            while d:
+                j = (d & -d).bit_length() - 1
+                m |= hb[j]
+                d &= d - 1
+            hb.append(m)
+        out = []
+        by_name: Dict[str, List[Tuple[int, int, int, bool]]] = defaultdict(list)
+        for i, (_, _, ranges, _) in enumerate(self.ops):
+            for name, lo, hi, w in ranges:
+                by_name[name].append((i, lo, hi, w))
+        for name, acc in by_name.items():
+            for a in range(len(acc)):
+                i, lo, hi, w = acc[a]
+                for b in range(a + 1, len(acc)):
+                    j, lo2, hi2, w2 = acc[b]
+                    if i == j or not (w or w2) or not (lo < hi2 and lo2 < hi):
+                        continue
+                    if self.ops[i][0] == self.ops[j][0]:
+                        continue  # same stream: ordered
+                    x, y = (i, j) if i < j else (j, i)
+                    if not (hb[y] >> x) & 1:
+                        out.append((name, f"{self.ops[x][0]}:{self.ops[x][1]}", f"{self.ops[y][0]}:{self.ops[y][1]}"))
+        return out
+
+    def check(self, tag: str = "") -> None:
+        found = self.conflicts()
+        if found:
+            lines = [f"  {n}: {a}  <->  {b}" for n, a, b in found[:20]]
+            raise HazardError(f"stream-plan hazard{(' in ' + tag) if tag else ''}: {len(found)} unordered "
+                              "overlapping accesses with a write:\n" + "\n".join(lines))

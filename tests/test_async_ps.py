@@ -137,3 +137,45 @@ def test_cli_async_ps_job(tmp_path):
     assert ckpt.checkpoint_step(prefix) == 2 * (640 // 64)  # both workers' steps: one shared global step
     sd = ckpt.load_checkpoint(prefix)
     assert int(sd["global_step"]) == 20
+
+
+def _fail_job(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    torch.set_num_threads(1)
+    from torch.distributed import rpc
+
+    from rocfm.config import parse_flags
+    from rocfm.parallel import async_ps as A
+
+    cfg = parse_flags(["--feature_size", "3000", "--field_size", "39", "--embedding_size", "8", "--deep_layers",
+                       "32,16", "--dropout", "1.0,1.0", "--batch_size", "64", "--parallelism", "async_ps", "--num_ps", "1",
+                       "--dist_timeout_s", "120", "--log_steps", "0"])
+
+    def task(est, w, nw):
+        if w == 1:
+            raise ValueError("injected worker failure")
+        A._wait_ps0(lambda: rpc.rpc_sync(A.ps_name(0), A._done_count) >= nw, "the workers", cfg.dist_timeout_s)
+        return {}
+
+    try:
+        A.run_job(cfg, task_fn=task)
+        res = "ok"
+    except BaseException as e:  # noqa: BLE001
+        res = f"{type(e).__name__}: {e}"
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(res)
+
+
+def test_a_failing_worker_fails_the_chief_instead_of_hanging(tmp_path):
+    """A worker that raises reports to ps0; the chief's wait for every worker raises (well within
+    dist_timeout_s) instead of spinning forever, and the failing worker's error propagates."""
+    import time
+
+    t0 = time.time()
+    mp.start_processes(_fail_job, args=(3, _port(), str(tmp_path)), nprocs=3, join=True, start_method="spawn")
+    assert time.time() - t0 < 100
+    chief = open(tmp_path / "r1.txt").read()
+    worker = open(tmp_path / "r2.txt").read()
+    assert "a worker failed" in chief, chief
+    assert "injected worker failure" in worker, worker

@@ -194,3 +194,87 @@ def test_train_stream_raises_on_a_malformed_record(tmp_path):
     with pytest.raises(RuntimeError, match="batch 9 record 3.*id out of range"):
         eng.train_stream(ds.raw_groups(4, hold=2), 4, hold=2)
         torch.cuda.synchronize()
+
+
+def test_malformed_record_never_trains(tmp_path):
+    """A malformed record halts every step the side chain prepares once the parser has flagged it
+    (optim.h kHaltStepBit): the engine ends bitwise equal to a clean run over the batches of the
+    graphs prepared before the flag — 4 or 8 steps here, by copy-stream timing — never past the
+    bad batch (index 9), and its optimizer slots did not move in the halted steps."""
+    from rocfm.models.deepfm import ModelSpec, init_params
+    from rocfm.models.fused import FusedDeepFM
+    from rocfm.optim import OptHParams
+
+    V, B, F, S = 5000, 64, 39, 4
+    rng = np.random.default_rng(3)
+    labels = rng.integers(0, 2, B * 20).astype(np.float32)
+    ids = rng.integers(0, V, (B * 20, F))
+    vals = rng.normal(size=(B * 20, F)).astype(np.float32)
+    clean = str(tmp_path / "clean.tfrecords")
+    T.write_tfrecord(clean, labels, ids, vals)
+    bad_ids = ids.copy()
+    bad_ids[B * 9 + 3, 7] = V + 5  # batch 9, record 3
+    bad = str(tmp_path / "bad.tfrecords")
+    T.write_tfrecord(bad, labels, bad_ids, vals)
+    spec = ModelSpec(V, F, 10, [64, 32], [0.5, 0.5], l2_reg=1e-4)
+
+    def engine():
+        return FusedDeepFM(spec, OptHParams(name="Adam", lr=1e-3), B, DEV, params=init_params(spec, 0))
+
+    def state(e):
+        return [e.emb.clone(), e.dense.clone()] + [s.clone() for s in e.emb_slots + e.dense_slots]
+
+    e = engine()
+    with pytest.raises(RuntimeError, match="batch 9 record 3.*id out of range"):
+        e.train_stream(T.TFRecordDataset([bad], F, B, V, num_threads=2).raw_groups(S, hold=2), S, hold=2)
+        torch.cuda.synchronize()
+        e.check()
+    torch.cuda.synchronize()
+    got = state(e)
+    matches = []
+    for n in (4, 8):
+        r = engine()
+        done = r.train_stream(T.TFRecordDataset([clean], F, B, V, num_threads=2).raw_groups(S, hold=2, limit=n), S,
+                              hold=2)
+        torch.cuda.synchronize()
+        assert done == n
+        matches.append(all(torch.equal(x, y) for x, y in zip(got, state(r))))
+    assert any(matches), "the engine state matches no clean prefix of the stream"
+
+
+def test_estimator_writes_no_checkpoint_after_a_malformed_record(tmp_path):
+    """save_checkpoints_steps=1 on a stream with a malformed record in batch 9: the job fails, and
+    no checkpoint at or past the bad batch's step exists (state_dict checks the parser first)."""
+    from rocfm import checkpoint as ckpt
+    from rocfm.config import parse_flags
+    from rocfm.estimator import Estimator
+
+    V, B, F = 5000, 64, 39
+    rng = np.random.default_rng(4)
+    d = tmp_path / "data"
+    d.mkdir()
+    ids = rng.integers(0, V, (B * 24, F))
+    ids[B * 9 + 3, 7] = V + 5
+    T.write_tfrecord(str(d / "tr.tfrecords"), rng.integers(0, 2, B * 24).astype(np.float32), ids,
+                     rng.normal(size=(B * 24, F)).astype(np.float32))
+    md = str(tmp_path / "m")
+    cfg = parse_flags(["--feature_size", str(V), "--field_size", str(F), "--embedding_size", "10",
+                       "--deep_layers", "64,32", "--dropout", "1.0,1.0", "--batch_size", str(B), "--training_data_dir", str(d),
+                       "--model_dir", md, "--engine", "fused", "--save_checkpoints_steps", "1",
+                       "--save_checkpoints_secs", "0", "--keep_checkpoint_max", "100", "--log_steps", "0"])
+    est = Estimator(cfg)
+    with pytest.raises(RuntimeError, match="id out of range"):
+        est.train([str(d / "tr.tfrecords")], num_epochs=1)
+    prefix = ckpt.latest_checkpoint(md)
+    assert prefix is None or ckpt.checkpoint_step(prefix) <= 9, prefix
+
+
+def test_decode_lds_gate():
+    """The parser's LDS stage fits every schema up to 192 fields on gfx950 (160 KiB opt-in); wider
+    ones are refused before any launch (the Estimator then parses on the host)."""
+    from rocfm.ops import hip
+
+    H = hip()
+    assert H.decode_fits(39) and H.decode_fits(192)
+    assert not H.decode_fits(193) and not H.decode_fits(0)
+    assert H.decode_lds_bytes(192) <= 160 * 1024

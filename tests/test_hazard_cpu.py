@@ -120,3 +120,86 @@ def test_proxy_notes_calls_and_passes_classes():
     r.begin("main")
     assert px.launch(1, 2) == 3
     assert r.calls["main"] == [("launch", (1, 2))]
+
+
+# ---- the streamed loop's three-stream plan (StreamPlan) ------------------------------------------
+def test_stream_plan_orders_through_waits_transitively():
+    from rocfm.utils.hazard import HazardError, StreamPlan
+
+    p = StreamPlan()
+    p.op("copy", "fill slot 0", [("ring", 0, 1, True)])
+    t = p.record("copy")
+    p.op("side", "unrelated")
+    p.wait("side", t)
+    p.op("side", "read slot 0", [("ring", 0, 1, False)])
+    t2 = p.record("side")
+    p.wait("main", t2)
+    p.op("main", "m")
+    p.wait("copy", p.record("main"))
+    p.op("copy", "refill slot 0", [("ring", 0, 1, True)])  # ordered after the read via main
+    assert p.conflicts() == []
+    p.check()
+    q = StreamPlan()
+    q.op("copy", "fill", [("ring", 2, 4, True)])
+    q.op("side", "read", [("ring", 3, 5, False)])  # no wait: unordered overlap
+    q.op("main", "read elsewhere", [("ring", 4, 5, False)])
+    found = q.conflicts()
+    assert found == [("ring", "copy:fill", "side:read")]
+    with pytest.raises(HazardError, match="copy:fill"):
+        q.check("t")
+
+
+def _simulate_train_stream(S: int, graphs: int, early: bool):
+    """The event plan of FusedDeepFM.train_stream / _launch_multi on a 4·S-slot ring, in plan ops."""
+    from rocfm.utils.hazard import StreamPlan
+
+    R = 4 * S
+    p = StreamPlan()
+    staged = 0
+
+    def stage(k):
+        nonlocal staged
+        p.op("copy", f"stage {staged}", [("ring", staged % R, staged % R + k, True)])
+        staged += k
+        return p.record("copy")
+
+    cevs = [stage(2 * S)]
+    p.wait("main", cevs[0])
+    p.op("main", "prime", [("ring", 0, S, False), ("m_batches", 0, 1, True)])
+    prime = p.record("main")
+    sevs, side_ev, i = [], None, 0
+    for j in range(graphs):
+        w = sevs[j - 3] if j >= 3 else prime
+        if early and j >= 3:
+            w = sevs[j - 4] if j >= 4 else prime
+        p.wait("copy", w)
+        cevs.append(stage(S))
+        p.wait("side", cevs[j])
+        q = j % 2
+        before = p.record("main")
+        p.wait("main", side_ev)
+        p.op("main", f"main {j}", [("m_batches", q, q + 1, False)])
+        p.wait("side", before)
+        lo = (i + S) % R
+        p.op("side", f"side {j}", [("ring", lo, lo + S, False), ("m_batches", 1 - q, 2 - q, True)])
+        side_ev = p.record("side")
+        sevs.append(side_ev)
+        i += S
+    return p
+
+
+def test_train_stream_event_plan_is_race_free_and_an_early_refill_is_caught():
+    """The loop's plan (copy refills wait for the side graph three back) has no unordered access;
+    waiting one side graph too early lets a refill overwrite ring slots a side graph may still be
+    reading — the checker names both operations."""
+    from rocfm.utils.hazard import HazardError
+
+    for S in (2, 4, 16):
+        _simulate_train_stream(S, 12, early=False).check()
+    bad = _simulate_train_stream(4, 12, early=True)
+    found = bad.conflicts()
+    assert found and all(n == "ring" for n, _, _ in found)
+    assert any(a.startswith("copy:stage") and b.startswith("side:side") or
+               b.startswith("copy:stage") and a.startswith("side:side") for _, a, b in found)
+    with pytest.raises(HazardError):
+        bad.check()

@@ -83,3 +83,35 @@ def test_injected_shared_write_is_caught(monkeypatch):
     with pytest.raises(HazardError, match=r"injected_write\.arg0 W eng\.m_pos\+0 +<->  deepfm_rows\.contrib_pos R"):
         drv.train_steps(8, 4)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_train_stream_three_stream_plan(raw, monkeypatch, tmp_path):
+    """The streamed loop's copy (H2D + device parse into the HBM ring), side (fetch + sort of the
+    next graph's batches) and main streams, checked for unordered overlapping accesses after every
+    graph (utils/hazard.py StreamPlan); a refill that waits one side graph too early
+    (ROCFM_HAZARD_INJECT=ring) is caught."""
+    from rocfm.data import tfrecord as T
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.models.deepfm import init_params
+    from rocfm.models.fused import FusedDeepFM
+    from rocfm.utils.hazard import HazardError
+
+    monkeypatch.setenv("ROCFM_HAZARD", "1")
+    f = str(tmp_path / "tr.tfrecords")
+    write_synthetic_tfrecord(f, 128 * 40, 4001, 39, seed=2)
+    spec, hp = _cfg("Adam")
+
+    def run():
+        e = FusedDeepFM(spec, hp, 128, torch.device("cuda"), params=init_params(spec, 3))
+        ds = T.TFRecordDataset([f], 39, 128, 4001, num_threads=2)
+        src = ds.raw_groups(4, hold=2) if raw else ds.groups(4, hold=2)
+        n = e.train_stream(src, 4, hold=2)
+        torch.cuda.synchronize()
+        return n
+
+    assert run() == 40
+    monkeypatch.setenv("ROCFM_HAZARD_INJECT", "ring")
+    with pytest.raises(HazardError, match="ring"):
+        run()
+    torch.cuda.synchronize()

@@ -227,3 +227,12 @@ def test_step_tail_wgrad_plan_fits_one_dispatch_round():
     assert n + emb(39) <= 256 and tw[0] >= 2, (n, tw)
     n0, tw = H.wgrad_plan([1248, 256, 128, 64], 1024, -1, 256)  # standalone launch: plain tiles
     assert tw == [1, 1, 1] and n0 == 39 * 8 + 8 * 4 + 4 * 2 + (256 + 128 + 64) // 32 + 1
+    # ROCFM_WGRAD_TW=auto widens exactly as the unset variable does (it used to read as "force 0",
+    # i.e. plain tiles); 2 / 4 force a width
+    try:
+        os.environ["ROCFM_WGRAD_TW"] = "auto"
+        assert H.wgrad_plan([1248, 256, 128, 64], 1024, emb(39), 256)[1] == [4, 4, 2]
+        os.environ["ROCFM_WGRAD_TW"] = "2"
+        assert H.wgrad_plan([1248, 256, 128, 64], 1024, emb(39), 256)[1] == [2, 2, 2]
+    finally:
+        os.environ.pop("ROCFM_WGRAD_TW", None)

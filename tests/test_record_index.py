@@ -126,3 +126,35 @@ def test_raw_mode_rejects_skip_bad_and_stream(tmp_path):
         next(iter(T.TFRecordDataset(files, 39, 64, skip_bad=True, pin_memory=False).raw_groups(4)))
     with pytest.raises(ValueError):
         next(iter(T.TFRecordDataset(files, 39, 64, stream_mode=True, pin_memory=False).raw_groups(4)))
+
+
+def test_rewritten_file_with_a_stale_index_fails_loudly_without_crc_checks(tmp_path):
+    """A file rewritten in place with the same size and mtime keeps a sidecar index whose interior
+    offsets are wrong (only the size, the mtime and both framing ends are checked on load); with
+    verify_crc off the loader still checks every frame's length CRC, so it raises instead of
+    decoding garbage."""
+    import shutil
+
+    f = str(tmp_path / "tr.tfrecords")
+    small = np.arange(1, 40).reshape(1, 39)           # 1-byte varints
+    large = np.arange(200, 239).reshape(1, 39)        # 2-byte varints
+    vals = np.ones((1, 39), np.float32)
+    lab = np.zeros(1, np.float32)
+
+    def write(order):
+        for i, ids in enumerate(order):
+            T.write_tfrecord(f, lab, ids, vals, append=i > 0)
+
+    write([small, large, small])
+    assert io().build_index(f, True) == 3
+    st = os.stat(f)
+    shutil.copy(f + ".rfidx", str(tmp_path / "old.rfidx"))
+    size = os.path.getsize(f)
+    write([large, small, small])  # same size, the second frame starts elsewhere
+    assert os.path.getsize(f) == size
+    shutil.copy(str(tmp_path / "old.rfidx"), f + ".rfidx")
+    os.utime(f, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert io().index_info(f) is not None  # the stale sidecar still passes the load checks
+    ds = T.TFRecordDataset([f], 39, 1, 50000, num_threads=1, pin_memory=False, verify_crc=False)
+    with pytest.raises(RuntimeError, match="TFRecord"):
+        list(ds)

@@ -119,3 +119,58 @@ def test_engine_bitwise_equal_across_sort_libraries(monkeypatch):
     for key, sd in out.items():
         for name, v in ref.items():
             assert torch.equal(sd[name], v), f"{key} {name}"
+
+
+@pytest.mark.parametrize("V,S", [(100_000_000, 16), (100_000_000, 64), (1_000_000_000, 64)])
+def test_wide_vocabulary_streams_through_seg_sort(V, S, tmp_path):
+    """100M- and 1B-row vocabularies through the streamed multi-step graphs: the side chain sorts
+    every batch on its own 27-30 id bits (seg_sort.hip; plain per-batch keys where S << id_bits no
+    longer fits 32 bits — no 64-bit keys, no rocPRIM) and the result is bitwise equal to per-step
+    launches (one single-segment sort per step) — table rows and Adam slots of every touched id,
+    and every dense parameter and slot."""
+    import gc
+
+    from rocfm.data import tfrecord as T
+    from rocfm.data.synthetic import write_synthetic_tfrecord
+    from rocfm.models.deepfm import ModelSpec
+    from rocfm.models.fused import FusedDeepFM, sort_lib
+    from rocfm.optim import OptHParams
+
+    assert sort_lib() == "rocfm"
+    B, F, n = 256, 39, S + 9  # a full graph and a 9-step remainder graph
+    f = str(tmp_path / "tr.tfrecords")
+    write_synthetic_tfrecord(f, B * n, V, F, seed=4)
+    spec = ModelSpec(V, F, 10, [128, 64, 32], [0.5, 0.5, 0.5], l2_reg=1e-4)
+    hp = OptHParams(name="Adam", lr=1e-3)
+    dev = torch.device("cuda")
+    host = [tuple(x.clone() for x in g) for g in T.TFRecordDataset([f], F, B, V, num_threads=2).groups(8, hold=2)]
+    ids = torch.cat([g[0] for g in host]).to(dev)
+    vals = torch.cat([g[1] for g in host]).to(dev)
+    labels = torch.cat([g[2] for g in host]).to(dev)
+    assert ids.shape[0] == n
+    touched = torch.unique(ids.reshape(-1)).long()
+
+    def snapshot(e):
+        out = [e.emb[touched].cpu(), e.dense.cpu()]
+        out += [s[touched].cpu() for s in e.emb_slots] + [s.cpu() for s in e.dense_slots]
+        return out
+
+    res = []
+    for streamed in (True, False):
+        e = FusedDeepFM(spec, hp, B, dev, params=None, seed=7, use_graph=streamed)
+        if streamed:
+            got = e.train_stream(T.TFRecordDataset([f], F, B, V, num_threads=2).raw_groups(S, hold=2), S, hold=2)
+            assert got == n
+            assert e.m_plain == ((S << e.m_idbits) > (1 << 32)) and e.m_keys64 is None
+        else:
+            e.attach_pool(ids, vals, labels)
+            for _ in range(n):
+                e.train_step()
+        torch.cuda.synchronize()
+        e.check()
+        res.append(snapshot(e))
+        del e
+        gc.collect()
+        torch.cuda.empty_cache()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
