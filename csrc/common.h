@@ -132,6 +132,18 @@ __device__ __forceinline__ size_t frag_at(int nt, int u, int C, int lane) {
 }
 __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
 
+// MFMA-fragment-swizzled layout of the transposed activations / output gradients actT, dzT
+// ([feature c][batch b], features padded to 32, Bp % 16 == 0) that the weight-gradient tiles read
+// as 32x32x16 operands: the block (c / 32, b / 16) is 32 features × 16 batch rows = 512 elements
+// stored as 64 lanes × 8 in the order the operand wants them (lane l: feature 32·(c/32) + (l & 31),
+// batch rows 16·(b/16) + 8·(l >> 5) .. +7), so every fragment load of a wave is ONE contiguous 1 KiB
+// read (the row-major [c][b] layout cost 32 strided 32-B pieces per load).  Any 8 batch rows b..b+7
+// with b % 8 == 0 of one feature stay contiguous (the row kernel's 8-B / 16-B stores).
+__host__ __device__ __forceinline__ size_t act_swz(int c, int b, int Bp) {
+  return ((size_t)(c >> 5) * (size_t)(Bp >> 4) + (size_t)(b >> 4)) * 512 +
+         (size_t)(((c & 31) + 32 * ((b >> 3) & 1)) * 8 + (b & 7));
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)) and
 // leaves its global stores in flight (no vmcnt(0)), unlike __syncthreads().  Valid where no wave
 // reads, within the kernel, global memory another wave of the workgroup wrote (the fused kernels

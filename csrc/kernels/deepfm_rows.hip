@@ -10,7 +10,7 @@
 //   D  y_d = h_L·w_out + c_out, y = y_lin + y_d, p = σ(y), loss, g = dL/dy          (PS:248-276)
 //   E  backward data path through the MLP (dz_l = 1[h_l>0]/keep · dh_l, dh = dz·Wᵀ)
 //   F  FM backward: de = g·(S − e) + dh0, per-lookup gradient row [x·de | g·x]
-// It writes bf16 activations/dz transposed ([feature][batch]) for the weight-gradient kernel
+// It writes bf16 activations/dz transposed ([feature][batch], fragment-swizzled: common.h act_swz) for the weight-gradient kernel
 // (mlp_wgrad.hip) and the per-lookup gradient rows for the embedding update (emb_update.hip).
 // Nothing reduces across examples, so there are no atomics and no inter-workgroup hand-offs.
 //
@@ -527,13 +527,13 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           w[j] = (uint32_t)h0[(h * 8 + 2 * j) * lda + c] | ((uint32_t)h0[(h * 8 + 2 * j + 1) * lda + c] << 16);
-        *reinterpret_cast<uint4*>(p.actT[0] + (size_t)c * Bp + row0 + h * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+        *reinterpret_cast<uint4*>(p.actT[0] + act_swz(c, row0 + h * 8, Bp)) = make_uint4(w[0], w[1], w[2], w[3]);
       }
     } else {  // 4 rows × 1 column per item → one 8-B store
       for (int c = t; c < D0p; c += kRowThreads) {
         const uint32_t w0 = (uint32_t)h0[c] | ((uint32_t)h0[lda + c] << 16);
         const uint32_t w1 = (uint32_t)h0[2 * lda + c] | ((uint32_t)h0[3 * lda + c] << 16);
-        *reinterpret_cast<uint2*>(p.actT[0] + (size_t)c * Bp + row0) = make_uint2(w0, w1);
+        *reinterpret_cast<uint2*>(p.actT[0] + act_swz(c, row0, Bp)) = make_uint2(w0, w1);
       }
     }
   }
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         O[(rb + i) * ldo + c] = f2bf(a);
       }
       if (train && rb < RT)
-        *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + rb) =
+        *reinterpret_cast<uint2*>(p.actT[l + 1] + act_swz(c, row0 + rb, Bp)) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
      }
     }
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
             hv[i] = a;
             O[r * ldo + c] = f2bf(a);
           }
-          *reinterpret_cast<uint2*>(p.actT[l + 1] + (size_t)c * Bp + row0 + 4 * rg) =
+          *reinterpret_cast<uint2*>(p.actT[l + 1] + act_swz(c, row0 + 4 * rg, Bp)) =
               make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
         }
       }
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         v[i] = (rv > 0.f && row0 + r < p.B) ? dz : 0.f;
         dst[r * ldz + c] = f2bf(v[i]);
       }
-      *reinterpret_cast<uint2*>(p.dzT[l + 1] + (size_t)c * Bp + row0 + 4 * rg) =
+      *reinterpret_cast<uint2*>(p.dzT[l + 1] + act_swz(c, row0 + 4 * rg, Bp)) =
           make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     }
   };
@@ -914,7 +914,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         if (FP8 && a == 1) atomicMax(reinterpret_cast<unsigned*>(s_amax) + r, __float_as_uint(fabsf(bf2f(f2bf(v[i])))));
       }
       if (rg * 4 < RT)
-        *reinterpret_cast<uint2*>(p.dzT[a] + (size_t)c * Bp + row0 + rg * 4) =
+        *reinterpret_cast<uint2*>(p.dzT[a] + act_swz(c, row0 + rg * 4, Bp)) =
             make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     }
   }
@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
             }
           }
           if (rb < RT)
-            *reinterpret_cast<uint2*>(p.dzT[li] + (size_t)c * Bp + row0 + rb) =
+            *reinterpret_cast<uint2*>(p.dzT[li] + act_swz(c, row0 + rb, Bp)) =
                 make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         } else {
 #pragma unroll
@@ -1136,9 +1136,18 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if constexpr (!SH::kStatic || BN) {
     if (p.bn) bn_grid_exit(p);
   }
+  // diagnostics (ablate bit 3): one grid-wide barrier after the step's row work, as a persistent
+  // rows → tail kernel would need — its in-launch price against the kernel boundary it would replace
+  // (profiles/r5_persistent_step.md; p.bn_sync / bn_error set by tools/diag_phases.py)
+  if (DIAG && (ablate & 8) && p.bn_sync != nullptr) {
+    ROWS_STAMP(13);
+    bn_grid_sync(p, 0);
+    ROWS_STAMP(14);
+    bn_grid_exit(p);
+  }
   if (DIAG && p.stamps != nullptr) {
     lds_barrier();
-    if (t < 13) p.stamps[blockIdx.x * 16 + t] = s_stamp[t];
+    if (t < 15) p.stamps[blockIdx.x * 16 + t] = s_stamp[t];
   }
 }
 

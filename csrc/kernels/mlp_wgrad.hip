@@ -1,8 +1,9 @@
 // MLP weight gradients (+ fused optimizer) and dense-parameter maintenance kernels.
 //
 // dW_l = h_lᵀ · dz_{l+1} reduces over the batch, the one cross-example reduction of the MLP.
-// The row kernel (deepfm_rows.hip) leaves h and dz transposed ([feature][batch], bf16), so both
-// MFMA operands are 16-B contiguous per lane:
+// The row kernel (deepfm_rows.hip) leaves h and dz transposed ([feature][batch], bf16) in the
+// fragment-swizzled order of common.h act_swz, so every operand load of a wave is one contiguous
+// 1 KiB block:
 //   A[i][b] = actT[i][b], B[b][o] = dzT[o][b]  →  v_mfma_f32_32x32x16_bf16, f32 accumulate.
 // One workgroup owns one 32×32 tile of one layer's dW (no atomics, no split-K seam): its 4 waves
 // take a quarter of the batch each and combine through LDS; the tile's epilogue then applies the

@@ -94,8 +94,10 @@ __device__ __forceinline__ void wgrad_tile(const WgradParams& p, const OptStep& 
   const int ti = local / nto, to = local % nto;
   const int sub = wave % TW, part = wave / TW;
   const int oc = (to * TW + sub) * 32;  // this wave's 32 output columns
-  const uint16_t* A = p.actT[li] + (size_t)(ti * 32 + (lane & 31)) * Bp + 8 * (lane >> 5);
-  const uint16_t* Bm = p.dzT[li + 1] + (size_t)(oc + (lane & 31)) * Bp + 8 * (lane >> 5);
+  // fragment-swizzled operands (common.h act_swz): the k-step at batch b is the contiguous 1 KiB
+  // block (tile, b / 16), lane l's 8 elements at 8·l — one coalesced read per wave
+  const uint16_t* A = p.actT[li] + act_swz(ti * 32, 0, Bp) + 8 * lane;
+  const uint16_t* Bm = p.dzT[li + 1] + act_swz(oc, 0, Bp) + 8 * lane;
   const int q = Bp * TW / 8;  // batch share per wave (Bp % 128 == 0 → a multiple of 16)
   f32x16 acc = {};
   const int bs = part * q, be = bs + q;
@@ -105,8 +107,8 @@ __device__ __forceinline__ void wgrad_tile(const WgradParams& p, const OptStep& 
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int b = max(bs, min(b0 + 16 * u, be - 16));
-      fa[u] = *reinterpret_cast<const bf16x8*>(A + b);
-      fb[u] = *reinterpret_cast<const bf16x8*>(Bm + b);
+      fa[u] = *reinterpret_cast<const bf16x8*>(A + (size_t)b * 32);  // block b / 16 = 512 elements
+      fb[u] = *reinterpret_cast<const bf16x8*>(Bm + (size_t)b * 32);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -154,14 +156,8 @@ __device__ __forceinline__ void wgrad_tile(const WgradParams& p, const OptStep& 
     p.params[idx[e]] = w[e];
     if (p.s0) p.s0[idx[e]] = a[e];
     if (p.s1) p.s1[idx[e]] = b[e];
-    const uint16_t hw = f2bf(w[e]);
-    p.Wb[li][(size_t)ii[e] * Dout + oo[e]] = hw;  // 64-B runs along o
-    if (p.WTs[li]) {
-      p.WTs[li][frag_swz(oo[e], ii[e], Din)] = hw;
-      p.Wbs[li][frag_swz(ii[e], oo[e], Dout)] = hw;
-    }
     const int el = t + kWgThreads * e;
-    s_T[(el >> 10) * (32 * 34) + (oo[e] & 31) * 34 + (ii[e] & 31)] = hw;
+    s_T[(el >> 10) * (32 * 34) + (oo[e] & 31) * 34 + (ii[e] & 31)] = f2bf(w[e]);
   }
   const bool q8 = li == 0 && p.w8.f;
   if (q8) {
@@ -178,12 +174,38 @@ __device__ __forceinline__ void wgrad_tile(const WgradParams& p, const OptStep& 
     for (int ww = 0; ww < kWgThreads / 64; ++ww) m = fmaxf(m, s_m8[ww]);
     atomicMax(reinterpret_cast<unsigned*>(p.w8.amax + (((p.step ? *p.step : 0) + 1) & 1)), __float_as_uint(m));
   }
+  // the bf16 weight copies of the refreshed tile, from the LDS tile T[o][i] (stride 34): every store
+  // is a coalesced 4-B (row-major copies, 64-B runs) or 16-B (swizzled copies: a 32×32 tile is two
+  // contiguous 1 KiB fragment blocks in each) piece — per-element 2-B stores cost an epilogue ∝ TW
 #pragma unroll
-  for (int s = 0; s < TW; ++s) {  // Wᵀ rows (o-major) written 4 B per thread, 64-B runs along i
-    const int o = t >> 4, ip = (t & 15) * 2;
+  for (int s = 0; s < TW; ++s) {
     const uint16_t* T = s_T + s * (32 * 34);
-    const uint32_t v2 = (uint32_t)T[o * 34 + ip] | ((uint32_t)T[o * 34 + ip + 1] << 16);
-    *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)((to * TW + s) * 32 + o) * Din + ti * 32 + ip) = v2;
+    const int o0 = (to * TW + s) * 32, i0 = ti * 32;
+    {  // Wᵀ rows (o-major) and W rows (i-major), 4 B per thread
+      const int r = t >> 4, cp = (t & 15) * 2;
+      const uint32_t wt = (uint32_t)T[r * 34 + cp] | ((uint32_t)T[r * 34 + cp + 1] << 16);
+      *reinterpret_cast<uint32_t*>(p.WT[li] + (size_t)(o0 + r) * Din + i0 + cp) = wt;
+      const uint32_t wb = (uint32_t)T[cp * 34 + r] | ((uint32_t)T[(cp + 1) * 34 + r] << 16);
+      *reinterpret_cast<uint32_t*>(p.Wb[li] + (size_t)(i0 + r) * Dout + o0 + cp) = wb;
+    }
+    if (p.WTs[li] && t < 256) {  // frag_swz copies: 2 blocks × 64 lanes × 8 elements each
+      const int ln = t & 63, blk = (t >> 6) & 1, which = t >> 7;  // which 0: WTs, 1: Wbs
+      const int r16 = ln & 15, c8 = 8 * (ln >> 4);
+      uint32_t q[4];
+      if (which == 0) {  // WTs [Dout][Din]: row o = o0 + 16·blk + r16, columns i0 + c8 .. +7
+        const uint16_t* src = T + (16 * blk + r16) * 34 + c8;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = (uint32_t)src[2 * j] | ((uint32_t)src[2 * j + 1] << 16);
+        *reinterpret_cast<uint4*>(p.WTs[li] + frag_swz(o0 + 16 * blk + r16, i0 + c8, Din)) =
+            make_uint4(q[0], q[1], q[2], q[3]);
+      } else {  // Wbs [Din][Dout]: row i = i0 + 16·blk + r16, columns o0 + c8 .. +7
+        const int ir = 16 * blk + r16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          q[j] = (uint32_t)T[(c8 + 2 * j) * 34 + ir] | ((uint32_t)T[(c8 + 2 * j + 1) * 34 + ir] << 16);
+        *reinterpret_cast<uint4*>(p.Wbs[li] + frag_swz(i0 + ir, o0 + c8, Dout)) = make_uint4(q[0], q[1], q[2], q[3]);
+      }
+    }
   }
   ROCFM_STAMP(p.stamps, 2);
 }
@@ -223,12 +245,12 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
     while (lb >= p.bias_start[li + 1]) ++li;
     const int cb = lb - p.bias_start[li];
     const int o = cb * 32 + (t >> 4);
-    const uint16_t* row = p.dzT[li + 1] + (size_t)o * Bp;
+    const uint16_t* dz = p.dzT[li + 1];
     float s = 0.f;
     for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
       uint4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(dz + act_swz(o, min(b0 + 128 * u, Bp - 8), Bp));
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (b0 + 128 * u < Bp) s += sum_bf16x8(v[u]);
@@ -247,12 +269,11 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, const int bid) 
     if (push) push_wait_ready(p.push, push_seen);
     for (int c0 = 0; c0 < Dn; c0 += 32) {
       const int c = min(c0 + (t >> 4), Dn - 1);
-      const uint16_t* row = H + (size_t)c * Bp;
       float s = 0.f;
       for (int b0 = sub * 8; b0 < Bp; b0 += 128 * 8) {
         uint4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(row + min(b0 + 128 * u, Bp - 8));
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(H + act_swz(c, min(b0 + 128 * u, Bp - 8), Bp));
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           if (b0 + 128 * u < Bp) s += dot_bf16x8_f32(v[u], p.g + b0 + 128 * u);

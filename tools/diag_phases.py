@@ -59,8 +59,11 @@ def main():
         eng.wgrad_params[p].stamps = s_wg.data_ptr()
         eng.emb_params[p].stamps = s_emb.data_ptr()
     abl = int(os.environ.get("ABLATE", "0"))
+    sync = torch.zeros(4, dtype=torch.int32, device=dev)  # ABLATE bit 3: the grid barrier's counters
     for p in range(2):
         eng.rows_params[p].ablate = abl
+        if abl & 8:
+            eng.rows_params[p].bn_sync, eng.rows_params[p].bn_error = sync.data_ptr(), sync[2:].data_ptr()
     if multi:
         eng.train_steps(8, 4)  # builds the multi-step parameter blocks
         for q in range(2):
@@ -68,6 +71,8 @@ def main():
                 rows, wp, _, ep, _ = eng.m_params[q][k]
                 rows.stamps, wp.stamps, ep.stamps = s_rows.data_ptr(), s_wg.data_ptr(), s_emb.data_ptr()
                 rows.ablate = abl
+                if abl & 8:
+                    rows.bn_sync, rows.bn_error = sync.data_ptr(), sync[2:].data_ptr()
         eng._m_graphs = {}  # recapture with the stamp pointers
     for _ in range(3):
         s_rows.zero_(); s_wg.zero_(); s_emb.zero_()
@@ -80,6 +85,9 @@ def main():
     report("deepfm_rows", s_rows.view(-1, 16).cpu(), [0, 1, 2, 3, 4, 5, 9, 10, 11, 12],
            ["0 ids/vals stage", "A gather+e+h0", "B FM + h0T store", "C layer0 fwd", "C layer1 fwd",
             "C layer2 fwd", "D head + dz_L", "E backward (3 GEMMs)", "F FM bwd + contrib"])
+    if abl & 8:
+        report("deepfm_rows grid barrier (diagnostic)", s_rows.view(-1, 16).cpu(), [13, 14], ["grid barrier"])
+        print("   barrier timeouts:", int(sync[2].item()))
     wg = s_wg.view(-1, 16).cpu()
     report("mlp_wgrad (tile WGs)", wg[wg[:, 1] > 0], [0, 1, 2], ["MFMA + LDS reduce", "epilogue (opt+bf16)"])
     report("emb_rows_update", s_emb.view(-1, 16).cpu(), [0, 1, 2, 3, 4],
