@@ -105,8 +105,15 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const int c0 = bid * kE;
   if (c0 >= n) return;  // grid sized for p.n
   const int cend = min(c0 + kE, n);
-  const int i = c0 + t;
-  const bool live = t < kE && i < n;  // this thread holds one of the chunk's entries
+  // kSplit (the fused tail: 256 entries on 512 threads): both halves of the workgroup hold the
+  // chunk's 256 entries, each the float4 columns of its half of the row — half the row loads and
+  // half the segmented scan per thread (k = 32: 5 + 4 of 9 float4); heads are compacted by half 0
+  constexpr bool kSplit = 2 * kE == kChunk && KP4 >= 2;
+  constexpr int KH = kSplit ? (KP4 + 1) / 2 : KP4;  // float4 columns per thread in steps 1-2
+  const int te = kSplit ? t % kE : t, half = kSplit ? t / kE : 0;
+  const int i = c0 + te;
+  const bool live_e = te < kE && i < n;     // this thread's slot holds one of the chunk's entries
+  const bool live = live_e && half == 0;    // … and this thread represents it in the compaction
   const OptStep st = opt_step(p.opt, p.step ? *p.step : 0);
   const int ce_pre = (p.chunk_end != nullptr && t == 0) ? p.chunk_end[bid] : 0;  // issued with the keys
   // fused DP push (mode 2): the peers' "entered" flags, read with the keys, checked before the stores
@@ -128,8 +135,8 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   // 1. keys, run heads, and every entry's gradient row (one latency for the whole chunk)
   uint32_t key = 0xffffffffu, prevk = 0xffffffffu;
   bool head = false;
-  float4 v[KP4];
-  if (live) {
+  float4 v[KH];
+  if (live_e) {
     key = p.skeys[i];
     if (i > 0) prevk = p.skeys[i - 1];
     head = (i == 0) || (prevk != key);
@@ -137,23 +144,31 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)i * p.Kp)
                                          : contrib_row4(p, p.svals[i] - p.val_base);
 #pragma unroll
-    for (int u = 0; u < KP4; ++u) v[u] = skip ? make_float4(0.f, 0.f, 0.f, 0.f) : src[u];
+    for (int u = 0; u < KH; ++u) {
+      const int c = half * KH + u;
+      const float4 x = src[min(c, KP4 - 1)];
+      v[u] = (skip || c >= KP4) ? make_float4(0.f, 0.f, 0.f, 0.f) : x;
+    }
   } else {
 #pragma unroll
-    for (int u = 0; u < KP4; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < KH; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // 2. wave-level segmented inclusive scan (segments: runs, cut at wave boundaries)
   {
-    const unsigned long long hm = __ballot(head || lane == 0 || !live);
+    const unsigned long long hm = __ballot(head || lane == 0 || !live_e);
     const unsigned long long below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const int seg = 63 - __clzll(hm & below);
     seg_scan_dpp(v, lane, seg);
-    if (t < kE) {  // (wave-uniform: kE is a multiple of 64)
+    if (te < kE) {  // (wave-uniform: kE is a multiple of 64)
 #pragma unroll
-      for (int u = 0; u < KP4; ++u) s_rows[t * KP4 + u] = v[u];
+      for (int u = 0; u < KH; ++u) {
+        const int c = half * KH + u;
+        if (c < KP4) s_rows[te * KP4 + c] = v[u];
+      }
     }
   }
-  // 3. compact the heads in order
+  // 3. compact the heads in order (one representative thread per entry: half 0)
+  if (!live) head = false;
   const unsigned long long m = __ballot(head);
   const int before = __popcll(m & ((1ull << lane) - 1ull));
   if (lane == 0) s_wcnt[wave] = __popcll(m);

@@ -277,8 +277,12 @@ class FusedDeepFM:
         self.touched = (torch.zeros(self.V, dtype=torch.int32, device=dev) if embedding_update == "exact"
                         else None)
         self.dense_grads_flat = torch.zeros(L.total, dtype=torch.float32, device=dev)
-        self.sort_stream = torch.cuda.Stream(device=dev)
-        self.aux_stream = torch.cuda.Stream(device=dev)  # mlp_wgrad runs concurrently with the embedding update
+        # side (fetch + sort), aux (mlp_wgrad beside the embedding update) and copy (train_stream's
+        # H2D + device parse) streams: process-wide, so every engine gets the same hardware queues
+        # whatever ran before it (utils/streams.py)
+        from ..utils.streams import engine_streams
+
+        self.sort_stream, self.aux_stream, self._copy_stream = engine_streams(dev)
         # inference buffers (separate from the training slots)
         self.pred_ids = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
         self.pred_vals = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
@@ -1117,12 +1121,18 @@ class FusedDeepFM:
         R = max(4 * S + npre, (int(ring_batches) + S - 1) // S * S)
         hold = max(1, int(hold))
         dev = self.device
+        # ROCFM_HAZARD=1: every copy / side / main operation of this loop and its event waits go
+        # into a happens-before plan, checked after each graph launch (utils/hazard.py StreamPlan)
+        self._plan = hazard.StreamPlan() if self._hazard is not None else None
         ring = getattr(self, "_stream_ring", None)
         if ring is None or ring[0].shape[0] != R:
             ring = (torch.zeros(R, self.B, self.F, dtype=torch.int32, device=dev),
                     torch.zeros(R, self.B, self.F, dtype=torch.float32, device=dev),
                     torch.zeros(R, self.B, dtype=torch.float32, device=dev))
             self._stream_ring = ring
+            # the zero fill runs on the CURRENT stream, behind whatever is queued there (a 1B-row
+            # engine's table initialisation: seconds) — the copy stream below waits for it
+            self._pl_op("main", "ring allocation (zero fill)", [("ring", 0, R, True)])
         i0 = self._i
         # pool batch index of global step i = (start + i) % R  with start ≡ −(i0 − npre) (mod R) →
         # slot i − i0 + npre: the prefix (steps i0 − npre .. i0 − 1) in slots 0 .. npre − 1
@@ -1130,19 +1140,24 @@ class FusedDeepFM:
         if npre:
             for k in range(3):
                 ring[k][:npre].copy_(prefix[k])
+            self._pl_op("main", "prefix", self._pl_ring(0, npre, True, slot0=0))
         self._ring_mode_stream = True
-        copy = getattr(self, "_copy_stream", None) or torch.cuda.Stream(device=dev)
-        self._copy_stream = copy
+        copy = self._copy_stream
         it = iter(batches)
-        # ROCFM_HAZARD=1: every copy / side / main operation of this loop and its event waits go
-        # into a happens-before plan, checked after each graph launch (utils/hazard.py StreamPlan)
-        self._plan = hazard.StreamPlan() if self._hazard is not None else None
+        # every copy-stream write (H2D copies, the device parser into the ring) is ordered after all
+        # the work queued so far on the current stream: the ring's zero fill above, the engine's own
+        # initialisation, the prefix copies.  Without it the zero fill of a new ring could land
+        # AFTER the parser had written the first batches (seen at 1B rows, where the table's
+        # initialisation keeps the current stream busy for seconds: the whole stream trained on
+        # zeroed batches; tests/test_sort_gpu.py::test_wide_vocabulary_streams_through_seg_sort)
+        if os.environ.get("ROCFM_HAZARD_INJECT", "") != "ring_init":  # (hazard test: leave it out)
+            copy.wait_stream(torch.cuda.current_stream(dev))
+            if self._plan is not None:
+                self._plan.wait_stream("copy", "main")
         names = {}  # stream handle → plan stream name
         if self._plan is not None:
             names = {copy.cuda_stream: "copy", self.sort_stream.cuda_stream: "side",
                      torch.cuda.current_stream(dev).cuda_stream: "main"}
-            if npre:
-                self._pl_op("main", "prefix", self._pl_ring(0, npre, True, slot0=0))
 
         def mark(stream):
             e = torch.cuda.Event()

@@ -149,7 +149,7 @@ def test_stream_plan_orders_through_waits_transitively():
         q.check("t")
 
 
-def _simulate_train_stream(S: int, graphs: int, early: bool):
+def _simulate_train_stream(S: int, graphs: int, early: bool, skip_init_wait: bool = False):
     """The event plan of FusedDeepFM.train_stream / _launch_multi on a 4·S-slot ring, in plan ops."""
     from rocfm.utils.hazard import StreamPlan
 
@@ -163,6 +163,9 @@ def _simulate_train_stream(S: int, graphs: int, early: bool):
         staged += k
         return p.record("copy")
 
+    p.op("main", "ring allocation (zero fill)", [("ring", 0, R, True)])
+    if not skip_init_wait:
+        p.wait_stream("copy", "main")
     cevs = [stage(2 * S)]
     p.wait("main", cevs[0])
     p.op("main", "prime", [("ring", 0, S, False), ("m_batches", 0, 1, True)])
@@ -203,3 +206,6 @@ def test_train_stream_event_plan_is_race_free_and_an_early_refill_is_caught():
                b.startswith("copy:stage") and a.startswith("side:side") for _, a, b in found)
     with pytest.raises(HazardError):
         bad.check()
+    # the first refill racing the ring's zero fill on the compute stream (no copy.wait_stream(main))
+    found = _simulate_train_stream(4, 3, early=False, skip_init_wait=True).conflicts()
+    assert any("ring allocation" in a or "ring allocation" in b for _, a, b in found)

@@ -115,3 +115,8 @@ def test_train_stream_three_stream_plan(raw, monkeypatch, tmp_path):
     with pytest.raises(HazardError, match="ring"):
         run()
     torch.cuda.synchronize()
+    # the copy stream no longer waits for the ring's zero fill on the compute stream (the 1B-row race)
+    monkeypatch.setenv("ROCFM_HAZARD_INJECT", "ring_init")
+    with pytest.raises(HazardError, match="ring allocation"):
+        run()
+    torch.cuda.synchronize()
