@@ -558,7 +558,7 @@ def secondary_windows(a, spec, hp, params, dev, pool):
 
     out = {}
 
-    def tf_window():
+    def tf_window(prefix="tfrecord_"):
         # the loader-fed window: >= 2048 steps streamed from the TFRecord files (several epochs of a
         # 512-batch file set), warm-up with the same ring and graph set, so the window holds no
         # graph rebuild or capture; the time to the first graph is reported separately
@@ -570,12 +570,12 @@ def secondary_windows(a, spec, hp, params, dev, pool):
         ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(128, a.warmup), 32
         try:
             t = measure_tfrecord(ta, spec, hp, params, dev)
-            out["tfrecord_steps"] = ta.steps
+            out[prefix + "steps"] = ta.steps
             for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
                       "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode"):
-                out["tfrecord_" + ("examples_per_sec" if k == "value" else k)] = t.get(k)
+                out[prefix + ("examples_per_sec" if k == "value" else k)] = t.get(k)
         except Exception as e:  # a secondary window never costs the headline
-            out["tfrecord_error"] = f"{type(e).__name__}: {e}"[:400]
+            out[prefix + "error"] = f"{type(e).__name__}: {e}"[:400]
 
     # the TFRecord window runs first: after the other windows it measured 20 % slower than in a
     # process of its own (profiles/r4_radix_ab.md); ROCFM_BENCH_TF_FIRST=0 restores the old order
@@ -633,6 +633,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
     if not tf_first:
         tf_window()
     out.update(scale_windows(a, spec, hp, dev))
+    if os.environ.get("ROCFM_BENCH_TF_TWICE", "0") == "1":  # diagnostics: the same window again, last
+        tf_window("tfrecord_last_")
     return out
 
 

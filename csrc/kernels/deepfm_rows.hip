@@ -1303,8 +1303,12 @@ static void launch_rows_t(const RowsParams& p, hipStream_t stream) {
 // (profiles/r3_row_tile.md).  The runtime-shape kernel takes 16 or 8 (4 asks for 8 there), and 16
 // with batch norm (its statistics partials are per 16-row workgroup).
 constexpr int kDefaultRowTile = 8;
+// wide input layers (F·K ≥ 1024: the reference's k = 32 shapes, whose row phases are bound by
+// streaming the layer-0 weights through each CU): 4 examples per workgroup — 256 workgroups halve
+// the gather / FM / FM-backward work per CU at the same weight stream (k = 32: 57.4 → 56.3 and
+// 44.1 → 43.5 µs per step; k = 10 unchanged, profiles/r5_wgrad_swizzle.md)
 static int row_tile_for(const RowsParams& p, bool is_static_shape) {
-  const int rt = p.row_tile ? p.row_tile : kDefaultRowTile;
+  const int rt = p.row_tile ? p.row_tile : (is_static_shape && p.dims[0] >= 1024 ? 4 : kDefaultRowTile);
   if (p.bn) return kRowTile;  // batch-norm statistics partials are per 16-row workgroup
   if (is_static_shape) return rt;
   return rt == 4 ? 8 : rt;

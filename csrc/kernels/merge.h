@@ -128,6 +128,49 @@ struct HotApplyParams {
 void launch_merge_range_apply(const MergeParams& p, const DenseApplyParams* d, hipStream_t stream);
 int merge_range_lds_entries(int Kp);
 
+// ---- plan-ahead merge (merge_plan.hip) ------------------------------------------------------------
+// Side chain, per graph of S steps: this rank's unique ids per step (uniq_keys), then — after the
+// exchange of every rank's lists — the union of the W lists of each step with every id's position in
+// every rank's list (plan_build).  Main chain, per step: merge_plan_apply.
+struct PlanParams {
+  int S, W, cap;
+  // uniq_keys: this rank's sorted lookup keys [S][n] with their per-chunk run-head counts [S][nch]
+  const uint32_t* skeys;
+  const int32_t* chunk_heads;
+  int n, chunk, nch;
+  uint32_t* ukeys;          // step k's unique ids at ukeys + k·ukey_stride (ascending, ≤ cap)
+  long long ukey_stride;
+  int32_t* ucount;          // step k's count at ucount[k·ucount_stride]
+  long long ucount_stride;
+  int32_t* overflow;        // nullable sticky flag: more than cap unique ids
+  // plan_build: rank r's list of step k at gkeys + r·gk_stride + k·gkey_step, its count at
+  // gcounts + r·gc_stride + k·gcount_step (the gathered send buffers: gk_stride == gc_stride)
+  const uint32_t* gkeys;
+  const int32_t* gcounts;
+  long long gk_stride, gc_stride, gkey_step, gcount_step;
+  uint32_t pad_key;         // > every id (the vocabulary size): pads sort last
+  uint32_t* pkeys;          // [S][W·cap] sort input
+  uint32_t* skeys_sorted;   // [S][W·cap]
+  uint32_t* svals_sorted;   // [S][W·cap] global index k·W·cap + r·cap + j
+  int32_t* tile_counts;     // [S][⌈W·cap / 1024⌉]
+  uint32_t* plan_rows;      // [S][W·cap] union ids (ascending)
+  int32_t* plan_pos;        // [S][W·cap][W] position of the id in rank r's list, −1 if absent
+  int32_t* plan_count;      // [S] union sizes
+};
+struct PlanStep {            // one step's plan (the slices of PlanParams' outputs for step k)
+  const uint32_t* rows;
+  const int32_t* pos;
+  const int32_t* count;
+};
+void launch_uniq_keys(const PlanParams& p, hipStream_t stream);
+size_t plan_sort_temp_bytes(int S, int W, int cap, int bits);
+int plan_tile_ints(int S, int W, int cap);
+void launch_plan_build(const PlanParams& p, void* temp, size_t temp_bytes, int bits, hipStream_t stream);
+// the step's merge from its plan (the gathered rows: MergeParams rows / row_stride / Kp / W / cap;
+// the optimizer / dense-gradient outputs as in the other merges); d: the MLP optimizer as extra
+// workgroups (nullable)
+void launch_merge_plan_apply(const MergeParams& p, const PlanStep& ps, const DenseApplyParams* d, hipStream_t stream);
+
 // search mode; d (nullable): the MLP optimizer launched as extra workgroups; sv (nullable): a
 // row-shard serve (shard.h) as further workgroups; hot (nullable): the replicated rows' update
 struct ShardServeParams;

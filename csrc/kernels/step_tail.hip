@@ -71,8 +71,10 @@ void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
                 "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
   const int n_emb = e.n > 0 ? cdiv(e.n, tail_chunk_entries()) : 0;
-  const char* tw = std::getenv("ROCFM_WGRAD_TW");  // auto: widen to one dispatch round; 2|4: forced
-  const bool widen = tw && *tw && std::strcmp(tw, "1") != 0;
+  // widened weight-gradient tiles when the two roles exceed one dispatch round (wgrad_prepare;
+  // ROCFM_WGRAD_TW=1 keeps plain 32 × 32 tiles)
+  const char* tw = std::getenv("ROCFM_WGRAD_TW");
+  const bool widen = !(tw && std::strcmp(tw, "1") == 0);
   const int n_wg = wgrad_prepare(w, widen ? n_emb : -1, tail_cus());
   const dim3 grid(n_emb + n_wg), block(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots

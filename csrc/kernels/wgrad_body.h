@@ -3,6 +3,7 @@
 #include "deepfm_rows.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace rocfm {
 
@@ -389,8 +390,10 @@ inline int wgrad_prepare(WgradParams& p, int co_resident = -1, int max_wg = 256)
   };
   int n = fill();
   if (co_resident < 0) return n;
-  // A/B: ROCFM_WGRAD_TW=2|4 forces a width on every layer it divides; any other value (auto) widens
-  // automatically below
+  // ROCFM_WGRAD_TW: unset = widen automatically up to 32 × 64 tiles (the default: the reference's
+  // k = 32 shapes measured 57.4 → 55.0 µs and 44.1 → 43.3 µs per step with it, the 32 × 128 tiles
+  // of `auto` lost, profiles/r5_wgrad_swizzle.md); auto = up to 32 × 128; 2 | 4 = that width on
+  // every layer it divides
   const char* env = getenv("ROCFM_WGRAD_TW");
   const int forced = env ? atoi(env) : 0;
   if (forced == 2 || forced == 4) {
@@ -398,11 +401,12 @@ inline int wgrad_prepare(WgradParams& p, int co_resident = -1, int max_wg = 256)
       if (p.dims[l + 1] % (32 * forced) == 0) p.tw[l] = forced;
     return fill();
   }
+  const int tw_max = (env && std::strcmp(env, "auto") == 0) ? 4 : 2;
   while (n + co_resident > max_wg) {  // widen the layer with the most tiles that can still widen
     int best = -1, bt = 0;
     for (int l = 0; l < p.nl; ++l) {
       const int nt = p.tile_start[l + 1] - p.tile_start[l];
-      if (p.tw[l] < 4 && p.dims[l + 1] % (64 * p.tw[l]) == 0 && nt > bt) {
+      if (p.tw[l] < tw_max && p.dims[l + 1] % (64 * p.tw[l]) == 0 && nt > bt) {
         best = l;
         bt = nt;
       }

@@ -117,7 +117,8 @@ def main():
             k_, c_, r_, d_, sd_ = src
             p.keys, p.rows, p.counts = k_.data_ptr(), r_.data_ptr(), c_.data_ptr()
             dir_of = {"range": (d_.data_ptr(), nb + 1, nb, div), "search+dir": (sd_.data_ptr(), snb + 1, snb, sdiv)}
-            _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, sum(len(x) for x in lists))
+            _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, sum(len(x) for x in lists),
+                         plan_for(H, W, cap, k_, c_, Vk, dev, s))
             torch.cuda.synchronize()
             if raw is not None:
                 del src, k_, c_, r_, d_, sd_
@@ -137,8 +138,42 @@ def _uncached_view(ptr, shape, dtype, dev):
     return torch.as_tensor(raw, device=dev).view(*shape)
 
 
-def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live):
+def plan_for(H, W, cap, keys32, counts, Vk, dev, s):
+    """The plan-ahead merge's side-chain product for these W lists (merge_plan.hip plan_build, one
+    step): union ids + every id's position in every list.  Returns (PlanStep, build µs)."""
+    n = W * cap
+    i32 = dict(dtype=torch.int32, device=dev)
+    bufs = {k: torch.zeros(n, **i32) for k in ("pkeys", "sk", "sv", "rows")}
+    pos = torch.zeros(n * W, **i32)
+    cnt = torch.zeros(4, **i32)
+    tiles = torch.zeros(H.plan_tile_ints(1, W, cap), **i32)
+    bits = max(1, int(Vk).bit_length())  # the pad key Vk sorts after every id
+    temp = torch.zeros(max(16, H.plan_sort_temp_bytes(1, W, cap, bits)), dtype=torch.uint8, device=dev)
+    pp = H.PlanParams()
+    pp.S, pp.W, pp.cap = 1, W, cap
+    pp.gkeys, pp.gcounts = keys32.data_ptr(), counts.data_ptr()
+    pp.gk_stride, pp.gc_stride, pp.gkey_step, pp.gcount_step = cap, 1, 0, 0
+    pp.pad_key = Vk
+    pp.pkeys, pp.skeys_sorted, pp.svals_sorted = bufs["pkeys"].data_ptr(), bufs["sk"].data_ptr(), bufs["sv"].data_ptr()
+    pp.tile_counts, pp.plan_rows, pp.plan_pos, pp.plan_count = (tiles.data_ptr(), bufs["rows"].data_ptr(),
+                                                                pos.data_ptr(), cnt.data_ptr())
+    for _ in range(3):
+        H.plan_build(pp, temp.data_ptr(), temp.numel(), bits, s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        H.plan_build(pp, temp.data_ptr(), temp.numel(), bits, s)
+    e1.record()
+    torch.cuda.synchronize()
+    ps = H.PlanStep()
+    ps.rows, ps.pos, ps.count = bufs["rows"].data_ptr(), pos.data_ptr(), cnt.data_ptr()
+    return ps, e0.elapsed_time(e1) * 1000 / 20, (bufs, pos, cnt, tiles, temp)  # (keeps the buffers alive)
+
+
+def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live, plan=None):
     res = {}
+    if plan is not None:
+        names = names + ("plan",)
     for name in names:
         p.dirs, p.dir_stride, p.nb, p.bucket_div = dir_of.get(name, (0, 0, 0, 1))
 
@@ -147,6 +182,8 @@ def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live):
                 H.merge_search_apply(p, None, s)
             elif name == "range":
                 H.merge_range_apply(p, None, s)
+            elif name == "plan":
+                H.merge_plan_apply(p, plan[0], None, s)
             else:
                 H.merge_scatter(p, s)
                 H.merge_apply(p, s)
@@ -161,7 +198,9 @@ def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live):
         res[name] = e0.elapsed_time(e1) * 1000 / a.iters
     print(f"W={W} {mem} cap={cap} live rows={live} buckets={nb}: search {res['search']:.2f} us, "
           f"search+dir ({snb} buckets) {res['search+dir']:.2f} us, "
-          f"maps {res['maps']:.2f} us, range {res['range']:.2f} us", flush=True)
+          f"maps {res['maps']:.2f} us, range {res['range']:.2f} us"
+          + (f", plan apply {res['plan']:.2f} us (critical path; plan build {plan[1]:.2f} us on the side chain)"
+             if plan is not None else ""), flush=True)
     # the merges write the same dense gradient rows
     outs = []
     for name in names:
@@ -171,6 +210,8 @@ def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live):
             H.merge_search_apply(p, None, s)
         elif name == "range":
             H.merge_range_apply(p, None, s)
+        elif name == "plan":
+            H.merge_plan_apply(p, plan[0], None, s)
         else:
             H.merge_scatter(p, s)
             H.merge_apply(p, s)
