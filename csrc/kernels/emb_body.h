@@ -292,13 +292,28 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
     float4 w[4], a[4], b[4], g[4];
     uint32_t kk[4];
     size_t idx4[4];
+    // the table / slot loads of all 4 items depend only on the run's key: issued first (one LDS
+    // read each), the run's gradient pieces are summed out of LDS while they are in flight
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = min(base + u * kChunk + t, nitems - 1);
+      const int r = it / KP4, u4 = it - r * KP4;
+      kk[u] = s_hkey[r];
+      const bool skip = p.max_key && kk[u] >= p.max_key;
+      const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
+      idx4[u] = row * KP4 + u4;
+      if (p.mode == 0) {  // issue the row's parameter + slot loads now
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        w[u] = tbl_load4<BT>(p.emb, idx4[u]);
+        a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;
+        b[u] = p.s1 ? reinterpret_cast<const float4*>(p.s1)[idx4[u]] : z;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int it = min(base + u * kChunk + t, nitems - 1);
       const int r = it / KP4, u4 = it - r * KP4;
       const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
-      kk[u] = s_hkey[r];
-      const bool skip = p.max_key && kk[u] >= p.max_key;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
       for (int ww = w0; ww <= w1; ++ww) {
@@ -310,14 +325,6 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
         for (int ww = 0; ww < kWaves; ++ww) acc = f4add(acc, s_cont[ww * KP4 + u4]);
       }
       g[u] = make_float4(acc.x * p.grad_scale, acc.y * p.grad_scale, acc.z * p.grad_scale, acc.w * p.grad_scale);
-      const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
-      idx4[u] = row * KP4 + u4;
-      if (p.mode == 0) {  // issue the row's parameter + slot loads now
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        w[u] = tbl_load4<BT>(p.emb, idx4[u]);
-        a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;
-        b[u] = p.s1 ? reinterpret_cast<const float4*>(p.s1)[idx4[u]] : z;
-      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -138,6 +138,7 @@ struct PlanParams {
   const uint32_t* skeys;
   const int32_t* chunk_heads;
   int n, chunk, nch;
+  int id_shift;             // > 0: the sorted keys are composite (k << id_shift | id): ids = key − (k << id_shift)
   uint32_t* ukeys;          // step k's unique ids at ukeys + k·ukey_stride (ascending, ≤ cap)
   long long ukey_stride;
   int32_t* ucount;          // step k's count at ucount[k·ucount_stride]

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(1024) void uniq_keys_kernel(const PlanParams p) {
   for (int w = 0; w < wave; ++w) before += s_w[w];
   before += __popcll(m & ((1ull << lane) - 1ull));
   uint32_t* out = p.ukeys + (size_t)k * p.ukey_stride;
-  if (head && before < p.cap) out[before] = key;
+  if (head && before < p.cap) out[before] = p.id_shift > 0 ? key - ((uint32_t)k << p.id_shift) : key;
   if (c == p.nch - 1 && t == 0) {
     int tot = s_base;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_w[w];
@@ -145,6 +145,7 @@ template <int KP4, int WMAX>
 __device__ __forceinline__ void plan_apply_body(const MergeParams& p, const PlanStep& ps, const int u) {
   if (u >= *ps.count) return;
   const uint32_t row = ps.rows[u] / p.key_div;
+  if (row >= p.Vmap) return;  // (never: every plan id is a table row; a bad plan must not write past the table)
   const int32_t* pp = ps.pos + (size_t)u * p.W;
   const int W = p.W;
   const size_t base = (size_t)row * KP4;

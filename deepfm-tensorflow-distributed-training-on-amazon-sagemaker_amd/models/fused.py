@@ -1188,8 +1188,16 @@ class FusedDeepFM:
                         m = k - got
                         carry[0] = RawGroup(b.bytes[m:], b.offs[m:], n - m, b.B)
                         b, n = RawGroup(b.bytes[:m], b.offs[:m], m, b.B), m
+                    timing = getattr(self, "copy_timing", None)  # diagnostics (bench): H2D + parse time
+                    if timing is not None:
+                        t0 = torch.cuda.Event(enable_timing=True)
+                        t0.record(copy)
                     with torch.cuda.stream(copy):
                         self._stage_raw(b, staged % R, R, staged)
+                    if timing is not None:
+                        t1 = torch.cuda.Event(enable_timing=True)
+                        t1.record(copy)
+                        timing.append((t0, t1, int(b.used_bytes()), n))
                     self._pl_op("copy", f"raw stage of batches {staged}..{staged + n - 1}",
                                 self._pl_ring(0, n, True, slot0=staged % R) + [("raw_stage", 0, 1, True)])
                     pending.append((mark(copy), b))

@@ -108,6 +108,20 @@ def search_dir_buckets(W: int, V: int) -> int:
     return max(64, min(8192, V // 16))
 
 
+# The plan-ahead merge (merge_plan.hip) from this many ranks on: the union of the ranks' exported
+# ids and every id's position in every export are built on the side chain a graph ahead (the ids
+# exchanged there), so the step's merge is one plan-driven gather-sum (ROCFM_MERGE=plan forces it
+# from 2 ranks, any other forced merge keeps it off).  profiles/r5_dp_plan_merge.md.
+PLAN_MIN_W = 5
+
+
+def plan_merge_enabled(W: int, exchange: str) -> bool:
+    """By default with the p2p exchange (the ids ride a p2p exchange of their own); over RCCL (a
+    side-chain all-gather in a process group of its own) only when forced."""
+    m = os.environ.get("ROCFM_MERGE", "auto")
+    return W >= 2 and (m == "plan" or (m == "auto" and W >= PLAN_MIN_W and exchange == "p2p"))
+
+
 def range_merge_enabled(W: int) -> bool:
     """The range merge (bucket directories written by the sorted export; merge.hip range mode) for
     the multi-step DP path with ≥ 2 ranks — opt-in (ROCFM_MERGE=range).  Measured against the
@@ -645,11 +659,14 @@ class FusedDataParallel:
         self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
+        self.m_plan = self.mode == "dp" and e.Kp <= H.tail_max_kp() and plan_merge_enabled(self.world, self.exchange)
         self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and (self.world <= SEARCH_MAX_W or self.range
-                                                                            or self.sdir)
+                                                                            or self.sdir or self.m_plan)
         e._build_multi(Smax, heads=self.m_sorted)
         e._m_pool = e.pool_ids
         S_, n = e.mS, e.n_lookup
+        if self.m_plan:
+            self._build_plan(S_)
         self.m_dp = []
         for q in range(2):
             row = []
@@ -715,6 +732,10 @@ class FusedDataParallel:
                 H.merge_range_apply(mg, da, s)  # bucketed row merge ‖ MLP optimizer, one launch
                 if ed is not None:
                     H.emb_dense_update(ed, s)
+            elif self.mode == "dp" and self.m_plan:
+                H.merge_plan_apply(mg, self.plan_steps[q][k], da, s)  # plan-driven gather-sum ‖ MLP optimizer
+                if ed is not None:
+                    H.emb_dense_update(ed, s)
             elif self.mode == "dp" and self.m_sorted:
                 H.merge_search_apply(mg, da, s)  # row merge ‖ MLP optimizer, one launch
                 if ed is not None:
@@ -727,6 +748,92 @@ class FusedDataParallel:
             else:
                 H.dense_apply(da, s)
                 H.emb_dense_update(ed, s)
+
+    # ---- plan-ahead merge (merge_plan.hip) -------------------------------------------------------
+    def _build_plan(self, S: int) -> None:
+        """Buffers of the plan-ahead merge for S-step graphs, and its side-chain hook: after the
+        side chain has sorted the next graph's batches, this rank's unique ids of each batch (the
+        rows its sorted export will write, in that order) go to every rank; every rank then builds
+        the same plan — for each step, the union of the W ranks' ids and each id's position in
+        every rank's export.  Outputs by graph parity: the side graph of parity q fills 1-q."""
+        e, H = self.eng, self.eng.H
+        W, cap, dev = self.world, self.cap, self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        Sp = (S + 3) // 4 * 4
+        self.plan_S, self.plan_Sp = S, Sp
+        self.plan_slot = (Sp + S * cap + 3) // 4 * 4  # [S counts | pad | S lists of cap ids] (4-B words)
+        self.plan_send = torch.zeros(self.plan_slot, dtype=torch.float32, device=dev)
+        self.plan_ex = None
+        if self.exchange == "p2p":  # the ids ride a p2p exchange of their own (collective to open)
+            from .p2p import open_exchanges
+
+            if getattr(self, "_plan_ex_open", None) is None or self._plan_ex_open.slot < self.plan_slot:
+                if getattr(self, "_plan_ex_open", None) is not None:
+                    self._plan_ex_open.close()
+                exs = open_exchanges([self.plan_slot], dev, "p2p")
+                self._plan_ex_open = exs[0]
+            self.plan_ex = self._plan_ex_open
+            self.plan_recv_ptr = self.plan_ex.recv_ptr
+            self.plan_gstride = self.plan_ex.slot
+        else:  # RCCL: a group of its own, so the side chain's all-gather never interleaves with the step's
+            if getattr(self, "plan_group", None) is None:
+                self.plan_group = dist.new_group(list(range(W))) if dist.is_initialized() else None
+            self.plan_recv = torch.zeros(W * self.plan_slot, dtype=torch.float32, device=dev)
+            self.plan_recv_ptr = self.plan_recv.data_ptr()
+            self.plan_gstride = self.plan_slot
+        seg = W * cap
+        self.plan_scratch = [torch.zeros(S * seg, **i32) for _ in range(3)]  # sort input, sorted keys, values
+        self.plan_tiles = torch.zeros(H.plan_tile_ints(S, W, cap), **i32)
+        self.plan_bits = max(1, int(e.V).bit_length())  # the pad key V sorts after every id
+        self.plan_temp = torch.zeros(max(16, H.plan_sort_temp_bytes(S, W, cap, self.plan_bits)), dtype=torch.uint8,
+                                     device=dev)
+        self.plan_rows = torch.zeros(2, S * seg, **i32)
+        self.plan_pos = torch.zeros(2, S * seg * W, **i32)
+        self.plan_cnt = torch.zeros(2, Sp, **i32)
+        self.plan_steps = []
+        for q in range(2):
+            row = []
+            for k in range(S):
+                ps = H.PlanStep()
+                ps.rows = self.plan_rows[q, k * seg:].data_ptr()
+                ps.pos = self.plan_pos[q, k * seg * W:].data_ptr()
+                ps.count = self.plan_cnt[q, k:].data_ptr()
+                row.append(ps)
+            self.plan_steps.append(row)
+        e._m_post = self._plan_post
+
+    def _plan_post(self, qo: int, stream) -> None:
+        """Side chain (or the prime, on the main stream): the plan of the graph of parity qo."""
+        e, H = self.eng, self.eng.H
+        s = stream.cuda_stream
+        S, Sp, cap, W = self.plan_S, self.plan_Sp, self.cap, self.world
+        send = self.plan_send.data_ptr()
+        pp = H.PlanParams()
+        pp.S, pp.W, pp.cap = S, W, cap
+        pp.skeys, pp.chunk_heads = e.m_sk[qo].data_ptr(), e.m_chd[qo].data_ptr()
+        pp.n, pp.chunk, pp.nch = e.n_lookup, e.m_chunk, e.m_nch
+        pp.id_shift = e.m_idbits if e.m_composite else 0  # the export's ids: key − id_offset
+        pp.ukeys, pp.ukey_stride = send + 4 * Sp, cap
+        pp.ucount, pp.ucount_stride = send, 1
+        pp.overflow = self.overflow.data_ptr()
+        H.uniq_keys(pp, s)
+        if self.plan_ex is not None:
+            self.plan_ex.push(self.plan_ex.params(send, self.plan_slot), s)
+        elif dist.is_initialized() and (W > 1 or self.force):
+            with torch.cuda.stream(stream):
+                dist.all_gather_into_tensor(self.plan_recv, self.plan_send, group=self.plan_group)
+        else:
+            self.plan_recv[: self.plan_slot].copy_(self.plan_send)
+        r0 = self.plan_recv_ptr
+        pp.gkeys, pp.gcounts = r0 + 4 * Sp, r0
+        pp.gk_stride = pp.gc_stride = self.plan_gstride
+        pp.gkey_step, pp.gcount_step = cap, 1
+        pp.pad_key = e.V
+        pp.pkeys, pp.skeys_sorted, pp.svals_sorted = (t.data_ptr() for t in self.plan_scratch)
+        pp.tile_counts = self.plan_tiles.data_ptr()
+        pp.plan_rows, pp.plan_pos, pp.plan_count = (self.plan_rows[qo].data_ptr(), self.plan_pos[qo].data_ptr(),
+                                                    self.plan_cnt[qo].data_ptr())
+        H.plan_build(pp, self.plan_temp.data_ptr(), self.plan_temp.numel(), self.plan_bits, s)
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         e = self.eng
@@ -848,6 +955,10 @@ class FusedDataParallel:
         if self.p2p is not None:
             self.p2p.close()
             self.p2p = None
+        if getattr(self, "_plan_ex_open", None) is not None:
+            self._plan_ex_open.close()
+            self._plan_ex_open = None
+            self.plan_ex = None
 
     def check(self, replicas: bool = True) -> None:
         """Raise if a rank exported more unique rows than the exchange capacity (rows past the

@@ -189,8 +189,8 @@ def _check_dp_vs_single(tmp_path, world, mode, exchange, steps, spg, update, pus
 def test_fused_dp_world8_rehearsal(tmp_path):
     """Eight ranks on one GPU (the node's rank count): the push fans out to 7 peers (the copy push:
     eight ranks' spinning producers would compete for one GPU's CUs), the merge takes the
-    position-map path DP runs beyond SEARCH_DIR_MAX_W, multi-step graphs; ≡ the single-GPU union
-    batch, replicas bit-identical."""
+    plan-ahead path DP runs from PLAN_MIN_W ranks (the ids exchanged and the plan built on the side
+    chain), multi-step graphs; ≡ the single-GPU union batch, replicas bit-identical."""
     _check_dp_vs_single(tmp_path, 8, "dp", "p2p", 11, 4, "sparse", push="0")
 
 
@@ -209,6 +209,16 @@ def test_fused_dp_world4_hash_merge(tmp_path, monkeypatch, update):
     4 ranks, multi-step graphs and the p2p push ≡ the single-GPU union batch."""
     monkeypatch.setenv("ROCFM_MERGE", "hash")
     _check_dp_vs_single(tmp_path, 4, "dp", "p2p", 11, 4, update)
+
+
+@pytest.mark.parametrize("world,update", [(2, "sparse"), (4, "sparse"), (4, "exact")])
+def test_fused_dp_plan_merge(tmp_path, monkeypatch, world, update):
+    """The plan-ahead merge (ROCFM_MERGE=plan; the default from PLAN_MIN_W ranks): every rank's
+    unique ids of the next graph's batches go over a p2p exchange of their own on the side chain,
+    where every rank builds the union + positions plan; the step merges by the plan — multi-step
+    graphs ≡ the single-GPU union batch, replicas bit-identical."""
+    monkeypatch.setenv("ROCFM_MERGE", "plan")
+    _check_dp_vs_single(tmp_path, world, "dp", "p2p", 11, 4, update)
 
 
 @pytest.mark.parametrize("merge", ["direct", "hash"])
