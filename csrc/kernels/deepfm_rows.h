@@ -105,6 +105,15 @@ struct RowsParams {
   const int32_t* contrib_nxt;
   Fp8W0 w8;  // fp8 kernels: the pre-quantised input-layer weights (the kernel reads f, b, inv_scale
              // and, training, zeroes amax[(step + 1) & 1])
+  // row-tile split (deepfm_rows.hip CtShape G): `split` workgroups per row tile (0 / 1 = off; 2 for
+  // the training kernel of a wide input layer, bf16, no dedup — the launcher falls back to 1
+  // otherwise).  xbuf: [Bp / 8][dims[1]][16] bf16 exchange of layer 0's outputs; xctr: [Bp / 8]
+  // arrival counters, zeroed once at allocation and never reset; xerr: set if an exchange wait
+  // timed out (the host check raises; the counters must then be zeroed again).
+  int split;
+  uint16_t* xbuf;
+  unsigned* xctr;
+  int* xerr;
 };
 
 struct WgradParams {

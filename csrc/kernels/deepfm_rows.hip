@@ -122,6 +122,7 @@ __device__ __forceinline__ void rowtile_gemm(const uint16_t* A, int lda, const u
 // the whole grid is resident; every spin is bounded (1 s) and flags bn_error instead of hanging.
 constexpr uint64_t kBnSpinTicks = 100000000ull;  // s_memrealtime runs at 100 MHz
 typedef __attribute__((address_space(1))) unsigned bn_gu32;
+typedef __attribute__((address_space(1))) unsigned long long xg_u64;
 
 // Grid barrier k (0-based, in execution order) of this launch on one monotonic arrival counter:
 // every wave drains its stores, one lane per workgroup releases at agent scope (writes back this
@@ -173,6 +174,7 @@ struct RtShape {
   static constexpr int GU = 4;                 // gathered rows per thread per batch (phases A, F)
   static constexpr int KSF0E = 1, NJB0H = 1, NTF0 = 1, NTB1 = 1;
   static constexpr bool kLateBw0 = false, kWide = false;
+  static constexpr int G = 1, T0F = 0, FG = 0, T0B = 0;
   int F, K, nl, d[kMaxHidden + 1];
   __device__ explicit RtShape(const RowsParams& p) : F(p.F), K(p.K), nl(p.nl) {
 #pragma unroll
@@ -190,15 +192,25 @@ struct RtShape {
 // input layers, e.g. the notebook's 39×32 = 1248): the backward ones are then prefetched at the
 // last hidden layer's forward GEMM (under it, the head and the upper backward layers) instead of
 // before layer 0, and phase F re-gathers its rows after the layer-0 backward GEMM.
-template <int F_, int K_, int D1, int D2, int D3>
+// G_ > 1: the row-tile split — G_ workgroups share one row tile (profiles/r5_layer0_split.md).
+// Member m computes layer 0's forward tiles [m·T0F, (m+1)·T0F) and hands them to the others
+// through an in-launch exchange (RowsParams::xbuf / xctr), the layer-0 dgrad tiles of its fields
+// [m·FG, (m+1)·FG) and those fields' per-lookup gradient rows; everything else runs on every
+// member (its global stores on member 0 only), so each CU streams 1/G_ of W0 twice per step.
+template <int F_, int K_, int D1, int D2, int D3, int G_ = 1>
 struct CtShape {
   static constexpr bool kStatic = true;
   static constexpr int F = F_, K = K_;
   static constexpr int nl = D3 ? 3 : (D2 ? 2 : 1);
   static constexpr int D0 = (F_ * K_ + 31) / 32 * 32;
   __device__ static constexpr int dim(int l) { return l == 0 ? D0 : l == 1 ? D1 : l == 2 ? D2 : D3; }
+  static constexpr int G = G_;
+  static constexpr int T0F = D1 / 16 / G_;                    // layer-0 forward tiles per member
+  static constexpr int FG = (F_ + G_ - 1) / G_;               // fields per member (the last: fewer)
+  static constexpr int T0B = G_ > 1 ? FG * K_ / 16 : D0 / 16;  // layer-0 dgrad tiles per member (≤)
+  static_assert(G_ == 1 || (K_ % 16 == 0 && (D1 / 16) % G_ == 0), "row split: K and D1/16 multiples");
   static constexpr int KSF0 = D0 / 32, KSF1 = D1 / 32 > 0 ? D1 / 32 : 1, KSF2 = D2 / 32 > 0 ? D2 / 32 : 1;
-  static constexpr int NJB0 = (D0 / 16 + kWaves - 1) / kWaves;
+  static constexpr int NJB0 = (T0B + kWaves - 1) / kWaves;
   static constexpr int KSB0 = D1 / 32, KSB1 = D2 / 32 > 0 ? D2 / 32 : 1, KSB2 = D3 / 32 > 0 ? D3 / 32 : 1;
   static constexpr int KP4 = (K_ + 1 + 3) / 4;
   static constexpr int GU = (kRowTile * F_ * KP4 + kRowThreads - 1) / kRowThreads;
@@ -211,8 +223,8 @@ struct CtShape {
   // then stream through the KSF0 registers of one tile — slot u is refilled with the next tile's
   // k-step u right after its MFMA has been issued — so the second tile's loads fly under the first
   // tile's MFMAs and epilogue (the per-CU fragment bandwidth, not registers, bounds the layer).
-  static constexpr int NTF0 = (D1 / 16 + kWaves - 1) / kWaves;
-  static constexpr int NTB1 = NTF0;
+  static constexpr int NTF0 = (T0F + kWaves - 1) / kWaves;
+  static constexpr int NTB1 = (D1 / 16 + kWaves - 1) / kWaves;
   static constexpr bool kWide = NTF0 > 1;
   // registers for layer-0 backward fragments: all NJB0 tiles, or (kLateBw0) a ring of NJB0H tiles —
   // slot j % NJB0H is refilled with tile j + NJB0H right after tile j's MFMAs have been issued (wide
@@ -223,7 +235,19 @@ struct CtShape {
   static_assert(!kWide || (kLateBw0 && NTF0 == 2), "CtShape: a 256-wide first layer needs the streamed layer 0");
   static_assert(D1 % 32 == 0 && D2 % 32 == 0 && D3 % 32 == 0, "hidden dims padded to 32");
   static_assert(GU <= 12, "CtShape: at most 12 gathered rows per thread");
+  static_assert(G_ == 1 || kLateBw0, "row split: wide input layers only");
 };
+
+template <class SH, int RT, int KP4>
+__device__ constexpr int gather_units();
+// phase F's per-lookup items of one member: its FG fields (all F without the split)
+template <class SH, int RT, int KP4>
+__device__ constexpr int gather_units_f() {
+  if constexpr (SH::kStatic && SH::G > 1)
+    return (RT * SH::FG * KP4 + kRowThreads - 1) / kRowThreads;
+  else
+    return gather_units<SH, RT, KP4>();
+}
 
 template <class SH, int RT, int KP4>
 __device__ constexpr int gather_units() {
@@ -284,7 +308,17 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const bool train = MODE == kDynamic ? (p.train != 0) : (MODE == kTrain);
   const int ablate = DIAG ? p.ablate : 0;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int row0 = blockIdx.x * RT;
+  // row-tile split: the G members of row tile rt are blocks (rt / 8)·8G + m·8 + rt % 8 — equal
+  // blockIdx % 8, one XCD under round-robin dispatch (a speed matter only), consecutive in dispatch
+  // order (the exchange's waiters never wait on a block queued behind them)
+  constexpr int G = SH::G;
+  const int mbr = G > 1 ? (int)((blockIdx.x >> 3) % G) : 0;
+  const int rtile = G > 1 ? (int)((blockIdx.x / (8 * G)) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
+  const bool lead = mbr == 0;  // the member that stores the row tile's shared outputs
+  const int row0 = rtile * RT;
+  // layer-0 dgrad tiles of this member: its fields' columns (all of dims[0] without the split)
+  const int tb0 = G > 1 ? mbr * SH::T0B : 0;
+  const int tb1 = G > 1 ? min(tb0 + SH::T0B, sh.dim(0) / 16) : sh.dim(0) / 16;
   const int F = sh.F, K = sh.K, NL = sh.nl;
   const int D0 = F * K, D0p = sh.dim(0);
   const uint32_t magicF = p.magicF;
@@ -332,7 +366,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const float wo = p.w_out[min(t, sh.dim(SH::nl) - 1)];
     const float lab = p.labels[min(row0 + (t & (RT - 1)), max(p.B - 1, 0))];
     const float bo = *p.b_out, fb = *p.fm_bias;
-    const int nt = min(wave, sh.dim(1) / 16 - 1);
+    const int nt = G > 1 ? mbr * SH::T0F + min(wave, SH::T0F - 1) : min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
     for (int u = 0; u < SH::KSF0E; ++u) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nt, u, sh.dim(0), lane));
 #pragma unroll
@@ -448,7 +482,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   ROWS_STAMP(2);
 
   if constexpr (SH::kStatic && SH::KSF0E < SH::KSF0) {  // the rest of layer 0's forward fragments
-    const int nt = min(wave, sh.dim(1) / 16 - 1);
+    const int nt = G > 1 ? mbr * SH::T0F + min(wave, SH::T0F - 1) : min(wave, sh.dim(1) / 16 - 1);
 #pragma unroll
     for (int u = SH::KSF0E; u < SH::KSF0; ++u) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nt, u, sh.dim(0), lane));
   }
@@ -520,9 +554,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   if (train && !(ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
     const uint16_t* h0 = reinterpret_cast<const uint16_t*>(smem + L.act[0]);
     const int lda = L.lda[0];
+    // (split: the member's own fields' columns; the last member also the padding columns)
+    const int cb = G > 1 ? mbr * SH::FG * K : 0;
+    const int ce = (G > 1 && mbr < G - 1) ? cb + SH::FG * K : D0p;
     if constexpr (RT >= 8) {
-      for (int it = t; it < D0p * (RT / 8); it += kRowThreads) {
-        const int c = RT == 8 ? it : it >> 1, h = RT == 8 ? 0 : it & 1;
+      for (int it = t; it < (ce - cb) * (RT / 8); it += kRowThreads) {
+        const int c = cb + (RT == 8 ? it : it >> 1), h = RT == 8 ? 0 : it & 1;
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -530,7 +567,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         *reinterpret_cast<uint4*>(p.actT[0] + act_swz(c, row0 + h * 8, Bp)) = make_uint4(w[0], w[1], w[2], w[3]);
       }
     } else {  // 4 rows × 1 column per item → one 8-B store
-      for (int c = t; c < D0p; c += kRowThreads) {
+      for (int c = cb + t; c < ce; c += kRowThreads) {
         const uint32_t w0 = (uint32_t)h0[c] | ((uint32_t)h0[lda + c] << 16);
         const uint32_t w1 = (uint32_t)h0[2 * lda + c] | ((uint32_t)h0[3 * lda + c] << 16);
         *reinterpret_cast<uint2*>(p.actT[0] + act_swz(c, row0, Bp)) = make_uint2(w0, w1);
@@ -607,21 +644,31 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       if (l == SH::nl - 1 && train && !(ablate & 4)) {
 #pragma unroll
         for (int j = 0; j < SH::NJB0H; ++j) {
-          const int nt = min(wave + kWaves * j, sh.dim(0) / 16 - 1);
+          const int nt = min(tb0 + wave + kWaves * j, tb1 - 1);
 #pragma unroll
           for (int u = 0; u < SH::KSB0; ++u) bw0[j][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
         }
       }
     }
     const int ntiles = Dout >> 4;
+    // split: layer 0's forward tiles of this member only
+    const int ltb = (G > 1 && l == 0) ? mbr * SH::T0F : 0;
+    const int lte = (G > 1 && l == 0) ? ltb + SH::T0F : ntiles;
     // compile-time shapes: tile j of this wave is wave + 8j (layer 0 of a wide shape has 2, every
     // other layer 1 — the outer loop then runs once); runtime shapes: one tile per iteration
     constexpr int kNT = SH::kStatic ? SH::NTF0 : 1;
-    for (int nt0 = wave; nt0 < ntiles; nt0 += kNT * kWaves) {
+    for (int nt0 = ltb + wave; nt0 < lte; nt0 += kNT * kWaves) {
 #pragma unroll
      for (int j = 0; j < kNT; ++j) {
       const int nt = nt0 + kWaves * j;
-      if (j > 0 && (l > 0 || nt >= ntiles)) break;
+      if (j > 0 && (l > 0 || nt >= lte)) break;
+      // diagnostics (ablate bits 4 / 5): only 1/2 or 1/4 of layer 0's forward tiles — what a
+      // workgroup of a row-group split over 2 / 4 workgroups would stream (profiles/r5_layer0_split.md)
+      if (DIAG && l == 0 && (ablate & 48)) {
+        if (j > 0 && SH::kWide) break;
+        const int wcut = SH::kWide ? ((ablate & 32) ? 4 : 8) : ((ablate & 32) ? 2 : 4);
+        if (wave >= wcut) break;
+      }
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SH::kStatic) {
         const uint16_t* ap = A + (lane & 15) * lda + 8 * (lane >> 4);
@@ -631,7 +678,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
           for (int u = 0; u < SH::KSF0; ++u) {
             acc = mfma16x16x32(ld_frag(ap + 32 * u), fw0[u], acc);
-            if (j + 1 < kNT) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nxt, u, sh.dim(0), lane));
+            if (j + 1 < kNT && !(DIAG && (ablate & 48))) fw0[u] = ld_w0<FP8>(p.WTs[0], p.w8.f, frag_at(nxt, u, sh.dim(0), lane));
           }
         } else if (l == 0) {
           if constexpr (FP8) {
@@ -691,10 +738,62 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         hv[i] = a;
         O[(rb + i) * ldo + c] = f2bf(a);
       }
-      if (train && rb < RT)
+      if (train && rb < RT && (G == 1 || l == 0 || lead))
         *reinterpret_cast<uint2*>(p.actT[l + 1] + act_swz(c, row0 + rb, Bp)) =
             make_uint2(pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3]));
+      if (G > 1 && l == 0 && rb < RT) {  // the exchange: 4 rows of column c, one 8-B write-through store
+        const size_t xo = (((size_t)rtile * G + mbr) * (SH::T0F * 16) + (c - ltb * 16)) * 16 + rb;
+        const unsigned long long v8 = (unsigned long long)pack_bf2(hv[0], hv[1]) |
+                                      ((unsigned long long)pack_bf2(hv[2], hv[3]) << 32);
+        __hip_atomic_store((xg_u64*)(p.xbuf + xo), v8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
      }
+    }
+    if constexpr (G > 1) {
+      if (l == 0) {
+        // hand-off (MI355X_MICROARCH.md § visibility, Valid forms row 1): every wave drains its
+        // write-through stores, ONE lane adds to the row tile's arrival counter (agent scope); the
+        // last arrival learns it from the returned value, the others poll it (sc1 loads, s_sleep,
+        // bounded); every load of a peer's columns is an sc1 load.  The counter rises by G per
+        // launch and is never reset (arrival parity = old mod G).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+          bn_gu32* ctr = (bn_gu32*)(p.xctr) + rtile;
+          const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned gen0 = old - old % (unsigned)G;
+          if (old - gen0 != (unsigned)G - 1u) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - gen0 < (unsigned)G) {
+              __builtin_amdgcn_s_sleep(1);
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kBnSpinTicks) {
+                atomicOr(p.xerr, 1);
+                break;
+              }
+            }
+          }
+        }
+        __syncthreads();
+        constexpr int kCols = SH::T0F * 16, kPc = RT / 4;  // a member's columns; 4-row pieces per column
+        for (int it = t; it < (G - 1) * kCols * kPc; it += kRowThreads) {
+          const int pi = it / (kCols * kPc), rem = it - pi * (kCols * kPc);
+          const int q = pi < mbr ? pi : pi + 1;  // the peer member
+          const int cc = rem / kPc, r4 = (rem - cc * kPc) * 4;
+          const unsigned long long v8 = __hip_atomic_load(
+              (xg_u64*)(p.xbuf + (((size_t)rtile * G + q) * kCols + cc) * 16 + r4), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT);
+          const int c = q * kCols + cc;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) O[(r4 + i) * ldo + c] = (uint16_t)(v8 >> (16 * i));
+        }
+        if constexpr (RT < kRowTile) {  // padding rows of the peers' columns: zero MFMA operands
+          for (int it = t; it < (kRowTile - RT) * (G - 1) * kCols; it += kRowThreads) {
+            const int r = RT + it / ((G - 1) * kCols), k = it - (r - RT) * ((G - 1) * kCols);
+            const int q = k / kCols < mbr ? k / kCols : k / kCols + 1;
+            O[r * ldo + q * kCols + (k % kCols)] = 0;
+          }
+        }
+      }
     }
     if constexpr (!SH::kStatic || BN) {
       if (p.bn && train) {
@@ -787,11 +886,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
       g = valid ? g * p.inv_scale : 0.f;
       s_g[r] = g;
-      if (valid) {
+      if (valid && lead) {
         p.prob[gr] = pr;
         if (p.loss_rows) p.loss_rows[gr] = loss;
       }
-      if (train && r < RT) p.g_out[gr] = g;
+      if (train && r < RT && lead) p.g_out[gr] = g;
     }
   }
   if (!train) return;
@@ -801,14 +900,25 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 
   // phase F's embedding rows are re-read here, long before they are needed (hidden by phase E);
   // kLateBw0 shapes re-read them after the layer-0 backward GEMM (register budget)
-  const int nitemsF = RT * F * KP4;
-  constexpr int UF = kGU;
+  // phase F's items: (row, field, float4 column); split: only this member's FG fields — item
+  // (r, fl, c4) is field mbr·FG + fl, past F on the last member (no item)
+  constexpr int FI = (G > 1) ? SH::FG : 0;  // fields per member (0: all F)
+  const int nitemsF = RT * (G > 1 ? FI : F) * KP4;
+  constexpr int UF = gather_units_f<SH, RT, KP4>();
+  auto item_rf = [&](int idx) {  // lookup (r·F + f) of item idx
+    if constexpr (G > 1) {
+      const int rfl = idx / KP4, r = rfl / FI, f = min(mbr * FI + (rfl - r * FI), F - 1);
+      return r * F + f;
+    } else {
+      return idx / KP4;
+    }
+  };
   float4 rowsF[UF];
   if constexpr (!SH::kLateBw0) {
 #pragma unroll
     for (int u = 0; u < UF; ++u) {
       const int idx = min(u * kRowThreads + t, nitemsF - 1);
-      const int rf = idx / KP4, c4 = idx - rf * KP4;
+      const int rf = item_rf(idx), c4 = idx % KP4;
       rowsF[u] = tbl_load4<BT>(emb4, (size_t)s_ids[rf] * KP4 + c4);
     }
   }
@@ -913,7 +1023,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         dz_cur[r * ldz + c] = f2bf(v[i]);
         if (FP8 && a == 1) atomicMax(reinterpret_cast<unsigned*>(s_amax) + r, __float_as_uint(fabsf(bf2f(f2bf(v[i])))));
       }
-      if (rg * 4 < RT)
+      if (rg * 4 < RT && lead)
         *reinterpret_cast<uint2*>(p.dzT[a] + act_swz(c, row0 + rg * 4, Bp)) =
             make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     }
@@ -924,9 +1034,11 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     if (a == NL) ROWS_STAMP(10);
     const int li = a - 1, Dout = sh.dim(a), Din = sh.dim(li);
 
-    const int ntiles = Din >> 4;
+    // (split: the layer-0 dgrad tiles of this member's fields)
+    const int ntb = li == 0 ? tb0 : 0;
+    const int ntiles = li == 0 ? tb1 : (Din >> 4);
     constexpr int NJ = SH::kStatic ? (SH::NJB0 > 1 ? SH::NJB0 : 1) : 4;
-    for (int nt0 = wave; nt0 < ntiles; nt0 += NJ * kWaves) {
+    for (int nt0 = ntb + wave; nt0 < ntiles; nt0 += NJ * kWaves) {
       f32x4 accs[NJ];
       if constexpr (SH::kStatic) {
         const uint16_t* ap = dz_cur + (lane & 15) * ldz + 8 * (lane >> 4);
@@ -938,15 +1050,17 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
           bf16x8 av[SH::KSB0];
 #pragma unroll
           for (int u = 0; u < SH::KSB0; ++u) av[u] = ld_frag(ap + 32 * u);
+          // (diagnostics, ablate bits 4 / 5: only the first 1/2 or 1/4 of the tiles, as above)
+          const int jcut = (DIAG && (ablate & 48)) ? ((ablate & 32) ? (NJ + 3) / 4 : (NJ + 1) / 2) : NJ;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             const int slot = j % SH::NJB0H;
-            if (nt0 + kWaves * j < ntiles) {
+            if (nt0 + kWaves * j < ntiles && j < jcut) {
 #pragma unroll
               for (int u = 0; u < SH::KSB0; ++u) accs[j] = mfma16x16x32(av[u], bw0[slot][u], accs[j]);
             }
-            if (j + SH::NJB0H < SH::NJB0) {
-              const int nt = min(wave + kWaves * (j + SH::NJB0H), sh.dim(0) / 16 - 1);
+            if (j + SH::NJB0H < SH::NJB0 && j + SH::NJB0H < jcut) {
+              const int nt = min(tb0 + wave + kWaves * (j + SH::NJB0H), tb1 - 1);
 #pragma unroll
               for (int u = 0; u < SH::KSB0; ++u) bw0[slot][u] = ld_w0<FP8>(p.Wbs[0], p.w8.b, frag_at(nt, u, sh.dim(1), lane));
             }
@@ -1035,7 +1149,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
               if ((lane & 15) == 0) atomicMax(reinterpret_cast<unsigned*>(s_amax) + rb + i, __float_as_uint(m));
             }
           }
-          if (rb < RT)
+          if (rb < RT && lead)
             *reinterpret_cast<uint2*>(p.dzT[li] + act_swz(c, row0 + rb, Bp)) =
                 make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         } else {
@@ -1060,7 +1174,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
       for (int u = 0; u < UF; ++u) {
         const int idx = min(base + u * kRowThreads + t, nitemsF - 1);
-        const int rf = idx / KP4, c4 = idx - rf * KP4;
+        const int rf = item_rf(idx), c4 = idx % KP4;
         rowsF[u] = tbl_load4<BT>(emb4, (size_t)s_ids[rf] * KP4 + c4);
       }
     }
@@ -1074,9 +1188,10 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     for (int u = 0; u < UF; ++u) {
       const int idx0 = base + u * kRowThreads + t;
       const int idx = min(idx0, nitemsF - 1);
-      const int rf = idx / KP4, c4 = idx - rf * KP4;
+      const int rf = item_rf(idx), c4 = idx % KP4;
       const int r = fdiv(rf, magicF), f = rf - r * F;
       ok[u] = idx0 < nitemsF && row0 + r < p.B;
+      if constexpr (G > 1) ok[u] = ok[u] && mbr * FI + (idx / KP4) % FI < F;
       const float g = s_g[r], x = s_vals[rf];
       const float* S = s_S + r * K;
       const float* dh = s_f32 + r * D0p + f * K;
@@ -1088,7 +1203,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
       dst[u] = s_pos[rf] * KP4 + c4;
     }
-    if (p.dedup) {  // the tile's rows stay in LDS: summed per group below
+    if (G == 1 && p.dedup) {  // the tile's rows stay in LDS: summed per group below (no split)
       if (L.gr == L.f32) lds_barrier();  // (over dh0: every thread's reads of it are done)
       float4* s_gr = reinterpret_cast<float4*>(smem + L.gr);
 #pragma unroll
@@ -1102,7 +1217,7 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
         if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
     }
   }
-  if (p.dedup) {
+  if (G == 1 && p.dedup) {
     // per-tile dedup: each group (equal id within this row tile) sums its lookups' rows in lookup
     // order — head first, then along the nxt chain — and stores ONE row at its compacted index
     lds_barrier();
@@ -1247,7 +1362,7 @@ static void launch_rows_impl(const RowsParams& p, hipStream_t stream) {
     ROCFM_REQUIRE(p.Bp / kRowTile <= limit, "deepfm_rows: batch_norm needs every workgroup of the batch resident "
                                             "at once (batch too large for one launch; use engine=torch)");
   }
-  hipLaunchKernelGGL(kern, dim3(p.Bp / RT), dim3(kRowThreads), p.lds.total, stream, p);
+  hipLaunchKernelGGL(kern, dim3(p.Bp / RT * SH::G), dim3(kRowThreads), p.lds.total, stream, p);
 }
 
 // Static shapes: branch-free train / inference kernels; the diagnostic (stamps, ablations)
@@ -1307,7 +1422,9 @@ constexpr int kDefaultRowTile = 8;
 // streaming the layer-0 weights through each CU): 4 examples per workgroup — 256 workgroups halve
 // the gather / FM / FM-backward work per CU at the same weight stream (k = 32: 57.4 → 56.3 and
 // 44.1 → 43.5 µs per step; k = 10 unchanged, profiles/r5_wgrad_swizzle.md)
+static bool split_ok(const RowsParams& p);
 static int row_tile_for(const RowsParams& p, bool is_static_shape) {
+  if (is_static_shape && split_ok(p)) return 8;  // the row-tile split: 8-row tiles (2 × 128 workgroups)
   const int rt = p.row_tile ? p.row_tile : (is_static_shape && p.dims[0] >= 1024 ? 4 : kDefaultRowTile);
   if (p.bn) return kRowTile;  // batch-norm statistics partials are per 16-row workgroup
   if (is_static_shape) return rt;
@@ -1354,6 +1471,30 @@ static bool try_static(const RowsParams& p, hipStream_t stream) {
   return true;
 }
 
+// The row-tile split (2 workgroups per 8-row tile) for the training kernel of the reference's flag
+// defaults (39 × 32 → 256-128-64: W0 is 624 KiB; profiles/r5_layer0_split.md), bf16 MFMA, no
+// per-tile dedup, no batch norm.  ROCFM_ROW_SPLIT / RowsParams::split = 2 asks for it.
+static bool split_ok(const RowsParams& p) {
+  return p.split == 2 && p.train && !p.fp8 && !p.bn && !p.dedup && !p.force_generic && p.xbuf && p.xctr &&
+         p.xerr && static_match<39, 32, 256, 128, 64>(p) && (p.row_tile == 0 || p.row_tile == 8) &&
+         (p.Bp / 8) % 8 == 0;
+}
+static bool try_split(const RowsParams& p, hipStream_t stream) {
+  if (!split_ok(p)) return false;
+  using SH = CtShape<39, 32, 256, 128, 64, 2>;
+  constexpr int KP4 = 9;
+  const bool diag = p.stamps != nullptr || p.ablate != 0;
+  if (p.tbl_bf16) {
+    if (diag) throw std::invalid_argument("deepfm_rows: split diagnostics need an f32 table");
+    launch_rows_impl<KP4, SH, false, kTrain, false, true, 8>(p, stream);
+  } else if (diag) {
+    launch_rows_impl<KP4, SH, false, kTrain, true, false, 8>(p, stream);
+  } else {
+    launch_rows_impl<KP4, SH, false, kTrain, false, false, 8>(p, stream);
+  }
+  return true;
+}
+
 // batch_norm runs the compile-time-shape kernels too, with an f32 table and bf16 MFMA
 static bool static_ok(const RowsParams& p) { return !p.force_generic && !(p.bn && (p.tbl_bf16 || p.fp8)); }
 
@@ -1366,6 +1507,8 @@ static bool is_static(const RowsParams& p) {
 
 // Examples per workgroup the launcher will use for these parameters (the per-tile dedup of the side
 // chain must cut the same tiles).
+int deepfm_rows_split(const RowsParams& p) { return static_ok(p) && split_ok(p) ? 2 : 1; }
+
 int deepfm_rows_tile(const RowsParams& p) {
   return row_tile_for(p, is_static(p));
 }
@@ -1399,7 +1542,7 @@ void launch_deepfm_rows(RowsParams p, hipStream_t stream) {
     for (int a = 1; a <= p.nl; ++a) ROCFM_REQUIRE(p.dims[a] <= p.bn_dmax, "deepfm_rows: bn_dmax < hidden dim");
   }
   if (static_ok(p)) {
-    if (try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
+    if (try_split(p, stream) || try_static<39, 10, 128, 64, 32>(p, stream) || try_static<39, 8, 128, 64, 32>(p, stream) ||
         try_static<39, 12, 128, 64, 32>(p, stream) || try_static<39, 10, 64, 32, 0>(p, stream) ||
         try_static<39, 32, 128, 64, 32>(p, stream) || try_static<39, 32, 256, 128, 64>(p, stream)) {
       ROCFM_HIP_CHECK(hipGetLastError());

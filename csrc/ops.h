@@ -22,6 +22,7 @@ RowsLds rows_lds_layout(const int* dims, int nl, int F, int K, int bn = 0, int d
 RowsLds rows_lds_layout_for(const RowsParams& p);  // the layout the launcher uses
 void launch_deepfm_rows(RowsParams p, hipStream_t stream);
 int deepfm_rows_tile(const RowsParams& p);
+int deepfm_rows_split(const RowsParams& p);  // workgroups per row tile the launcher will use (1 or 2)
 bool deepfm_rows_static(const RowsParams& p);  // a compile-time-shape instantiation will run
 
 // mlp_wgrad.hip

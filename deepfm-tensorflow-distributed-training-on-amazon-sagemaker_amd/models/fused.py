@@ -218,6 +218,18 @@ class FusedDeepFM:
             self.bn_grad = torch.zeros(L.nl, 2, self.bn_dmax, dtype=torch.float32, device=dev)
             self.bn_sync = torch.zeros(4, dtype=torch.int32, device=dev)
             self.bn_error = torch.zeros(4, dtype=torch.int32, device=dev)
+        # row-tile split (deepfm_rows.hip CtShape G; profiles/r5_layer0_split.md): two workgroups per
+        # 8-row tile, each streaming half of a wide input layer's weights, with an in-launch exchange
+        # of layer 0's outputs.  ROCFM_ROW_SPLIT = auto (wide input layers: dims[0] ≥ 1024 and a
+        # 256-wide first hidden layer — the kernel has it for the reference's flag defaults), 1, 2.
+        sp = os.environ.get("ROCFM_ROW_SPLIT", "auto")
+        if sp not in ("auto", "1", "2"):
+            raise ValueError(f"ROCFM_ROW_SPLIT must be auto, 1 or 2, got {sp!r}")
+        self.row_split = 2 if (sp == "2" or (sp == "auto" and L.dims[0] >= 1024 and L.dims[1] >= 256)) else 1
+        if self.row_split > 1:
+            self.xbuf = torch.zeros(self.Bp // 8 * L.dims[1] * 16, dtype=torch.int16, device=dev)
+            self.xctr = torch.zeros(self.Bp // 8, dtype=torch.int32, device=dev)
+            self.xerr = torch.zeros(4, dtype=torch.int32, device=dev)
         self.WT = [torch.zeros(L.dims[l + 1], L.dims[l], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         self.Wb = [torch.zeros(L.dims[l], L.dims[l + 1], dtype=torch.bfloat16, device=dev) for l in range(L.nl)]
         # MFMA-fragment-swizzled copies (common.h frag_swz): what the compile-time-shape row kernel loads
@@ -375,6 +387,8 @@ class FusedDeepFM:
         rp.force_generic = 1 if self.force_generic else 0
         rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
         rp.row_tile = self.row_tile
+        if self.row_split > 1:  # (the launcher keeps one workgroup per tile where the split does not apply)
+            rp.split, rp.xbuf, rp.xctr, rp.xerr = 2, self.xbuf.data_ptr(), self.xctr.data_ptr(), self.xerr.data_ptr()
         self._set_w8(rp, 0)
         rp.dedup = 1 if (train and self.dedup) else 0
         rp.set_dims(L.dims)
@@ -1511,6 +1525,10 @@ class FusedDeepFM:
         self._check_decode(block=True)
         if self.bn and int(self.bn_error[0].item()) != 0:
             raise RuntimeError("deepfm_rows: a batch_norm grid barrier timed out (not every workgroup was resident)")
+        if self.row_split > 1 and int(self.xerr[0].item()) != 0:
+            self.xctr.zero_()  # (the arrival parity is lost with the timed-out launch)
+            self.xerr.zero_()
+            raise RuntimeError("deepfm_rows: a row-tile split exchange timed out (its steps' layer-1 inputs are invalid)")
         if self.id_guard and int(self.bad_ids.item()) != 0:
             raise ValueError(f"ROCFM_CHECK_IDS: a batch held feature ids outside [0, {self.id_limit}) "
                              "(they were trained as row 0)")

@@ -110,9 +110,12 @@ def search_dir_buckets(W: int, V: int) -> int:
 
 # The plan-ahead merge (merge_plan.hip) from this many ranks on: the union of the ranks' exported
 # ids and every id's position in every export are built on the side chain a graph ahead (the ids
-# exchanged there), so the step's merge is one plan-driven gather-sum (ROCFM_MERGE=plan forces it
-# from 2 ranks, any other forced merge keeps it off).  profiles/r5_dp_plan_merge.md.
-PLAN_MIN_W = 5
+# exchanged there), so the step's merge is one plan-driven gather-sum (ROCFM_MERGE=plan forces it,
+# also over RCCL; any other forced merge keeps it off).  tools/bench_merge.py, uncached p2p
+# memory: the step's apply 3.9 / 4.4 / 5.6 µs at W = 2 / 4 / 8 against 7.6 / 9.6 / 14.1 for the
+# best step-time merge, for 2.9 / 3.5 / 5.7 µs per step of plan building on the side chain of a
+# 16-step graph (profiles/r5_dp_plan_merge.md).
+PLAN_MIN_W = 2
 
 
 def plan_merge_enabled(W: int, exchange: str) -> bool:
@@ -140,10 +143,11 @@ class MergeMaps:
 
     def __init__(self, W: int, cap: int, rows: int, device):
         choice = os.environ.get("ROCFM_MERGE", "auto")
-        if choice not in ("auto", "direct", "hash", "range"):
-            raise ValueError(f"ROCFM_MERGE must be auto, direct, hash or range, got {choice!r}")
+        if choice not in ("auto", "direct", "hash", "range", "plan"):
+            raise ValueError(f"ROCFM_MERGE must be auto, direct, hash, range or plan, got {choice!r}")
         direct_bytes = (W + 1) * rows * 4
-        self.hashed = choice == "hash" or (choice == "auto" and direct_bytes > MERGE_MAP_BUDGET)
+        # (plan: the multi-step graphs merge by the plan; the per-step path keeps the automatic maps)
+        self.hashed = choice == "hash" or (choice in ("auto", "plan") and direct_bytes > MERGE_MAP_BUDGET)
         i32 = dict(dtype=torch.int32, device=device)
         if self.hashed:
             self.slots = 1 << max(4, math.ceil(math.log2(max(2 * W * cap, 2))))
@@ -659,7 +663,10 @@ class FusedDataParallel:
         self._graphs = {}  # captured graphs hold the previous parameter blocks / buffers
         # sorted export (the fused tail's chunks, run heads counted on the side chain) → the merge
         # needs no maps: one search-mode launch (merge.hip) after the exchange
-        self.m_plan = self.mode == "dp" and e.Kp <= H.tail_max_kp() and plan_merge_enabled(self.world, self.exchange)
+        # (not with the per-tile dedup: its export lists come from the compacted groups, whose chunk
+        # heads the plan's unique-id pass does not read)
+        self.m_plan = (self.mode == "dp" and e.Kp <= H.tail_max_kp() and not e.dedup
+                       and plan_merge_enabled(self.world, self.exchange))
         self.m_sorted = self.mode == "dp" and e.Kp <= H.tail_max_kp() and (self.world <= SEARCH_MAX_W or self.range
                                                                             or self.sdir or self.m_plan)
         e._build_multi(Smax, heads=self.m_sorted)
@@ -895,8 +902,9 @@ class FusedDataParallel:
             dist.all_reduce(x, op=dist.ReduceOp.MAX)
         n = len(names)
         out = {k: {"max": round(float(x[i]), 4), "min": round(-float(x[n + i]), 4)} for i, k in enumerate(names)}
-        out["merge_mode"] = ("range" if self.range else "search+dir" if (self.m_sorted and self.sdir)
-                             else "search" if self.m_sorted else "maps")
+        out["merge_mode"] = ("plan" if getattr(self, "m_plan", False) else "range" if self.range
+                             else "search+dir" if (self.m_sorted and self.sdir) else "search" if self.m_sorted
+                             else "maps")
         out["cap"] = int(self.cap)
         out["push"] = "fused" if self.fused_push else ("copy" if self.p2p is not None else "collective")
         return out

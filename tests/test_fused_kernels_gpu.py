@@ -727,3 +727,38 @@ def test_wide_static_kernel_equals_runtime_shape(dedup, monkeypatch):
     for x, y in zip(out[True], out[False]):
         d = (x - y).abs()
         assert bool((d <= 1e-6 + 1e-4 * y.abs()).all()), d.max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tbl,graph", [("f32", True), ("bf16", True), ("f32", False)])
+def test_row_split_equals_unsplit(tbl, graph, monkeypatch):
+    """The row-tile split (ROCFM_ROW_SPLIT=2: two workgroups per 8-row tile, each streaming half of
+    W0 and computing its half of layer 0's outputs and its fields' dgrad, with an in-launch exchange
+    of the outputs) ≡ one workgroup per tile, bitwise: the reference's flag-default shape (39 × 32 →
+    256-128-64), Adam + dropout, a batch that is not a multiple of 8, multi-step graphs and per-step
+    launches, f32 and bf16 tables; the exchange's error word stays clear."""
+    monkeypatch.setenv("ROCFM_DEDUP", "0")
+    spec = ModelSpec(feature_size=3000, field_size=39, embedding_size=32, layers=[256, 128, 64],
+                     keep_probs=[0.7] * 3, l2_reg=1e-3)
+    hp = OptHParams(name="Adam", lr=2e-3)
+    g = torch.Generator().manual_seed(5)
+    B = 200
+    pool = [_batch(B, 39, 3000, g) for _ in range(5)]
+    ids, vals, labels = (torch.stack([p[i] for p in pool]).cuda() for i in range(3))
+    out = {}
+    for split in ("1", "2"):
+        monkeypatch.setenv("ROCFM_ROW_SPLIT", split)
+        e = FusedDeepFM(spec, hp, B, "cuda", params=init_params(spec, 4), use_graph=graph, table_dtype=tbl)
+        assert e.H.deepfm_rows_split(e.rows_params[0]) == int(split)
+        e.attach_pool(ids, vals, labels)
+        if graph:
+            e.train_steps(13, 4)
+        else:
+            for _ in range(7):
+                e.train_step()
+        torch.cuda.synchronize()
+        e.check()
+        out[split] = (e.emb.clone(), e.dense.clone(), [s.clone() for s in e.emb_slots], e.prob[:B].clone())
+    a, b = out["1"], out["2"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[3], b[3])
+    assert all(torch.equal(x, y) for x, y in zip(a[2], b[2]))

@@ -117,8 +117,11 @@ def main():
             k_, c_, r_, d_, sd_ = src
             p.keys, p.rows, p.counts = k_.data_ptr(), r_.data_ptr(), c_.data_ptr()
             dir_of = {"range": (d_.data_ptr(), nb + 1, nb, div), "search+dir": (sd_.data_ptr(), snb + 1, snb, sdiv)}
-            _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, sum(len(x) for x in lists),
-                         plan_for(H, W, cap, k_, c_, Vk, dev, s))
+            plan = plan_for(H, W, cap, k_, c_, Vk, dev, s)
+            if W > 1:  # the side chain's per-step share when a 16-step graph builds its plans at once
+                print(f"W={W} {mem}: plan build {plan_for(H, W, cap, k_, c_, Vk, dev, s, S=16)[1]:.2f} us per step "
+                      f"at S = 16 ({plan[1]:.2f} at S = 1)")
+            _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, sum(len(x) for x in lists), plan)
             torch.cuda.synchronize()
             if raw is not None:
                 del src, k_, c_, r_, d_, sd_
@@ -138,19 +141,20 @@ def _uncached_view(ptr, shape, dtype, dev):
     return torch.as_tensor(raw, device=dev).view(*shape)
 
 
-def plan_for(H, W, cap, keys32, counts, Vk, dev, s):
-    """The plan-ahead merge's side-chain product for these W lists (merge_plan.hip plan_build, one
-    step): union ids + every id's position in every list.  Returns (PlanStep, build µs)."""
+def plan_for(H, W, cap, keys32, counts, Vk, dev, s, S=1):
+    """The plan-ahead merge's side-chain product for these W lists (merge_plan.hip plan_build, S
+    steps of the same lists, as one multi-step graph builds them): union ids + every id's position
+    in every list.  Returns (PlanStep of step 0, build µs PER STEP, kept buffers)."""
     n = W * cap
     i32 = dict(dtype=torch.int32, device=dev)
-    bufs = {k: torch.zeros(n, **i32) for k in ("pkeys", "sk", "sv", "rows")}
-    pos = torch.zeros(n * W, **i32)
-    cnt = torch.zeros(4, **i32)
-    tiles = torch.zeros(H.plan_tile_ints(1, W, cap), **i32)
+    bufs = {k: torch.zeros(S * n, **i32) for k in ("pkeys", "sk", "sv", "rows")}
+    pos = torch.zeros(S * n * W, **i32)
+    cnt = torch.zeros(max(4, S), **i32)
+    tiles = torch.zeros(H.plan_tile_ints(S, W, cap), **i32)
     bits = max(1, int(Vk).bit_length())  # the pad key Vk sorts after every id
-    temp = torch.zeros(max(16, H.plan_sort_temp_bytes(1, W, cap, bits)), dtype=torch.uint8, device=dev)
+    temp = torch.zeros(max(16, H.plan_sort_temp_bytes(S, W, cap, bits)), dtype=torch.uint8, device=dev)
     pp = H.PlanParams()
-    pp.S, pp.W, pp.cap = 1, W, cap
+    pp.S, pp.W, pp.cap = S, W, cap
     pp.gkeys, pp.gcounts = keys32.data_ptr(), counts.data_ptr()
     pp.gk_stride, pp.gc_stride, pp.gkey_step, pp.gcount_step = cap, 1, 0, 0
     pp.pad_key = Vk
@@ -167,7 +171,7 @@ def plan_for(H, W, cap, keys32, counts, Vk, dev, s):
     torch.cuda.synchronize()
     ps = H.PlanStep()
     ps.rows, ps.pos, ps.count = bufs["rows"].data_ptr(), pos.data_ptr(), cnt.data_ptr()
-    return ps, e0.elapsed_time(e1) * 1000 / 20, (bufs, pos, cnt, tiles, temp)  # (keeps the buffers alive)
+    return ps, e0.elapsed_time(e1) * 1000 / 20 / S, (bufs, pos, cnt, tiles, temp)  # (keeps the buffers alive)
 
 
 def _time_merges(H, a, p, W, cap, nb, snb, names, dir_of, s, dg, mem, live, plan=None):
