@@ -568,8 +568,14 @@ def secondary_windows(a, spec, hp, params, dev, pool):
         # (warm-up >= 4 graphs: the first launch is eager, so both parities' graphs get captured)
         # (32 steps per graph: 27.9-29.9 M ex/s vs 26.7-28.0 M at 16, profiles/r4_seg_sort.md)
         ta.steps, ta.warmup, ta.steps_per_graph = max(2048, a.steps), max(128, a.warmup), 32
+        state = os.environ.get("ROCFM_BENCH_GPU_STATE", "0") == "1"  # diagnostics: device clocks / temperature
+        if state:
+            from rocfm.utils.gpu_state import snapshot
+            out[prefix + "gpu_before"] = snapshot()
         try:
             t = measure_tfrecord(ta, spec, hp, params, dev)
+            if state:
+                out[prefix + "gpu_after"] = snapshot()
             out[prefix + "steps"] = ta.steps
             for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
                       "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode",

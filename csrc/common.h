@@ -38,6 +38,7 @@ constexpr int kWave = 64;
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (4 VGPR), raw bits
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;  // 16-B buffer-store payload
 typedef __attribute__((ext_vector_type(16))) float f32x16;  // 32x32 MFMA accumulator
 
 // D = A(16x32) · B(32x16) + C.  Lane l holds A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15];

@@ -111,6 +111,9 @@ struct RowsParams {
   // arrival counters, zeroed once at allocation and never reset; xerr: set if an exchange wait
   // timed out (the host check raises; the counters must then be zeroed again).
   int split;
+  // write-through (sc1) stores of the kernel's large outputs, so that the launch leaves less dirty
+  // L2 to write back at its end: bit 0 the per-lookup gradient rows (contrib), bit 1 h0ᵀ (actT[0])
+  int wt;
   uint16_t* xbuf;
   unsigned* xctr;
   int* xerr;

@@ -316,6 +316,9 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
   const int rtile = G > 1 ? (int)((blockIdx.x / (8 * G)) * 8 + (blockIdx.x & 7)) : (int)blockIdx.x;
   const bool lead = mbr == 0;  // the member that stores the row tile's shared outputs
   const int row0 = rtile * RT;
+  // write-through store targets (RowsParams::wt): buffer descriptors over contrib / h0ᵀ
+  const __amdgpu_buffer_rsrc_t wt_contrib = __builtin_amdgcn_make_buffer_rsrc(p.contrib, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_h0 = __builtin_amdgcn_make_buffer_rsrc(p.actT[0], (short)0, 0x7fffffff, 0x00020000);
   // layer-0 dgrad tiles of this member: its fields' columns (all of dims[0] without the split)
   const int tb0 = G > 1 ? mbr * SH::T0B : 0;
   const int tb1 = G > 1 ? min(tb0 + SH::T0B, sh.dim(0) / 16) : sh.dim(0) / 16;
@@ -564,7 +567,12 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           w[j] = (uint32_t)h0[(h * 8 + 2 * j) * lda + c] | ((uint32_t)h0[(h * 8 + 2 * j + 1) * lda + c] << 16);
-        *reinterpret_cast<uint4*>(p.actT[0] + act_swz(c, row0 + h * 8, Bp)) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (p.wt & 2) {  // write-through (sc1): nothing of it left dirty in L2 at the kernel's end
+          const u32x4 v = {w[0], w[1], w[2], w[3]};
+          __builtin_amdgcn_raw_buffer_store_b128(v, wt_h0, (int)(act_swz(c, row0 + h * 8, Bp) * 2), 0, 16);
+        } else {
+          *reinterpret_cast<uint4*>(p.actT[0] + act_swz(c, row0 + h * 8, Bp)) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
       }
     } else {  // 4 rows × 1 column per item → one 8-B store
       for (int c = cb + t; c < ce; c += kRowThreads) {
@@ -1214,7 +1222,14 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     } else {
 #pragma unroll
       for (int u = 0; u < UF; ++u)
-        if (ok[u]) reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
+        if (ok[u]) {
+          if (p.wt & 1) {  // write-through (sc1)
+            const f32x4 v = {o[u][0], o[u][1], o[u][2], o[u][3]};
+            __builtin_amdgcn_raw_buffer_store_b128(v, wt_contrib, dst[u] * 16, 0, 16);
+          } else {
+            reinterpret_cast<float4*>(p.contrib)[dst[u]] = make_float4(o[u][0], o[u][1], o[u][2], o[u][3]);
+          }
+        }
     }
   }
   if (G == 1 && p.dedup) {

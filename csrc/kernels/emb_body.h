@@ -86,7 +86,14 @@ __device__ __forceinline__ void seg_scan_dpp(float4 (&v)[N], int lane, int seg) 
 // entries, so a chunk's run heads — its optimizer items, the scattered table / slot round trip
 // that bounds the slowest chunks — are spread over twice the CUs; the threads past kE load no
 // entry but take part in the end search, the continuation rounds and the optimizer items.
-template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk>
+// PRE (apply mode, EmbUpdateParams::hkeys from the side chain): the table / slot loads of every
+// thread's first 4 optimizer items are issued at the start, right behind the gradient rows, from
+// the chunk's run-head keys the side chain compacted — they fly under the scan, the head
+// compaction, the end search and the continuation instead of after them.  Every load of that
+// prologue is unconditional (clamped addresses, values selected afterwards), so the waits the
+// compiler places for the gradient rows never include them (profiles/r5_emb_prefetch_negative.md:
+// exec-masked prefetch loads did exactly that).
+template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk, bool PRE = false>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
   __shared__ float4 s_rows[kE * KP4];  // the chunk's entries only (threads past kE hold none): with the
@@ -136,7 +143,45 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   uint32_t key = 0xffffffffu, prevk = 0xffffffffu;
   bool head = false;
   float4 v[KH];
-  if (live_e) {
+  constexpr int kPU = 4;  // items per thread per round of step 6
+  float4 pw[PRE ? kPU : 1], pa[PRE ? kPU : 1], pb[PRE ? kPU : 1];
+  if constexpr (PRE) {
+    uint32_t hk[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) hk[u] = p.hkeys[(size_t)bid * kE + min((u * kChunk + t) / KP4, kE - 1)];
+    const int ic = min(i, n - 1);
+    const uint32_t k0 = p.skeys[ic], k1 = p.skeys[max(ic - 1, 0)];
+    const float4* src = reinterpret_cast<const float4*>(p.contrib + (size_t)ic * p.Kp);
+    float4 x[KH];
+#pragma unroll
+    for (int u = 0; u < KH; ++u) x[u] = src[min(half * KH + u, KP4 - 1)];
+    // the items' rows (slots past the chunk's heads hold stale keys: clamped, never used)
+    const float4* s0v = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb);
+    const float4* s1v = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb);
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int it = u * kChunk + t;
+      const uint32_t row = min((hk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride, p.rows - 1u);
+      const size_t idx = (size_t)row * KP4 + (it % KP4);
+      pw[u] = tbl_load4<BT>(p.emb, idx);
+      pa[u] = s0v[idx];
+      pb[u] = s1v[idx];
+    }
+    if (live_e) {
+      key = k0;
+      prevk = ic > 0 ? k1 : 0xffffffffu;
+      head = (i == 0) || (prevk != key);
+      const bool skip = p.max_key && key >= p.max_key;
+#pragma unroll
+      for (int u = 0; u < KH; ++u) {
+        const int c = half * KH + u;
+        v[u] = (skip || c >= KP4) ? make_float4(0.f, 0.f, 0.f, 0.f) : x[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < KH; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  } else if (live_e) {
     key = p.skeys[i];
     if (i > 0) prevk = p.skeys[i - 1];
     head = (i == 0) || (prevk != key);
@@ -289,6 +334,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   const int nitems = nh * KP4;
   if (push) push_wait_ready(p.push, push_seen);
   for (int base = 0; base < nitems; base += kChunk * 4) {
+#pragma clang fp contract(off)  // (the gradient scale and L2 terms: the same bits in every instantiation)
     float4 w[4], a[4], b[4], g[4];
     uint32_t kk[4];
     size_t idx4[4];
@@ -302,7 +348,12 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       const bool skip = p.max_key && kk[u] >= p.max_key;
       const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
       idx4[u] = row * KP4 + u4;
-      if (p.mode == 0) {  // issue the row's parameter + slot loads now
+      if (PRE && base == 0) {  // loaded at the start (step 1)
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        w[u] = pw[u];
+        a[u] = p.s0 ? pa[u] : z;
+        b[u] = p.s1 ? pb[u] : z;
+      } else if (p.mode == 0) {  // issue the row's parameter + slot loads now
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         w[u] = tbl_load4<BT>(p.emb, idx4[u]);
         a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;

@@ -69,6 +69,13 @@ struct EmbUpdateParams {
   int dir_nb;
   uint32_t dir_div;
   int push_off_dir;
+  // apply mode (nullable): this batch's per-chunk run-head keys from the side chain
+  // (SortAuxParams::chunk_hkeys, [nch][chunk] with chunk = the tail's entries per workgroup) and
+  // the table's row count (clamp for the slots past a chunk's heads): the step tail then issues
+  // the first optimizer items' table / slot loads beside the gradient rows (emb_body.h PRE).
+  // Needs sorted_contrib, and both slots or an f32 table.
+  const uint32_t* hkeys;
+  uint32_t rows;
 };
 
 struct EmbDenseParams {

@@ -50,6 +50,9 @@ __device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
 // In-place update of param p and slots s0/s1 with gradient g.
 __device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st, float& p, float g, float& s0,
                                           float& s1) {
+  // every operation rounded on its own (no FMA contraction): the update is then the same bits in
+  // every kernel that inlines it, whatever the surrounding code lets the compiler fuse
+#pragma clang fp contract(off)
   if (st.skip) return;
   switch (o.type) {
     case kAdam: {

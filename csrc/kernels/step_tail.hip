@@ -38,19 +38,36 @@ static int tail_cus() {
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
 static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
-template <int KP4, bool BT, bool PUSH, int kE>
+template <int KP4, bool BT, bool PUSH, int kE, bool PRE = false>
 __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                  const int n_emb) {
   const int bid = blockIdx.x;
   if (bid < n_emb)
-    emb_rows_body<KP4, kTailThreads, BT, PUSH, kE>(e, bid);  // the longer role first: its workgroups dispatch first
+    emb_rows_body<KP4, kTailThreads, BT, PUSH, kE, PRE>(e, bid);  // the longer role first: its workgroups dispatch first
   else
     wgrad_body<PUSH>(w, bid - n_emb);
+}
+
+// the embedding role's table-load prologue (emb_body.h PRE): apply mode with the side chain's
+// run-head keys, sorted gradient rows, and both optimizer slots or an f32 table (the missing
+// slots' loads then read the table as a stand-in)
+static bool tail_pre(const EmbUpdateParams& e) {
+  return e.mode == 0 && e.hkeys != nullptr && e.rows > 0 && e.sorted_contrib && e.n_dev == nullptr &&
+         (!e.tbl_bf16 || (e.s0 && e.s1));
 }
 
 template <int KP4, bool PUSH, int kE>
 static void launch_tail_e(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
                           hipStream_t stream) {
+  if constexpr (!PUSH) {
+    if (tail_pre(e)) {
+      if (e.tbl_bf16)
+        hipLaunchKernelGGL((step_tail_kernel<KP4, true, false, kE, true>), grid, block, 0, stream, w, e, n_emb);
+      else
+        hipLaunchKernelGGL((step_tail_kernel<KP4, false, false, kE, true>), grid, block, 0, stream, w, e, n_emb);
+      return;
+    }
+  }
   if (e.tbl_bf16)
     hipLaunchKernelGGL((step_tail_kernel<KP4, true, PUSH, kE>), grid, block, 0, stream, w, e, n_emb);
   else

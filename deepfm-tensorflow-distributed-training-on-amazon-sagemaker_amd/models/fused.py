@@ -387,6 +387,7 @@ class FusedDeepFM:
         rp.force_generic = 1 if self.force_generic else 0
         rp.fp8 = 1 if self.compute_dtype == "fp8" else 0
         rp.row_tile = self.row_tile
+        rp.wt = int(os.environ.get("ROCFM_WT", "0"))  # write-through row-kernel outputs (deepfm_rows.h wt)
         if self.row_split > 1:  # (the launcher keeps one workgroup per tile where the split does not apply)
             rp.split, rp.xbuf, rp.xctr, rp.xerr = 2, self.xbuf.data_ptr(), self.xctr.data_ptr(), self.xerr.data_ptr()
         self._set_w8(rp, 0)
@@ -809,6 +810,12 @@ class FusedDeepFM:
         self.m_chd = torch.zeros(2, Smax * self.m_nch, **i32) if heads else None
         # per-tile dedup (rows of ONE batch per row tile): group links, compacted keys and counts
         self.m_dedup = self.dedup and shard is None
+        # the keys of every tail chunk's run heads (sort_aux, side chain): the step tail's
+        # embedding role issues its first optimizer items' table loads from them at its start
+        # (emb_body.h PRE; apply mode — single-GPU steps — without the per-tile dedup)
+        self.m_hk = (torch.zeros(2, Smax * self.m_nch * self.m_chunk, **i32)
+                     if (not self.m_dedup and self.Kp <= self.H.tail_max_kp()
+                         and os.environ.get("ROCFM_TAIL_PREFETCH", "0") == "1") else None)
         if self.m_dedup:
             self.m_nxt = torch.zeros(2, Smax * n, **i32)
             self.m_ck = torch.zeros(2, Smax * n, **i32)
@@ -835,6 +842,9 @@ class FusedDeepFM:
                     rows.dedup = 0
                 if self.Kp <= self.H.tail_max_kp():  # the fused tail's 512-entry chunks
                     ep.chunk_end = self.m_cend[q, k * self.m_nch:].data_ptr()
+                if self.m_hk is not None and ep.mode == 0:
+                    ep.hkeys = self.m_hk[q, k * self.m_nch * self.m_chunk:].data_ptr()
+                    ep.rows = int(self.emb.shape[0])
         self._m_graphs = {}
         self._m_primed = False
         self._m_warm = 0
@@ -885,10 +895,12 @@ class FusedDeepFM:
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
         if self.m_chd is not None:
             a.chunk_heads = self.m_chd[1 - q].data_ptr()
+        if self.m_hk is not None:
+            a.chunk_hkeys = self.m_hk[1 - q].data_ptr()
         if self.m_keys64 is not None:  # sorted 64-bit keys → plain per-batch ids in m_sk
             a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
         if self.m_dedup:  # positions / run ends / run heads come from the dedup over the compacted list
-            a.chunk_end = a.chunk_heads = 0
+            a.chunk_end = a.chunk_heads = a.chunk_hkeys = 0
         if not (self.m_dedup and self.m_keys64 is None):  # (64-bit keys: sort_aux writes the plain ids)
             H.sort_aux(a, stream.cuda_stream)
         if self.m_dedup:
