@@ -132,3 +132,10 @@ def test_pyproject_packages_exist():
     on_disk = {os.path.relpath(r, src) for r, _, fs in os.walk(src) if "__init__.py" in fs and "__pycache__" not in r}
     listed = {os.path.join(*p.split(".")[1:]) if "." in p else "." for p in cfg["packages"]}
     assert on_disk == listed, (on_disk, listed)
+
+
+def test_gpu_state_snapshot_never_raises():
+    """utils/gpu_state.snapshot: a read-only diagnostic — a dict of numbers, {} without a GPU."""
+    from rocfm.utils.gpu_state import snapshot
+    s = snapshot()
+    assert isinstance(s, dict) and all(isinstance(v, (int, float)) for v in s.values())
