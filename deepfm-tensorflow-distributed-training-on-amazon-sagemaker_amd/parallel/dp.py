@@ -114,8 +114,11 @@ def search_dir_buckets(W: int, V: int) -> int:
 # also over RCCL; any other forced merge keeps it off).  tools/bench_merge.py, uncached p2p
 # memory: the step's apply 3.9 / 4.4 / 5.6 µs at W = 2 / 4 / 8 against 7.6 / 9.6 / 14.1 for the
 # best step-time merge, for 2.9 / 3.5 / 5.7 µs per step of plan building on the side chain of a
-# 16-step graph (profiles/r5_dp_plan_merge.md).
-PLAN_MIN_W = 2
+# 16-step graph (profiles/r5_dp_plan_merge.md).  Default only beyond 4 ranks, where the step-time
+# merge costs most (14 µs at W = 8): in the shared-GPU rehearsals (2 / 4 ranks on one GPU) the
+# merge phase shrank but the headline loop ran slower with the plan's extra per-graph id exchange,
+# and a shared GPU cannot say whether that carries over to one GPU per rank.
+PLAN_MIN_W = 5
 
 
 def plan_merge_enabled(W: int, exchange: str) -> bool:

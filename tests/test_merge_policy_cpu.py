@@ -19,13 +19,13 @@ def test_search_dir_buckets_policy(monkeypatch):
 
 
 def test_plan_merge_policy(monkeypatch):
-    """The plan-ahead merge: the default with the p2p exchange from PLAN_MIN_W (2) ranks; over RCCL
+    """The plan-ahead merge: the default with the p2p exchange from PLAN_MIN_W (5) ranks; over RCCL
     only when forced (ROCFM_MERGE=plan); any other forced merge keeps it off; one rank never."""
     from rocfm.parallel.dp import PLAN_MIN_W, plan_merge_enabled
     monkeypatch.delenv("ROCFM_MERGE", raising=False)
-    assert PLAN_MIN_W == 2
+    assert PLAN_MIN_W == 5
     assert not plan_merge_enabled(1, "p2p")
-    assert plan_merge_enabled(2, "p2p") and plan_merge_enabled(8, "p2p")
+    assert not plan_merge_enabled(4, "p2p") and plan_merge_enabled(8, "p2p")
     assert not plan_merge_enabled(8, "rccl")
     monkeypatch.setenv("ROCFM_MERGE", "plan")
     assert plan_merge_enabled(2, "rccl") and not plan_merge_enabled(1, "rccl")
