@@ -113,6 +113,12 @@ def main():
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # ROCFM_NUMA_BIND=1: this process's threads (and the loader threads it starts) on the CPUs of
+    # its GPU's NUMA node (utils/numa.py; profiles/r5_stream_queues.md)
+    numa_cpus = None
+    if os.environ.get("ROCFM_NUMA_BIND", "0") == "1":
+        from rocfm.utils.numa import bind_to_gpu_node
+        numa_cpus = bind_to_gpu_node(local)
     # ROCFM_FORCE_COLLECTIVES=1 (one process): a 1-rank process group whose exchanges still run the
     # backend's collectives (rehearses the RCCL calls the multi-GPU node captures)
     pg = world > 1 or os.environ.get("ROCFM_FORCE_COLLECTIVES", "0") == "1"
@@ -287,6 +293,7 @@ def main():
         "world_size": dist.get_world_size() if pg else 1,
         "backend": (dist.get_backend() if pg else None),
         "rank_ms_per_step": {"max": round(ms, 4), "min": round(dt_min / a.steps * 1e3, 4)},
+        "numa_bind_cpus": (len(numa_cpus) if numa_cpus else None),
         # self-validation (rocfm.parallel.validate): replicas bit-identical across ranks after the
         # timed steps; the p2p exchange's first steps checked bitwise against the collective
         "replicas_consistent": replicas_ok,

@@ -139,3 +139,14 @@ def test_gpu_state_snapshot_never_raises():
     from rocfm.utils.gpu_state import snapshot
     s = snapshot()
     assert isinstance(s, dict) and all(isinstance(v, (int, float)) for v in s.values())
+
+
+def test_numa_cpulist_and_binding_are_safe():
+    """utils/numa: sysfs cpulist parsing; without a GPU (or sysfs) nothing is bound."""
+    import os
+
+    from rocfm.utils.numa import _parse_cpulist, bind_to_gpu_node, gpu_local_cpus
+    assert _parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    before = os.sched_getaffinity(0)
+    if gpu_local_cpus() is None:
+        assert bind_to_gpu_node() is None and os.sched_getaffinity(0) == before
