@@ -113,10 +113,10 @@ def main():
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # ROCFM_NUMA_BIND=1: this process's threads (and the loader threads it starts) on the CPUs of
+    # ROCFM_NUMA_BIND (default 1): this process's threads (and the loader threads it starts) on the CPUs of
     # its GPU's NUMA node (utils/numa.py; profiles/r5_stream_queues.md)
     numa_cpus = None
-    if os.environ.get("ROCFM_NUMA_BIND", "0") == "1":
+    if os.environ.get("ROCFM_NUMA_BIND", "1") == "1":
         from rocfm.utils.numa import bind_to_gpu_node
         numa_cpus = bind_to_gpu_node(local)
     # ROCFM_FORCE_COLLECTIVES=1 (one process): a 1-rank process group whose exchanges still run the
