@@ -53,6 +53,12 @@ class Estimator:
         if device is None:
             device = torch.device("cuda", self.info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
         self.device = torch.device(device)
+        # host threads next to the GPU (the loader's reader / worker threads and the pinned staging
+        # buffers they first touch): the GPU's NUMA node, unless ROCFM_NUMA_BIND=0 (utils/numa.py,
+        # profiles/r5_stream_queues.md)
+        if self.device.type == "cuda" and os.environ.get("ROCFM_NUMA_BIND", "1") == "1":
+            from .utils.numa import bind_to_gpu_node
+            bind_to_gpu_node(self.device.index or 0)
         self.spec = ModelSpec.from_config(cfg)
         self.world = _world()
         self.hp = OptHParams(name=cfg.optimizer, lr=cfg.learning_rate)
