@@ -586,7 +586,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
             out[prefix + "steps"] = ta.steps
             for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
                       "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode",
-                      "copy_stream_ms_per_group", "copy_stream_GBps", "copy_stream_busy_fraction"):
+                      "copy_stream_ms_per_group", "copy_stream_GBps", "copy_stream_busy_fraction",
+                      "copy_stream_h2d_ms_per_group", "copy_stream_parse_ms_per_group", "copy_stream_h2d_GBps"):
                 out[prefix + ("examples_per_sec" if k == "value" else k)] = t.get(k)
         except Exception as e:  # a secondary window never costs the headline
             out[prefix + "error"] = f"{type(e).__name__}: {e}"[:400]
@@ -862,10 +863,14 @@ def measure_tfrecord(a, spec, hp, params, dev):
         ms = g0[1].elapsed_time(g1[1])
         steady = (g1[2] - g0[2]) * B / (ms * 1e-3) if ms > 0 else None
     value = B * a.steps / dt
-    ct = [(x[0].elapsed_time(x[1]), x[2], x[3]) for x in eng.copy_timing]
+    ct = [(x[0].elapsed_time(x[1]), x[2], x[3], x[0].elapsed_time(x[4])) for x in eng.copy_timing]
     eng.copy_timing = None
     copy_ms = sum(c[0] for c in ct)
+    h2d_ms = sum(c[3] for c in ct)
     out_copy = {"copy_stream_ms_per_group": round(copy_ms / max(len(ct), 1), 3),
+                "copy_stream_h2d_ms_per_group": round(h2d_ms / max(len(ct), 1), 3),
+                "copy_stream_parse_ms_per_group": round((copy_ms - h2d_ms) / max(len(ct), 1), 3),
+                "copy_stream_h2d_GBps": round(sum(c[1] for c in ct) / max(h2d_ms, 1e-9) / 1e6, 2),
                 "copy_stream_GBps": round(sum(c[1] for c in ct) / max(copy_ms, 1e-9) / 1e6, 2),
                 "copy_stream_busy_fraction": round(copy_ms / (dt * 1e3), 3)} if ct else {}
     out = {

@@ -1223,7 +1223,7 @@ class FusedDeepFM:
                     if timing is not None:
                         t1 = torch.cuda.Event(enable_timing=True)
                         t1.record(copy)
-                        timing.append((t0, t1, int(b.used_bytes()), n))
+                        timing.append((t0, t1, int(b.used_bytes()), n, self._copy_mid))
                     self._pl_op("copy", f"raw stage of batches {staged}..{staged + n - 1}",
                                 self._pl_ring(0, n, True, slot0=staged % R) + [("raw_stage", 0, 1, True)])
                     pending.append((mark(copy), b))
@@ -1325,6 +1325,9 @@ class FusedDeepFM:
         used = g.used_bytes()
         d_bytes[:used].copy_(g.bytes.reshape(-1)[:used], non_blocking=True)
         d_offs[:n].copy_(g.offs, non_blocking=True)
+        if getattr(self, "copy_timing", None) is not None:  # diagnostics: H2D | parse split
+            self._copy_mid = torch.cuda.Event(enable_timing=True)
+            self._copy_mid.record(torch.cuda.current_stream(self.device))
         p = H.DecodeParams()
         p.bytes, p.offs, p.cap, p.nb, p.B, p.F = d_bytes.data_ptr(), d_offs.data_ptr(), cap, n, self.B, self.F
         ring = self._stream_ring
