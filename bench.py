@@ -289,6 +289,8 @@ def main():
             "hot_rows": a.hot_rows if parallelism == "rowshard" else None,
             "exchange": getattr(eng, "exchange", None) if pg else None,
             "fused_push": bool(getattr(eng, "fused_push", False)) if pg else None,
+            # the planned step tail (emb_plan.hip): embedding workgroups per step, or null (fixed chunks)
+            "emb_plan_workgroups": (getattr(eng, "m_plan_nw", None) if getattr(eng, "m_eplan", False) else None),
         },
         "world_size": dist.get_world_size() if pg else 1,
         "backend": (dist.get_backend() if pg else None),
@@ -394,6 +396,10 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
 
     * ``rccl``: the same DP step with the exchange on RCCL (all-gather captured in the graphs), the
       transport A/B of the node;
+    * ``merge_plan`` / ``merge_noplan``: the headline's DP step with the plan-ahead row merge forced
+      on / off (``ROCFM_MERGE``), and ``push_copy``: with the copy push instead of the fused producer
+      push (``ROCFM_DP_PUSH=0``), each with ``phase_ms`` — the A/Bs behind ``dp.PLAN_MIN_W`` and the
+      push default;
     * ``rowshard``: config 4 — the PS-equivalent row-sharded table at 100M rows
       (``…multiInstance.py:461-521``), p2p all-to-alls.
     Every window reports its own replica check and p2p shadow status."""
@@ -402,11 +408,13 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
     S = a.steps_per_graph
     B = a.batch_size
 
-    def run_window(name, build):
+    def run_window(name, build, env=None, phases=False):
         wd.window = name
         err = None
         res = {}
         eng = None
+        saved = {k: os.environ.get(k) for k in (env or {})}
+        os.environ.update(env or {})
         try:
             eng = build()
             eng.attach_pool(*pool)
@@ -432,9 +440,19 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
                    "shadow_exchange": eng.shadow.status if getattr(eng, "shadow", None) is not None else None,
                    "exchange": getattr(eng, "exchange", None),
                    "fused_push": bool(getattr(eng, "fused_push", False))}
+            if phases:  # per-rank device phase times (diagnostic, after the timed steps)
+                try:
+                    res["phase_ms"] = eng.phase_windows(64, S)
+                except Exception as e:  # noqa: BLE001
+                    res["phase_ms_error"] = f"{type(e).__name__}: {e}"[:300]
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"[:300]
         finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
             if eng is not None and hasattr(eng, "close"):
                 try:
                     eng.close()
@@ -455,6 +473,16 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
     cap = pool_exchange_capacity(pool_ids, 1)
     run_window("rccl", lambda: FusedDataParallel(spec, hp, B, dev, params=params, mode="dp", seed=a.seed,
                                                  capacity=cap, compute_dtype=a.compute_dtype, exchange="rccl"))
+
+    # the headline's DP step with each row merge and each push form, every one with its phase times:
+    # the node's measurement behind PLAN_MIN_W (dp.py) and the fused push default (p2p.py)
+    def dp_default():
+        return FusedDataParallel(spec, hp, B, dev, params=params, mode="dp", seed=a.seed, capacity=cap,
+                                 compute_dtype=a.compute_dtype, exchange=a.dp_exchange)
+
+    run_window("merge_plan", dp_default, env={"ROCFM_MERGE": "plan"}, phases=True)
+    run_window("merge_noplan", dp_default, env={"ROCFM_MERGE": "noplan"}, phases=True)
+    run_window("push_copy", dp_default, env={"ROCFM_DP_PUSH": "0"}, phases=True)
     from rocfm.data.synthetic import SyntheticCriteo
     from rocfm.models.deepfm import ModelSpec
 
@@ -587,7 +615,8 @@ def secondary_windows(a, spec, hp, params, dev, pool):
             for k in ("value", "ms_per_step", "steady_examples_per_sec", "fill_ms", "input_stall_fraction",
                       "loader_alone_examples_per_sec", "host_decode_loader_alone_examples_per_sec", "decode",
                       "copy_stream_ms_per_group", "copy_stream_GBps", "copy_stream_busy_fraction",
-                      "copy_stream_h2d_ms_per_group", "copy_stream_parse_ms_per_group", "copy_stream_h2d_GBps"):
+                      "copy_stream_h2d_ms_per_group", "copy_stream_parse_ms_per_group", "copy_stream_h2d_GBps",
+                      "gpu_stall_fraction", "gpu_side_stall_fraction", "gpu_main_busy_fraction", "host_copy_wait_s"):
                 out[prefix + ("examples_per_sec" if k == "value" else k)] = t.get(k)
         except Exception as e:  # a secondary window never costs the headline
             out[prefix + "error"] = f"{type(e).__name__}: {e}"[:400]
@@ -834,6 +863,8 @@ def measure_tfrecord(a, spec, hp, params, dev):
             yield x
 
     eng.copy_timing = []  # per raw group: H2D copy + device parse on the copy stream
+    eng.stall_timing = []  # per graph: main start / main end / side end (GPU-side gaps of the main stream)
+    eng.host_copy_wait_s = 0.0  # host time blocked on copy completions (a ring slot's host memory recycled)
     marks = []  # (host time, event) after each graph launch
 
     def after(first, n):
@@ -865,6 +896,24 @@ def measure_tfrecord(a, spec, hp, params, dev):
     value = B * a.steps / dt
     ct = [(x[0].elapsed_time(x[1]), x[2], x[3], x[0].elapsed_time(x[4])) for x in eng.copy_timing]
     eng.copy_timing = None
+    # GPU-side stall: the main stream's gaps between consecutive graphs (graph j may start only once
+    # graph j-1 AND side graph j-1 — the sort of its batches, behind their H2D copy — are done, and the
+    # host has submitted it); the part of each gap spent waiting for the side chain is its side stall
+    stt, eng.stall_timing = eng.stall_timing, None
+    gpu_stall = {}
+    if len(stt) > 2:
+        gap = side = busy = 0.0
+        for j in range(1, len(stt)):
+            s0, e0, d0 = stt[j - 1]
+            s1, e1, _ = stt[j]
+            g = e0.elapsed_time(s1)  # main end j-1 → main start j
+            gap += max(0.0, g)
+            side += min(max(0.0, g), max(0.0, e0.elapsed_time(d0)))
+            busy += s1.elapsed_time(e1)
+        span = stt[0][0].elapsed_time(stt[-1][1])
+        gpu_stall = {"gpu_stall_fraction": round(gap / span, 4), "gpu_side_stall_fraction": round(side / span, 4),
+                     "gpu_main_busy_fraction": round(busy / span, 4),
+                     "host_copy_wait_s": round(getattr(eng, "host_copy_wait_s", 0.0), 4)}
     copy_ms = sum(c[0] for c in ct)
     h2d_ms = sum(c[3] for c in ct)
     out_copy = {"copy_stream_ms_per_group": round(copy_ms / max(len(ct), 1), 3),
@@ -898,6 +947,7 @@ def measure_tfrecord(a, spec, hp, params, dev):
         "world_size": 1, "backend": None,
     }
     out.update(out_copy)
+    out.update(gpu_stall)
     if own:
         shutil.rmtree(d, ignore_errors=True)
     return out

@@ -11,13 +11,14 @@ Two Python extension modules are produced next to the package sources:
   fixed-schema Example decoder, multi-threaded prefetching batch loader, libsvm converter).
   Built with g++ so it works on CPU-only machines too.
 
-Usage: ``python build.py [--force] [-j N]``.  Incremental: objects are rebuilt only when a source
-or any header under csrc/ is newer.
+Usage: ``python build.py [--force] [-j N]``.  Incremental: an object is rebuilt only when its source or
+one of the headers it includes (transitively) is newer.
 """
 import argparse
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -38,17 +39,37 @@ def _py_includes():
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
 
 
-def _newest_header():
-    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
-    hs += glob.glob(os.path.join(CSRC, "**", "*.inc"), recursive=True)
-    return max((os.path.getmtime(h) for h in hs), default=0.0)
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
 
 
-def _stale(obj, src, hdr_time):
+def _deps(src, seen=None):
+    """The quoted headers a source includes, transitively (resolved next to the includer, then
+    under csrc/): an object is rebuilt only when one of ITS headers changed."""
+    seen = set() if seen is None else seen
+    try:
+        text = open(src, encoding="utf-8", errors="replace").read()
+    except OSError:
+        return seen
+    for name in _INC.findall(text):
+        for cand in (os.path.join(os.path.dirname(src), name), os.path.join(CSRC, name)):
+            cand = os.path.normpath(cand)
+            if os.path.exists(cand):
+                if cand not in seen:
+                    seen.add(cand)
+                    _deps(cand, seen)
+                break
+    return seen
+
+
+def _newest_header(src):
+    return max((os.path.getmtime(h) for h in _deps(src)), default=0.0)
+
+
+def _stale(obj, src):
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    return t < os.path.getmtime(src) or t < hdr_time
+    return t < os.path.getmtime(src) or t < _newest_header(src)
 
 
 def _run(cmd):
@@ -60,7 +81,6 @@ def _run(cmd):
 
 def hip_objects(force, jobs):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + [os.path.join(CSRC, "hip_module.cpp")]
-    hdr = _newest_header()
     os.makedirs(BUILD, exist_ok=True)
     base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", CSRC,
             "-Wno-unused-result", "-munsafe-fp-atomics"]
@@ -68,7 +88,7 @@ def hip_objects(force, jobs):
     for s in srcs:
         o = os.path.join(BUILD, "hip_" + os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _stale(o, s, hdr):
+        if force or _stale(o, s):
             extra = []
             if s.endswith(".cpp"):
                 extra = ["-x", "hip"] + sum((["-I", p] for p in _py_includes()), [])
@@ -82,7 +102,6 @@ def hip_objects(force, jobs):
 
 def io_objects(force, jobs):
     srcs = sorted(glob.glob(os.path.join(CSRC, "io", "*.cpp")))
-    hdr = _newest_header()
     os.makedirs(BUILD, exist_ok=True)
     base = [CXX, "-O3", "-fPIC", "-std=c++17", "-msse4.2", "-pthread", "-I", CSRC]
     base += sum((["-I", p] for p in _py_includes()), [])
@@ -90,7 +109,7 @@ def io_objects(force, jobs):
     for s in srcs:
         o = os.path.join(BUILD, "io_" + os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _stale(o, s, hdr):
+        if force or _stale(o, s):
             todo.append(base + ["-c", s, "-o", o])
     with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, todo))

@@ -92,10 +92,6 @@ struct SortAuxParams {
   // nullable: [S][ceil(n / chunk)] run heads per chunk (the sorted DP export's output bases,
   // EmbUpdateParams::chunk_heads); chunk must be a multiple of 64 and at most 1024
   int32_t* chunk_heads;
-  // nullable: [S][ceil(n / chunk) · chunk] the keys of each chunk's run heads, in order (slots past
-  // the chunk's head count untouched) — the step tail's embedding role issues the table rows'
-  // loads from them at its start (EmbUpdateParams::hkeys)
-  uint32_t* chunk_hkeys;
 };
 void launch_sort_aux(const SortAuxParams& p, hipStream_t stream);
 

@@ -143,8 +143,7 @@ __global__ __launch_bounds__(256) void sort_aux_kernel(const SortAuxParams p) {
   }
 }
 
-// One workgroup of `chunk` threads per (batch, chunk): run heads of the chunk (ballot counts) and,
-// with chunk_hkeys, their keys compacted in order.
+// One workgroup of `chunk` threads per (batch, chunk): run heads of the chunk (ballot counts).
 __global__ __launch_bounds__(1024) void chunk_heads_kernel(const SortAuxParams p, int nch) {
   __shared__ int s_w[16];
   const int k = blockIdx.y, c = blockIdx.x, t = threadIdx.x;
@@ -155,12 +154,6 @@ __global__ __launch_bounds__(1024) void chunk_heads_kernel(const SortAuxParams p
   const unsigned long long m = __ballot(head);
   if ((t & 63) == 0) s_w[t >> 6] = __popcll(m);
   __syncthreads();
-  if (p.chunk_hkeys != nullptr && head) {
-    int base = 0;
-    for (int w = 0; w < (t >> 6); ++w) base += s_w[w];
-    const int before = __popcll(m & ((1ull << (t & 63)) - 1ull));
-    p.chunk_hkeys[((size_t)k * nch + c) * p.chunk + base + before] = key;
-  }
   if (p.chunk_heads != nullptr && t == 0) {
     int h = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) h += s_w[w];
@@ -175,7 +168,7 @@ void launch_sort_aux(const SortAuxParams& p, hipStream_t stream) {
   const long long total = std::max<long long>((long long)p.S * p.n, (long long)p.S * ((p.n + p.chunk - 1) / p.chunk));
   hipLaunchKernelGGL(sort_aux_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, p);
   ROCFM_HIP_CHECK(hipGetLastError());
-  if (p.chunk_heads || p.chunk_hkeys) {  // after sort_aux: the 64-bit path reads the plain ids it wrote
+  if (p.chunk_heads) {  // after sort_aux: the 64-bit path reads the plain ids it wrote
     ROCFM_REQUIRE(p.chunk % 64 == 0 && p.chunk <= 1024, "sort_aux: chunk_heads needs chunk % 64 == 0, <= 1024");
     const int nch = (p.n + p.chunk - 1) / p.chunk;
     hipLaunchKernelGGL(chunk_heads_kernel, dim3(nch, p.S), dim3(p.chunk), 0, stream, p, nch);

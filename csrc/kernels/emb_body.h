@@ -86,19 +86,12 @@ __device__ __forceinline__ void seg_scan_dpp(float4 (&v)[N], int lane, int seg) 
 // entries, so a chunk's run heads — its optimizer items, the scattered table / slot round trip
 // that bounds the slowest chunks — are spread over twice the CUs; the threads past kE load no
 // entry but take part in the end search, the continuation rounds and the optimizer items.
-// PRE (apply mode, EmbUpdateParams::hkeys from the side chain): the table / slot loads of every
-// thread's first 4 optimizer items are issued at the start, right behind the gradient rows, from
-// the chunk's run-head keys the side chain compacted — they fly under the scan, the head
-// compaction, the end search and the continuation instead of after them.  Every load of that
-// prologue is unconditional (clamped addresses, values selected afterwards), so the waits the
-// compiler places for the gradient rows never include them (profiles/r5_emb_prefetch_negative.md:
-// exec-masked prefetch loads did exactly that).
-template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk, bool PRE = false>
+template <int KP4, int kChunk, bool BT = false, bool PUSH = false, int kE = kChunk>
 __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const int bid) {
   constexpr int kWaves = kChunk / 64;
   __shared__ float4 s_rows[kE * KP4];  // the chunk's entries only (threads past kE hold none): with the
                                        // fused tail's kE = 256 two 512-thread workgroups fit a CU at Kp = 36
-  __shared__ float4 s_cont[kWaves * KP4];
+  __shared__ float4 s_cont[2 * kWaves * KP4];  // continuation: one round's window pieces, then the fold
   __shared__ int s_head[kChunk + 1];
   __shared__ uint32_t s_hkey[kChunk + 1];
   __shared__ uint32_t s_hprev[kChunk + 1];  // sorted export directory: key of the entry before each head
@@ -143,45 +136,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   uint32_t key = 0xffffffffu, prevk = 0xffffffffu;
   bool head = false;
   float4 v[KH];
-  constexpr int kPU = 4;  // items per thread per round of step 6
-  float4 pw[PRE ? kPU : 1], pa[PRE ? kPU : 1], pb[PRE ? kPU : 1];
-  if constexpr (PRE) {
-    uint32_t hk[kPU];
-#pragma unroll
-    for (int u = 0; u < kPU; ++u) hk[u] = p.hkeys[(size_t)bid * kE + min((u * kChunk + t) / KP4, kE - 1)];
-    const int ic = min(i, n - 1);
-    const uint32_t k0 = p.skeys[ic], k1 = p.skeys[max(ic - 1, 0)];
-    const float4* src = reinterpret_cast<const float4*>(p.contrib + (size_t)ic * p.Kp);
-    float4 x[KH];
-#pragma unroll
-    for (int u = 0; u < KH; ++u) x[u] = src[min(half * KH + u, KP4 - 1)];
-    // the items' rows (slots past the chunk's heads hold stale keys: clamped, never used)
-    const float4* s0v = reinterpret_cast<const float4*>(p.s0 ? p.s0 : p.emb);
-    const float4* s1v = reinterpret_cast<const float4*>(p.s1 ? p.s1 : p.emb);
-#pragma unroll
-    for (int u = 0; u < kPU; ++u) {
-      const int it = u * kChunk + t;
-      const uint32_t row = min((hk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride, p.rows - 1u);
-      const size_t idx = (size_t)row * KP4 + (it % KP4);
-      pw[u] = tbl_load4<BT>(p.emb, idx);
-      pa[u] = s0v[idx];
-      pb[u] = s1v[idx];
-    }
-    if (live_e) {
-      key = k0;
-      prevk = ic > 0 ? k1 : 0xffffffffu;
-      head = (i == 0) || (prevk != key);
-      const bool skip = p.max_key && key >= p.max_key;
-#pragma unroll
-      for (int u = 0; u < KH; ++u) {
-        const int c = half * KH + u;
-        v[u] = (skip || c >= KP4) ? make_float4(0.f, 0.f, 0.f, 0.f) : x[u];
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < KH; ++u) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  } else if (live_e) {
+  if (live_e) {
     key = p.skeys[i];
     if (i > 0) prevk = p.skeys[i - 1];
     head = (i == 0) || (prevk != key);
@@ -291,40 +246,53 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
   __syncthreads();
   ROCFM_STAMP(p.stamps, 2);
   if (t == 0) s_head[nh] = min(s_last_end, cend);
-  // 5. continuation of the last run past the chunk: full reductions over following chunks
+  // 5. continuation of the last run past the chunk.  A run's sum is, everywhere, the left-to-right
+  //    fold from 0 of its window pieces — the segmented scan of each 64-entry window of the sorted
+  //    list (aligned to the list) at the run's last entry in that window — so the planned tail
+  //    (emb_plan_body.h), which cuts the list elsewhere and combines split runs across workgroups,
+  //    gets the same bits.  Threads t < KP4 hold the fold: first the run's in-chunk pieces, then
+  //    every following window's piece in order (each wave scans 2 windows per round).
   const int last_end = s_last_end;
   const bool cont = last_end > cend && !(p.max_key && s_hkey[nh - 1] >= p.max_key);
   if (cont) {
-    // every thread sums its own entries of the following chunks (two chunks' loads in flight per
-    // round, no cross-lane work inside the loop), then ONE butterfly per float4 column: the hot
-    // runs (ids present in every example: 1,024-entry runs) cost two load latencies, not a
-    // reduction per 512 entries
-    float4 tot[KP4];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < KP4) {
+      const int s = s_head[nh - 1], e = s_head[nh];
+      for (int ww = (s - c0) >> 6; ww <= (e - 1 - c0) >> 6; ++ww)
+        acc = f4add(acc, s_rows[(min(e, c0 + 64 * (ww + 1)) - 1 - c0) * KP4 + t]);
+    }
+    constexpr int kNW = 2;  // windows per wave per round
+    for (int w0 = cend; w0 < last_end; w0 += kNW * kChunk) {
+      float4 x[kNW][KP4];
 #pragma unroll
-    for (int u = 0; u < KP4; ++u) tot[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k0 = cend; k0 < last_end; k0 += 2 * kChunk) {
-      float4 w[2][KP4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = k0 + h * kChunk + t;
+      for (int h = 0; h < kNW; ++h) {
+        const int j = w0 + (h * kWaves + wave) * 64 + lane;
         if (j < last_end) {
           const float4* src = p.sorted_contrib ? reinterpret_cast<const float4*>(p.contrib + (size_t)j * p.Kp)
                                                : contrib_row4(p, p.svals[j] - p.val_base);
 #pragma unroll
-          for (int u = 0; u < KP4; ++u) w[h][u] = src[u];
+          for (int u = 0; u < KP4; ++u) x[h][u] = src[u];
         } else {
 #pragma unroll
-          for (int u = 0; u < KP4; ++u) w[h][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int u = 0; u < KP4; ++u) x[h][u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
 #pragma unroll
-      for (int u = 0; u < KP4; ++u) tot[u] = f4add(tot[u], f4add(w[0][u], w[1][u]));
-    }
-    seg_scan_dpp(tot, lane, 0);  // lane 63: the wave's total
-    if (lane == 63) {
+      for (int h = 0; h < kNW; ++h) {
+        seg_scan_dpp(x[h], lane, 0);
+        const int ws = w0 + (h * kWaves + wave) * 64;  // this window's piece ends at the run's last entry in it
+        if (ws < last_end && lane == min(63, last_end - 1 - ws)) {
 #pragma unroll
-      for (int u = 0; u < KP4; ++u) s_cont[wave * KP4 + u] = tot[u];
+          for (int u = 0; u < KP4; ++u) s_cont[(h * kWaves + wave) * KP4 + u] = x[h][u];
+        }
+      }
+      __syncthreads();
+      if (t < KP4) {
+        for (int q = 0; q < kNW * kWaves && w0 + q * 64 < last_end; ++q) acc = f4add(acc, s_cont[q * KP4 + t]);
+      }
+      __syncthreads();
     }
+    if (t < KP4) s_cont[t] = acc;  // the run's whole fold
   }
   __syncthreads();
   ROCFM_STAMP(p.stamps, 3);
@@ -348,12 +316,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       const bool skip = p.max_key && kk[u] >= p.max_key;
       const size_t row = skip ? 0 : (size_t)((kk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride);
       idx4[u] = row * KP4 + u4;
-      if (PRE && base == 0) {  // loaded at the start (step 1)
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        w[u] = pw[u];
-        a[u] = p.s0 ? pa[u] : z;
-        b[u] = p.s1 ? pb[u] : z;
-      } else if (p.mode == 0) {  // issue the row's parameter + slot loads now
+      if (p.mode == 0) {  // issue the row's parameter + slot loads now
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         w[u] = tbl_load4<BT>(p.emb, idx4[u]);
         a[u] = p.s0 ? reinterpret_cast<const float4*>(p.s0)[idx4[u]] : z;
@@ -366,14 +329,14 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
       const int r = it / KP4, u4 = it - r * KP4;
       const int s = s_head[r], e = s_head[r + 1];  // piece inside this chunk: [s, e)
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
-      for (int ww = w0; ww <= w1; ++ww) {
-        const int lastw = min(e, c0 + 64 * (ww + 1)) - 1 - c0;
-        acc = f4add(acc, s_rows[lastw * KP4 + u4]);
-      }
       if (cont && r == nh - 1) {
-#pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) acc = f4add(acc, s_cont[ww * KP4 + u4]);
+        acc = s_cont[u4];  // the fold of step 5
+      } else {
+        const int w0 = (s - c0) >> 6, w1 = (e - 1 - c0) >> 6;
+        for (int ww = w0; ww <= w1; ++ww) {
+          const int lastw = min(e, c0 + 64 * (ww + 1)) - 1 - c0;
+          acc = f4add(acc, s_rows[lastw * KP4 + u4]);
+        }
       }
       g[u] = make_float4(acc.x * p.grad_scale, acc.y * p.grad_scale, acc.z * p.grad_scale, acc.w * p.grad_scale);
     }
@@ -443,7 +406,7 @@ __device__ __forceinline__ void emb_rows_body(const EmbUpdateParams& p, const in
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           if (u4 * 4 + c >= p.K1) continue;  // padding columns keep their (zero) values
-          opt_apply(p.opt, st, wc[c], gc[c] + p.l2 * wc[c], ac[c], bc[c]);
+          opt_apply(p.opt, st, wc[c], l2_grad(gc[c], p.l2, wc[c]), ac[c], bc[c]);
         }
         tbl_store4<BT>(p.emb, idx4[u], w[u], p.step ? (uint32_t)*p.step : 0u);
         if (p.s0) reinterpret_cast<float4*>(p.s0)[idx4[u]] = a[u];

@@ -69,14 +69,38 @@ struct EmbUpdateParams {
   int dir_nb;
   uint32_t dir_div;
   int push_off_dir;
-  // apply mode (nullable): this batch's per-chunk run-head keys from the side chain
-  // (SortAuxParams::chunk_hkeys, [nch][chunk] with chunk = the tail's entries per workgroup) and
-  // the table's row count (clamp for the slots past a chunk's heads): the step tail then issues
-  // the first optimizer items' table / slot loads beside the gradient rows (emb_body.h PRE).
-  // Needs sorted_contrib, and both slots or an f32 table.
-  const uint32_t* hkeys;
-  uint32_t rows;
+  // apply mode, planned step tail (emb_plan.hip; nullable): this batch's work plan from the side
+  // chain — plan_nw items {es, ee, lead slot, tail slot} (one per embedding workgroup) and the
+  // split-run slots {key, first non-head window, last window, pieces}.  The shared combine state:
+  // plan_win [n/64 + 1][Kp] window pieces, plan_head [plan_nw][Kp] head-item folds, plan_ctr
+  // [plan_nw] arrival counters (zero between launches: the last arrival resets its slot)
+  const int4* plan_items;
+  const int4* plan_slots;
+  int plan_nw;
+  float* plan_win;
+  float* plan_head;
+  uint32_t* plan_ctr;
 };
+
+// The step tail's embedding work plan (emb_plan.hip), built on the side chain for every batch of
+// the next multi-step graph.  The sorted lookups are cut into plan_nw contiguous items of equal cost
+// (an entry costs 1, a run head `beta` more: its table / Adam-slot round trip), at run heads or —
+// inside runs longer than `lsplit` — at 64-entry window boundaries.  A run cut that way is "split":
+// every item holding a part of it publishes its window pieces (the head item its fold of them) and
+// the last item to arrive sums them in window order and applies the optimizer, so the result is the
+// same left-to-right fold of window pieces that the unplanned update computes (emb_body.h).
+struct EmbPlanParams {
+  const uint32_t* skeys;  // [S][n] sorted keys, one segment per batch
+  int n, S, nw;           // lookups per batch, batches, items per batch (= tail embedding workgroups)
+  int beta, lsplit;       // cost of a run head (in entries); shortest run that may be split
+  int32_t* runs;          // scratch [S][n + 1]
+  int4* items;            // [S][nw]
+  int4* slots;            // [S][nw]
+};
+void launch_emb_plan(const EmbPlanParams& p, hipStream_t stream);
+// the planned tail's bounds (emb_plan_body.h): run heads and window pieces per item
+constexpr int kPlanHcap = 264;
+constexpr int kPlanPcap = kPlanHcap + 48;
 
 struct EmbDenseParams {
   float* emb;

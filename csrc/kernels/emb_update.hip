@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(const EmbDensePar
     float* bp = &b.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], gp[u] * p.grad_scale + p.l2 * wp[u], ap[u], bp[u]);
+      if (c0 + u < p.K1) opt_apply(p.opt, st, wp[u], l2_grad(gp[u] * p.grad_scale, p.l2, wp[u]), ap[u], bp[u]);
     tbl_store4_rt(p.emb, i, w, stp, bf);
     if (has_g) G[i] = make_float4(0, 0, 0, 0);
     if (A) A[i] = a;

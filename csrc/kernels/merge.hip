@@ -262,7 +262,7 @@ __device__ __forceinline__ void merge_maps_body(const MergeParams& p, const int 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (c * 4 + u >= p.K1) continue;
-      opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
+      opt_apply(p.opt, st, wc[u], l2_grad(gc[u] * p.grad_scale, p.l2, wc[u]), ac[u], bc[u]);
     }
     tbl_store4_rt(p.emb, base + c, w[c], (uint32_t)*p.step, p.tbl_bf16 != 0);
     if (a4) a4[c] = a[c];
@@ -321,7 +321,7 @@ __device__ __forceinline__ void merged_row_out(const MergeParams& p, uint32_t ro
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (c * 4 + u >= p.K1) continue;
-      opt_apply(p.opt, st, wc[u], gc[u] * p.grad_scale + p.l2 * wc[u], ac[u], bc[u]);
+      opt_apply(p.opt, st, wc[u], l2_grad(gc[u] * p.grad_scale, p.l2, wc[u]), ac[u], bc[u]);
     }
     tbl_store4_rt(p.emb, base + c, w[c], (uint32_t)*p.step, p.tbl_bf16 != 0);
     if (a4) a4[c] = a[c];
@@ -499,7 +499,7 @@ __device__ __forceinline__ void hot_apply_body(const HotApplyParams& h, const in
     for (int u = 0; u < 4; ++u) {
       if (c * 4 + u >= h.K1) continue;
       const float g = has ? gc[u] * h.grad_scale : 0.f;
-      opt_apply(h.opt, st, wc[u], g + h.l2 * wc[u], ac[u], bc[u]);
+      opt_apply(h.opt, st, wc[u], l2_grad(g, h.l2, wc[u]), ac[u], bc[u]);
     }
     reinterpret_cast<float4*>(h.rows)[at] = w;
     if (h.s0) reinterpret_cast<float4*>(h.s0)[at] = a;

@@ -145,7 +145,10 @@ template <int KP4, int WMAX>
 __device__ __forceinline__ void plan_apply_body(const MergeParams& p, const PlanStep& ps, const int u) {
   if (u >= *ps.count) return;
   const uint32_t row = ps.rows[u] / p.key_div;
-  if (row >= p.Vmap) return;  // (never: every plan id is a table row; a bad plan must not write past the table)
+  if (row >= p.Vmap) {  // (never: every plan id is a table row) a bad plan writes nothing past the table and
+    if (p.overflow) atomicOr(p.overflow, 2);  // raises at check(): its gradients were not applied
+    return;
+  }
   const int32_t* pp = ps.pos + (size_t)u * p.W;
   const int W = p.W;
   const size_t base = (size_t)row * KP4;
@@ -229,7 +232,7 @@ __device__ __forceinline__ void plan_apply_body(const MergeParams& p, const Plan
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (c * 4 + e >= p.K1) continue;
-      opt_apply(p.opt, st, wc[e], gc[e] * p.grad_scale + p.l2 * wc[e], ac[e], bc[e]);
+      opt_apply(p.opt, st, wc[e], l2_grad(gc[e] * p.grad_scale, p.l2, wc[e]), ac[e], bc[e]);
     }
     tbl_store4_rt(p.emb, base + c, w[c], (uint32_t)*p.step, p.tbl_bf16 != 0);
     if (a4) a4[c] = a[c];

@@ -47,32 +47,38 @@ __device__ __forceinline__ OptStep opt_step(const OptParams& o, int64_t step) {
   return s;
 }
 
+// The gradient every embedding-row update feeds opt_apply: g + λ·w as ONE explicit fused
+// multiply-add, so every kernel that applies it (step tail, merges, dense update) rounds it the same
+// way whatever the surrounding code lets the compiler contract.
+__device__ __forceinline__ float l2_grad(float g, float l2, float w) { return __fmaf_rn(l2, w, g); }
+
 // In-place update of param p and slots s0/s1 with gradient g.
 __device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st, float& p, float g, float& s0,
                                           float& s1) {
-  // every operation rounded on its own (no FMA contraction): the update is then the same bits in
-  // every kernel that inlines it, whatever the surrounding code lets the compiler fuse
+  // the fused multiply-adds are explicit (__fmaf_rn) and nothing else may be contracted: the update
+  // is then the same bits in every kernel that inlines it, with the FMAs kept (round 5 had turned
+  // contraction off altogether)
 #pragma clang fp contract(off)
   if (st.skip) return;
   switch (o.type) {
     case kAdam: {
-      s0 = o.beta1 * s0 + (1.f - o.beta1) * g;
-      s1 = o.beta2 * s1 + (1.f - o.beta2) * g * g;
-      p -= st.lr_t * s0 / (sqrtf(s1) + o.eps);
+      s0 = __fmaf_rn(o.beta1, s0, (1.f - o.beta1) * g);
+      s1 = __fmaf_rn(o.beta2, s1, ((1.f - o.beta2) * g) * g);
+      p -= (st.lr_t * s0) / (sqrtf(s1) + o.eps);
       break;
     }
     case kAdagrad: {
-      s0 += g * g;
-      p -= o.lr * g * rsqrtf(s0);
+      s0 = __fmaf_rn(g, g, s0);
+      p = __fmaf_rn(-(o.lr * g), rsqrtf(s0), p);
       break;
     }
     case kMomentum: {
-      s0 = o.momentum * s0 + g;
-      p -= o.lr * s0;
+      s0 = __fmaf_rn(o.momentum, s0, g);
+      p = __fmaf_rn(-o.lr, s0, p);
       break;
     }
     case kFtrl: {
-      const float acc_new = s0 + g * g;
+      const float acc_new = __fmaf_rn(g, g, s0);
       // TF's ApplyFtrl special-cases the default lr_power = -0.5 with sqrt; powf otherwise
       float pn, po;
       if (o.ftrl_lr_power == -0.5f) {
@@ -83,14 +89,14 @@ __device__ __forceinline__ void opt_apply(const OptParams& o, const OptStep& st,
         po = powf(s0, -o.ftrl_lr_power);
       }
       const float sigma = (pn - po) / o.lr;
-      s1 += g - sigma * p;
-      const float quad = pn / o.lr + 2.f * o.ftrl_l2;
+      s1 += __fmaf_rn(-sigma, p, g);
+      const float quad = __fmaf_rn(2.f, o.ftrl_l2, pn / o.lr);
       p = fabsf(s1) > o.ftrl_l1 ? (copysignf(o.ftrl_l1, s1) - s1) / quad : 0.f;
       s0 = acc_new;
       break;
     }
     default:
-      p -= o.lr * g;
+      p = __fmaf_rn(-o.lr, g, p);
   }
 }
 

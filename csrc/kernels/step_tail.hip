@@ -1,31 +1,21 @@
 // The tail of a training step in ONE launch: the MLP weight gradients + fused optimizer
-// (wgrad_body, mlp_wgrad.hip) and the embedding-row update (emb_rows_body, emb_update.hip) are
-// independent — one reads the transposed activations / output gradients, the other the per-lookup
-// gradient rows and the sorted keys — so they run as disjoint workgroup roles of one grid
-// (≈70 wgrad + ⌈B·F/512⌉ embedding workgroups, all co-resident on 256 CUs).  This replaces two
-// serial launches (≈10 + 15 µs) or a second stream (whose fork/join inside a HIP graph costs more
-// than it overlaps) with ≈max of the two.
-#include "../ops.h"
-#include "emb_body.h"
-#include "wgrad_body.h"
+// (wgrad_body, mlp_wgrad.hip) and the embedding-row update (emb_rows_body, emb_update.hip; or the
+// planned emb_plan_body, emb_plan.hip) are independent — one reads the transposed activations /
+// output gradients, the other the per-lookup gradient rows and the sorted keys — so they run as
+// disjoint workgroup roles of one grid (≈60-90 wgrad + the embedding workgroups, all co-resident on
+// 256 CUs).  This replaces two serial launches (≈10 + 15 µs) or a second stream (whose fork/join
+// inside a HIP graph costs more than it overlaps) with ≈max of the two.  Kernels: step_tail_kern.h.
+#include "step_tail_kern.h"
 
 #include <cstdlib>
 #include <cstring>
 
 namespace rocfm {
 
-constexpr int kTailThreads = 512;
+// Sorted entries per unplanned embedding workgroup of the tail.  The side chain's per-chunk run
+// ends / run-head counts are cut at the same size (tail_chunk binding).
+int tail_chunk_entries() { return kTailEntries; }
 
-// Sorted entries per embedding workgroup of the tail (ROCFM_TAIL_CHUNK = 256 | 512).  The side
-// chain's per-chunk run ends / run-head counts are cut at the same size (tail_chunk binding).
-int tail_chunk_entries() {
-  static const int n = [] {
-    const char* v = std::getenv("ROCFM_TAIL_CHUNK");
-    const int x = v ? std::atoi(v) : kTailChunkDefault;
-    return (x == 256 || x == 512) ? x : kTailChunkDefault;
-  }();
-  return n;
-}
 // compute units of the current device (the step tail sizes its roles to one dispatch round)
 static int tail_cus() {
   static const int n = [] {
@@ -36,82 +26,52 @@ static int tail_cus() {
   return n;
 }
 constexpr int kTailMaxKp = 48;  // K <= 47 (notebook shape K = 32 → Kp = 36)
-static_assert(kTailThreads == kWgThreads, "wgrad role uses 512-thread workgroups");
 
-template <int KP4, bool BT, bool PUSH, int kE, bool PRE = false>
-__global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
-                                                                 const int n_emb) {
-  const int bid = blockIdx.x;
-  if (bid < n_emb)
-    emb_rows_body<KP4, kTailThreads, BT, PUSH, kE, PRE>(e, bid);  // the longer role first: its workgroups dispatch first
-  else
-    wgrad_body<PUSH>(w, bid - n_emb);
+static int tail_wgrad_workgroups(WgradParams& w, int n) {
+  // widened weight-gradient tiles when the two roles exceed one dispatch round (wgrad_prepare;
+  // ROCFM_WGRAD_TW=1 keeps plain 32 × 32 tiles), laid out for the unplanned chunk count
+  const char* tw = std::getenv("ROCFM_WGRAD_TW");
+  const bool widen = !(tw && std::strcmp(tw, "1") == 0);
+  return wgrad_prepare(w, widen ? (n > 0 ? cdiv(n, kTailEntries) : 0) : -1, tail_cus());
 }
 
-// the embedding role's table-load prologue (emb_body.h PRE): apply mode with the side chain's
-// run-head keys, sorted gradient rows, and both optimizer slots or an f32 table (the missing
-// slots' loads then read the table as a stand-in)
-static bool tail_pre(const EmbUpdateParams& e) {
-  return e.mode == 0 && e.hkeys != nullptr && e.rows > 0 && e.sorted_contrib && e.n_dev == nullptr &&
-         (!e.tbl_bf16 || (e.s0 && e.s1));
-}
-
-template <int KP4, bool PUSH, int kE>
-static void launch_tail_e(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
-                          hipStream_t stream) {
-  if constexpr (!PUSH) {
-    if (tail_pre(e)) {
-      if (e.tbl_bf16)
-        hipLaunchKernelGGL((step_tail_kernel<KP4, true, false, kE, true>), grid, block, 0, stream, w, e, n_emb);
-      else
-        hipLaunchKernelGGL((step_tail_kernel<KP4, false, false, kE, true>), grid, block, 0, stream, w, e, n_emb);
-      return;
-    }
-  }
-  if (e.tbl_bf16)
-    hipLaunchKernelGGL((step_tail_kernel<KP4, true, PUSH, kE>), grid, block, 0, stream, w, e, n_emb);
-  else
-    hipLaunchKernelGGL((step_tail_kernel<KP4, false, PUSH, kE>), grid, block, 0, stream, w, e, n_emb);
-}
-
-template <int KP4, bool PUSH>
-static void launch_tail_t(const WgradParams& w, const EmbUpdateParams& e, int n_emb, dim3 grid, dim3 block,
-                          hipStream_t stream) {
-  if (tail_chunk_entries() == 256)
-    launch_tail_e<KP4, PUSH, 256>(w, e, n_emb, grid, block, stream);
-  else
-    launch_tail_e<KP4, PUSH, 512>(w, e, n_emb, grid, block, stream);
+// the planned tail's embedding workgroups: at least the unplanned chunk count, and the CUs the
+// weight-gradient role leaves free less ROCFM_EMB_PLAN_RESERVE (default 0) for the side chain's
+// kernels, which run beside the main graph
+int tail_plan_workgroups(WgradParams w, int n) {
+  const int n_wg = tail_wgrad_workgroups(w, n);
+  const char* r = std::getenv("ROCFM_EMB_PLAN_RESERVE");
+  const int reserve = r ? std::max(0, std::atoi(r)) : 0;
+  return std::max(cdiv(n, kTailEntries), tail_cus() - n_wg - reserve);
 }
 
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream) {
   ROCFM_REQUIRE(e.Kp % 4 == 0 && e.Kp <= kTailMaxKp && e.K1 <= e.Kp,
                 "step_tail: Kp must be a multiple of 4 and <= 48");
   if (e.id_stride <= 0) e.id_stride = 1;
-  const int n_emb = e.n > 0 ? cdiv(e.n, tail_chunk_entries()) : 0;
-  // widened weight-gradient tiles when the two roles exceed one dispatch round (wgrad_prepare;
-  // ROCFM_WGRAD_TW=1 keeps plain 32 × 32 tiles)
-  const char* tw = std::getenv("ROCFM_WGRAD_TW");
-  const bool widen = !(tw && std::strcmp(tw, "1") == 0);
-  const int n_wg = wgrad_prepare(w, widen ? n_emb : -1, tail_cus());
-  const dim3 grid(n_emb + n_wg), block(kTailThreads);
+  TailLaunch l{};
+  l.plan = e.plan_items != nullptr && e.mode == 0 && e.n > 0;
+  ROCFM_REQUIRE(!l.plan || (e.sorted_contrib && e.n_dev == nullptr && e.max_key == 0 && e.push.W == 0 &&
+                            (w.push.W == 0 || w.fuse_opt) && e.plan_nw >= cdiv(e.n, kTailEntries) && e.plan_slots &&
+                            e.plan_win && e.plan_head && e.plan_ctr),
+                "step_tail: the planned embedding role needs sorted gradient rows, no dedup / sentinels / push, "
+                "and its plan buffers");
+  l.n_emb = l.plan ? e.plan_nw : (e.n > 0 ? cdiv(e.n, kTailEntries) : 0);
+  const int n_wg = tail_wgrad_workgroups(w, e.n);
+  l.grid = dim3(l.n_emb + n_wg);
+  l.block = dim3(kTailThreads);
   // fused DP push: the export role (mode 2) and the gradient-emitting wgrad role write the slots
-  const bool push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);
-  ROCFM_REQUIRE(!push || (e.push.W <= kPushMaxW && w.push.W <= kPushMaxW), "step_tail: push world > 8");
-  switch (e.Kp / 4) {
-#define ROCFM_KP4(N)                                                   \
-  case N:                                                              \
-    if (push)                                                          \
-      launch_tail_t<N, true>(w, e, n_emb, grid, block, stream);        \
-    else                                                               \
-      launch_tail_t<N, false>(w, e, n_emb, grid, block, stream);       \
-    break;
-    ROCFM_KP4(1) ROCFM_KP4(2) ROCFM_KP4(3) ROCFM_KP4(4) ROCFM_KP4(5) ROCFM_KP4(6) ROCFM_KP4(7) ROCFM_KP4(8)
-    ROCFM_KP4(9) ROCFM_KP4(10) ROCFM_KP4(11) ROCFM_KP4(12)
-#undef ROCFM_KP4
-    default:  // the 512-entry row staging of larger rows (8 KiB per float4 column) + the wgrad
-              // reduction tiles exceed 160 KiB of LDS beyond Kp = 48
-      throw std::invalid_argument("step_tail: Kp > 48 unsupported (use mlp_wgrad + emb_rows_update)");
-  }
+  l.push = (e.push.W > 0 && (e.mode == 2 || (e.mode == 1 && e.push_seg > 0))) || (w.push.W > 0 && !w.fuse_opt);
+  ROCFM_REQUIRE(!l.push || (e.push.W <= kPushMaxW && w.push.W <= kPushMaxW), "step_tail: push world > 8");
+  const int kp4 = e.Kp / 4;
+  // (beyond Kp = 48 the 256-entry row staging of the unplanned role + the wgrad reduction tiles
+  // exceed 160 KiB of LDS: mlp_wgrad + emb_rows_update run as two launches)
+  if (kp4 <= 4)
+    launch_tail_group_a(kp4, w, e, l, stream);
+  else if (kp4 <= 8)
+    launch_tail_group_b(kp4, w, e, l, stream);
+  else
+    launch_tail_group_c(kp4, w, e, l, stream);
   ROCFM_HIP_CHECK(hipGetLastError());
 }
 

@@ -33,8 +33,8 @@ void launch_dense_apply(DenseApplyParams p, hipStream_t stream);
 
 // step_tail.hip: mlp_wgrad + emb_rows_update as workgroup roles of one launch
 void launch_step_tail(WgradParams w, EmbUpdateParams e, hipStream_t stream);
-constexpr int kTailChunkDefault = 256;  // profiles/r3_dedup.md: 20-step windows 33.0 vs 34.6 µs
 int tail_chunk_entries();  // sorted entries per embedding workgroup of the fused tail
+int tail_plan_workgroups(WgradParams w, int n);  // embedding workgroups of the planned tail (emb_plan.hip)
 
 // sort.hip
 size_t sort_pairs_temp_bytes(int n, int end_bit);

@@ -27,6 +27,7 @@ from __future__ import annotations
 import dataclasses
 import math
 import os
+import time
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -773,10 +774,12 @@ class FusedDeepFM:
         idbits = max(1, math.ceil(math.log2(max(key_range, 2))))
         return idbits, max(1, int(Smax))
 
-    def _build_multi(self, Smax: int, shard: Optional[tuple] = None, heads: bool = False) -> None:
+    def _build_multi(self, Smax: int, shard: Optional[tuple] = None, heads: bool = False, plan: bool = False) -> None:
         """``shard=(W, Vs)``: the batches' sort keys are row-shard owner-major keys (emb_shard).
         ``heads``: the side chain also counts run heads per tail chunk (``m_chd``; the sorted DP
-        export places each chunk's rows from them)."""
+        export places each chunk's rows from them).  ``plan``: the single-GPU sparse update runs the
+        planned step tail (``emb_plan.hip``: the side chain cuts every batch's sorted lookups into
+        equal-cost items, one per embedding workgroup; ``ROCFM_EMB_PLAN=0`` keeps the fixed chunks)."""
         H, dev = self.H, self.device
         Bp, F, n = self.Bp, self.F, self.n_lookup
         self._m_shard = shard  # (W, Vs) or (W, Vs, hot ids tensor)
@@ -810,12 +813,6 @@ class FusedDeepFM:
         self.m_chd = torch.zeros(2, Smax * self.m_nch, **i32) if heads else None
         # per-tile dedup (rows of ONE batch per row tile): group links, compacted keys and counts
         self.m_dedup = self.dedup and shard is None
-        # the keys of every tail chunk's run heads (sort_aux, side chain): the step tail's
-        # embedding role issues its first optimizer items' table loads from them at its start
-        # (emb_body.h PRE; apply mode — single-GPU steps — without the per-tile dedup)
-        self.m_hk = (torch.zeros(2, Smax * self.m_nch * self.m_chunk, **i32)
-                     if (not self.m_dedup and self.Kp <= self.H.tail_max_kp()
-                         and os.environ.get("ROCFM_TAIL_PREFETCH", "0") == "1") else None)
         if self.m_dedup:
             self.m_nxt = torch.zeros(2, Smax * n, **i32)
             self.m_ck = torch.zeros(2, Smax * n, **i32)
@@ -842,13 +839,54 @@ class FusedDeepFM:
                     rows.dedup = 0
                 if self.Kp <= self.H.tail_max_kp():  # the fused tail's 512-entry chunks
                     ep.chunk_end = self.m_cend[q, k * self.m_nch:].data_ptr()
-                if self.m_hk is not None and ep.mode == 0:
-                    ep.hkeys = self.m_hk[q, k * self.m_nch * self.m_chunk:].data_ptr()
-                    ep.rows = int(self.emb.shape[0])
+        self._build_emb_plan(plan and shard is None)
         self._m_graphs = {}
         self._m_primed = False
         self._m_warm = 0
         self._mq = 0
+
+    def _build_emb_plan(self, want: bool) -> None:
+        """Buffers of the planned step tail (emb_plan.hip / emb_plan_body.h) and the plan fields of
+        every multi-step parameter block: per parity the S batches' items and split-run slots, built
+        on the side chain; the split runs' window pieces, head folds and arrival counters, shared by
+        the steps (they run one after another on the main stream)."""
+        H = self.H
+        self.m_eplan = bool(want and not self.m_dedup and self.embedding_update == "sparse"
+                            and self.Kp <= H.tail_max_kp() and os.environ.get("ROCFM_EMB_PLAN", "1") != "0")
+        if not self.m_eplan:
+            return
+        dev, n, Smax = self.device, self.n_lookup, self.mS
+        i32 = dict(dtype=torch.int32, device=dev)
+        nw = int(H.tail_plan_workgroups(self.m_params[0][0][1], n))
+        self.m_plan_nw = nw
+        self.m_plan_beta = int(os.environ.get("ROCFM_EMB_BETA", "4"))
+        self.m_plan_lsplit = int(os.environ.get("ROCFM_EMB_LSPLIT", "128"))
+        self.m_pitems = torch.zeros(2, Smax * nw * 4, **i32)
+        self.m_pslots = torch.zeros(2, Smax * nw * 4, **i32)
+        self.m_pruns = torch.zeros(Smax * (n + 1), **i32)
+        self.m_pwin = torch.zeros((n // 64 + 2) * self.Kp, dtype=torch.float32, device=dev)
+        self.m_phead = torch.zeros(nw * self.Kp, dtype=torch.float32, device=dev)
+        self.m_pctr = torch.zeros(nw + 4, **i32)  # [nw]: sticky "item outside the plan's bounds" flag
+        for q in range(2):
+            for k in range(Smax):
+                ep = self.m_params[q][k][3]
+                if ep.mode != 0:
+                    continue
+                ep.plan_items = self.m_pitems[q, k * nw * 4:].data_ptr()
+                ep.plan_slots = self.m_pslots[q, k * nw * 4:].data_ptr()
+                ep.plan_nw = nw
+                ep.plan_win, ep.plan_head = self.m_pwin.data_ptr(), self.m_phead.data_ptr()
+                ep.plan_ctr = self.m_pctr.data_ptr()
+
+    def _emb_plan(self, q: int, stream) -> None:
+        """Side chain: the work plans of the S batches just sorted into the parity-q buffers."""
+        H = self.H
+        pp = H.EmbPlanParams()
+        pp.skeys = self.m_sk[q].data_ptr()
+        pp.n, pp.S, pp.nw = self.n_lookup, self.mS, self.m_plan_nw
+        pp.beta, pp.lsplit = self.m_plan_beta, self.m_plan_lsplit
+        pp.runs, pp.items, pp.slots = self.m_pruns.data_ptr(), self.m_pitems[q].data_ptr(), self.m_pslots[q].data_ptr()
+        H.emb_plan(pp, stream.cuda_stream)
 
     def _fetch_multi_params(self, q: int, advance: int):
         """Preparation run beside a graph of parity q and ``advance`` steps: batches start at
@@ -895,12 +933,10 @@ class FusedDeepFM:
         a.pos, a.chunk_end = self.m_pos[1 - q].data_ptr(), self.m_cend[1 - q].data_ptr()
         if self.m_chd is not None:
             a.chunk_heads = self.m_chd[1 - q].data_ptr()
-        if self.m_hk is not None:
-            a.chunk_hkeys = self.m_hk[1 - q].data_ptr()
         if self.m_keys64 is not None:  # sorted 64-bit keys → plain per-batch ids in m_sk
             a.skeys64, a.skeys_out, a.id_bits = self.m_keys64[1].data_ptr(), self.m_sk[1 - q].data_ptr(), self.m_idbits
         if self.m_dedup:  # positions / run ends / run heads come from the dedup over the compacted list
-            a.chunk_end = a.chunk_heads = a.chunk_hkeys = 0
+            a.chunk_end = a.chunk_heads = 0
         if not (self.m_dedup and self.m_keys64 is None):  # (64-bit keys: sort_aux writes the plain ids)
             H.sort_aux(a, stream.cuda_stream)
         if self.m_dedup:
@@ -915,6 +951,8 @@ class FusedDeepFM:
             if self.m_chd is not None:
                 d.chunk_heads = self.m_chd[1 - q].data_ptr()
             H.dedup(d, stream.cuda_stream)
+        if getattr(self, "m_eplan", False):
+            self._emb_plan(1 - q, stream)
         if getattr(self, "_m_post", None) is not None:  # e.g. row-shard routing of the sorted batches
             self._m_post(1 - q, stream)
 
@@ -1013,13 +1051,22 @@ class FusedDeepFM:
             if self._m_side_ev is not None:
                 main.wait_event(self._m_side_ev)
                 self._pl_wait("main", self._m_side_ev)
+            st = getattr(self, "stall_timing", None)  # diagnostics (bench): GPU-side gaps of the main stream
+            if st is not None:
+                t_start, t_end, t_side = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                t_start.record(main)  # completes when graph N may start: main work before it + side N-1
             gm.replay()
+            if st is not None:
+                t_end.record(main)
             self._pl_op("main", f"main graph @{self._i}", main_rng)
             side.wait_event(before)
             self._pl_wait("side", before)
             with torch.cuda.stream(side):
                 gs.replay()
             self._pl_op("side", f"side graph @{self._i}", side_rng)
+            if st is not None:
+                t_side.record(side)
+                st.append((t_start, t_end, t_side))
             ev = self._pl_mark(torch.cuda.Event(), "side")
             ev.record(side)
         self._m_side_ev = ev
@@ -1089,7 +1136,7 @@ class FusedDeepFM:
 
     def _train_steps_multi(self, n: int, Smax: int) -> None:
         if getattr(self, "m_req", None) != Smax or getattr(self, "_m_pool", None) is not self.pool_ids:
-            self._build_multi(Smax)
+            self._build_multi(Smax, plan=True)
             self._m_pool = self.pool_ids
         if not self._m_primed:
             self._prime_multi()
@@ -1202,7 +1249,9 @@ class FusedDeepFM:
                     b, carry[0] = carry[0], None
                 else:
                     while len(pending) > hold - 1:  # the item `hold` back is recycled by this next()
+                        t_h = time.perf_counter()
                         pending.pop(0)[0].synchronize()
+                        self.host_copy_wait_s = getattr(self, "host_copy_wait_s", 0.0) + time.perf_counter() - t_h
                     b = next(it, None)
                     if b is None:
                         break
@@ -1268,7 +1317,7 @@ class FusedDeepFM:
         if build is not None:
             build(S)
         elif getattr(self, "m_req", None) != S or getattr(self, "_m_pool", None) is not self.pool_ids:
-            self._build_multi(S)
+            self._build_multi(S, plan=True)
             self._m_pool = self.pool_ids
         self._prime_multi()  # prepares steps i0 .. i0+S-1 from the ring
         prime_ev = mark(main)
@@ -1544,6 +1593,8 @@ class FusedDeepFM:
             self.xctr.zero_()  # (the arrival parity is lost with the timed-out launch)
             self.xerr.zero_()
             raise RuntimeError("deepfm_rows: a row-tile split exchange timed out (its steps' layer-1 inputs are invalid)")
+        if getattr(self, "m_eplan", False) and int(self.m_pctr[self.m_plan_nw].item()) != 0:
+            raise RuntimeError("step_tail: a planned embedding item exceeded the plan's bounds (its rows were not updated)")
         if self.id_guard and int(self.bad_ids.item()) != 0:
             raise ValueError(f"ROCFM_CHECK_IDS: a batch held feature ids outside [0, {self.id_limit}) "
                              "(they were trained as row 0)")

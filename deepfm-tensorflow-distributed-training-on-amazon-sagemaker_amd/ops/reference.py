@@ -196,3 +196,53 @@ def shard_route_reference(ids: np.ndarray, W: int, Vs: int, cap: int):
         for l in np.nonzero(ids % W == o)[0]:
             local[l] = o * cap + min(pos[int(ids[l])], cap - 1)
     return send, local, counts
+
+
+def emb_plan_reference(keys: np.ndarray, nw: int, beta: int = 4, lsplit: int = 128):
+    """Sequential replica of emb_plan.hip for ONE batch's sorted keys.
+
+    Returns ``(items [nw, 4], slots [nw, 4])``: item k = (es, ee, lead slot, tail slot) — empty items
+    are (0, 0, -1, -1) — and slot s = (key, first non-head window, last window, pieces) for every
+    split run, numbered in run order.  Cuts are the run heads and, inside runs longer than
+    ``lsplit``, the 64-entry window boundaries; cut c of run r goes to item
+    floor((c + beta·r) / Q), Q = ceil((n + beta·U) / nw)."""
+    keys = np.asarray(keys)
+    n = int(keys.size)
+    heads = np.flatnonzero(np.r_[True, keys[1:] != keys[:-1]]) if n else np.zeros(0, np.int64)
+    U = int(heads.size)
+    runs = np.r_[heads, n]
+    Q = max(1, (n + beta * U + nw - 1) // nw)
+    items = np.zeros((nw, 4), np.int64)
+    items[:, 2:] = -1
+    slots = np.zeros((nw, 4), np.int64)
+    cuts = []  # (position, run, is_head)
+    for r in range(U):
+        s, e = int(runs[r]), int(runs[r + 1])
+        cuts.append((s, r, True))
+        if e - s > lsplit:
+            c = (s & ~63) + 64
+            while c < e:
+                cuts.append((c, r, False))
+                c += 64
+    prev_item, nslot = -1, 0
+    cur_slot = {}  # run → slot
+    for j, (c, r, is_head) in enumerate(cuts):
+        it = (c + beta * r) // Q
+        if it != prev_item:
+            items[it, 0] = c
+            if prev_item >= 0:
+                items[prev_item, 1] = c
+            if not is_head:  # the run is split here
+                if r not in cur_slot:
+                    cur_slot[r] = nslot
+                    s0 = int(runs[r])
+                    slots[nslot] = (int(keys[s0]), c >> 6, (int(runs[r + 1]) - 1) >> 6, 1)
+                    items[(s0 + beta * r) // Q, 3] = nslot
+                    nslot += 1
+                sl = cur_slot[r]
+                items[it, 2] = sl
+                slots[sl, 3] += 1
+            prev_item = it
+    if prev_item >= 0:
+        items[prev_item, 1] = n
+    return items, slots

@@ -96,6 +96,14 @@ def range_merge_buckets(W: int, cap: int) -> int:
 SEARCH_DIR_MAX_W = 4
 
 
+def merge_choice() -> str:
+    """ROCFM_MERGE with ``noplan`` read as ``auto``: ``noplan`` is the automatic step-time merge
+    (search ≤ 4 ranks, maps above) with the plan-ahead merge off — the A/B the N > 1 bench runs
+    beside the default (``merge_noplan_*`` windows)."""
+    m = os.environ.get("ROCFM_MERGE", "auto")
+    return "auto" if m == "noplan" else m
+
+
 def search_dir_buckets(W: int, V: int) -> int:
     """Key buckets of the directory the sorted DP export writes for the SEARCH merge (2 ≤ W ≤
     SEARCH_DIR_MAX_W): each entry's binary search in the other ranks' lists starts inside its
@@ -103,7 +111,7 @@ def search_dir_buckets(W: int, V: int) -> int:
     buckets.  0 = off (ROCFM_SEARCH_DIR=0, one rank, or more than SEARCH_DIR_MAX_W ranks)."""
     if W < 2 or W > SEARCH_DIR_MAX_W or os.environ.get("ROCFM_SEARCH_DIR", "1") == "0":
         return 0
-    if os.environ.get("ROCFM_MERGE", "auto") != "auto":  # a forced merge (direct / hash / range) is kept
+    if merge_choice() != "auto":  # a forced merge (direct / hash / range) is kept
         return 0
     return max(64, min(8192, V // 16))
 
@@ -134,7 +142,7 @@ def range_merge_enabled(W: int) -> bool:
     search / maps merges (profiles/r3_merge_range.md): no gain on Criteo-shape ids, whose
     field-clustered Zipf ids crowd a few key buckets; 8.6 vs 10.6 µs at W = 4 only when the keys
     are first spread by a bijective hash."""
-    return W >= 2 and os.environ.get("ROCFM_MERGE", "auto") == "range"
+    return W >= 2 and merge_choice() == "range"
 
 
 class MergeMaps:
@@ -145,9 +153,9 @@ class MergeMaps:
     ``ROCFM_MERGE=direct|hash`` forces one (tests)."""
 
     def __init__(self, W: int, cap: int, rows: int, device):
-        choice = os.environ.get("ROCFM_MERGE", "auto")
+        choice = merge_choice()
         if choice not in ("auto", "direct", "hash", "range", "plan"):
-            raise ValueError(f"ROCFM_MERGE must be auto, direct, hash, range or plan, got {choice!r}")
+            raise ValueError(f"ROCFM_MERGE must be auto, noplan, direct, hash, range or plan, got {choice!r}")
         direct_bytes = (W + 1) * rows * 4
         # (plan: the multi-step graphs merge by the plan; the per-step path keeps the automatic maps)
         self.hashed = choice == "hash" or (choice in ("auto", "plan") and direct_bytes > MERGE_MAP_BUDGET)
@@ -979,6 +987,9 @@ class FusedDataParallel:
         self.eng.check()
         if self.p2p is not None and self.p2p.errored():
             raise RuntimeError("DP p2p exchange: a peer wait timed out (rank missing or stalled)")
+        if self.mode == "dp" and int(self.overflow.item()) & 2:
+            raise RuntimeError("DP plan merge: a union row id outside the table (merge_plan_apply skipped its "
+                               "gradients; the plan built on the side chain is corrupt)")
         if self.overflowed():
             raise RuntimeError(f"DP exchange overflow: a rank exported more unique rows than capacity {self.cap}; "
                                "rebuild with a larger capacity (default batch_size*field_size never overflows)")
@@ -990,7 +1001,7 @@ class FusedDataParallel:
         (sticky device flag set by merge_scatter; never with the default capacity)."""
         if self.mode != "dp":
             return False
-        return bool(int(self.overflow.item()))
+        return bool(int(self.overflow.item()) & 1)
 
     def load_state_dict(self, sd, strict: bool = True) -> None:
         self.eng.load_state_dict(sd, strict=strict)

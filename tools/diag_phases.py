@@ -53,7 +53,7 @@ def main():
     nrows = eng.Bp // 4  # ≥ the row kernel's workgroups (4..16 examples each)
     s_rows = torch.zeros(nrows * 16, dtype=torch.int64, device=dev)
     s_wg = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
-    s_emb = torch.zeros(((eng.n_lookup + 255) // 256) * 16, dtype=torch.int64, device=dev)  # ≥ per-chunk slots
+    s_emb = torch.zeros(max((eng.n_lookup + 255) // 256, 1024) * 16, dtype=torch.int64, device=dev)  # ≥ per-WG slots
     for p in range(2):
         eng.rows_params[p].stamps = s_rows.data_ptr()
         eng.wgrad_params[p].stamps = s_wg.data_ptr()
@@ -90,6 +90,32 @@ def main():
         print("   barrier timeouts:", int(sync[2].item()))
     wg = s_wg.view(-1, 16).cpu()
     report("mlp_wgrad (tile WGs)", wg[wg[:, 1] > 0], [0, 1, 2], ["MFMA + LDS reduce", "epilogue (opt+bf16)"])
+    if getattr(eng, "m_eplan", False) and multi:  # the planned embedding role (emb_plan_body.h)
+        st = s_emb.view(-1, 16).cpu()
+        report("emb_plan (planned items)", st, [0, 1, 2, 3],
+               ["keys+rows+scan+pieces", "publish + complete runs", "split-run combine"])
+        # the last step's plan: entries and run heads per item, and the slowest items
+        q = eng._mq ^ 1  # parity of the last graph
+        k = eng.mS - 1
+        nw = eng.m_plan_nw
+        it = eng.m_pitems[q, k * nw * 4:(k + 1) * nw * 4].view(nw, 4).cpu().long()
+        sk = eng.m_sk[q, k * eng.n_lookup:(k + 1) * eng.n_lookup].cpu().long()
+        heads = torch.ones_like(sk, dtype=torch.bool)
+        heads[1:] = sk[1:] != sk[:-1]
+        ent = (it[:, 1] - it[:, 0]).clamp(min=0)
+        hd = torch.tensor([int(heads[a:b].sum()) if b > a else 0 for a, b in it[:, :2].tolist()])
+        live = ent > 0
+        print(f"   items: {int(live.sum())} of {nw}; entries per item min {int(ent[live].min())} mean "
+              f"{float(ent[live].float().mean()):.0f} max {int(ent[live].max())}; heads min {int(hd[live].min())} "
+              f"mean {float(hd[live].float().mean()):.0f} max {int(hd[live].max())}; split-run slots "
+              f"{int((it[:, 3] >= 0).sum())}")
+        stf = st.double()
+        tot = (stf[:nw, 3] - stf[:nw, 0]) * 0.01
+        order = torch.argsort(tot, descending=True)[:6]
+        for w in order.tolist():
+            print(f"   slow item {w:3d}: total {tot[w]:.2f} us, entries {int(ent[w])}, heads {int(hd[w])}, "
+                  f"lead {int(it[w, 2])}, tail {int(it[w, 3])}")
+        return
     report("emb_rows_update", s_emb.view(-1, 16).cpu(), [0, 1, 2, 3, 4],
            ["keys+rows+scan+heads", "end search", "continuation", "optimizer items"])
     # the slowest embedding workgroups of the last step, with their chunk's run-head count
