@@ -765,13 +765,16 @@ def scale_windows(a, spec, hp, dev):
     rows = min(int(0.9 * total) // per_row, (free - (6 << 30)) // per_row, (1 << 31) - 1)
     rows = rows // 1_000_000 * 1_000_000
 
-    def capacity(sp, pool):
-        return FusedDeepFM(sp, hp, B, dev, params=None, seed=a.seed, compute_dtype="fp8")
+    def capacity(dtype):
+        return lambda sp, pool: FusedDeepFM(sp, hp, B, dev, params=None, seed=a.seed, compute_dtype=dtype)
 
     if rows >= 1_000_000:
-        window("capacity", rows, capacity, table_bytes=rows * per_row, hbm_total_bytes=int(total),
-               hbm_fraction=round(rows * per_row / total, 3), compute_dtype="fp8", table_dtype="f32",
-               optimizer_slots="f32 Adam m, v")
+        # config 5 as BASELINE.json names it (fp8 MFMA MLP input layer), then the same table with the
+        # bf16 MLP beside it: the fp8 layer's cost / gain at this shape, driver-observed
+        for name, dtype in (("capacity", "fp8"), ("capacity_bf16", "bf16")):
+            window(name, rows, capacity(dtype), table_bytes=rows * per_row, hbm_total_bytes=int(total),
+                   hbm_fraction=round(rows * per_row / total, 3), compute_dtype=dtype, table_dtype="f32",
+                   optimizer_slots="f32 Adam m, v")
     return out
 
 

@@ -100,7 +100,7 @@ struct EmbPlanParams {
 void launch_emb_plan(const EmbPlanParams& p, hipStream_t stream);
 // the planned tail's bounds (emb_plan_body.h): run heads and window pieces per item
 constexpr int kPlanHcap = 264;
-constexpr int kPlanPcap = kPlanHcap + 48;
+constexpr int kPlanPcap = kPlanHcap + 64;
 
 struct EmbDenseParams {
   float* emb;

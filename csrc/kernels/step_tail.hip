@@ -36,12 +36,13 @@ static int tail_wgrad_workgroups(WgradParams& w, int n) {
 }
 
 // the planned tail's embedding workgroups: at least the unplanned chunk count, and the CUs the
-// weight-gradient role leaves free less ROCFM_EMB_PLAN_RESERVE (default 0) for the side chain's
-// kernels, which run beside the main graph
+// weight-gradient role leaves free less ROCFM_EMB_PLAN_RESERVE (default 16) for the side chain's
+// kernels, which run beside the main graph (with every CU taken, one tail workgroup waited 3.8 µs
+// for a CU: profiles/r6_planned_tail.md)
 int tail_plan_workgroups(WgradParams w, int n) {
   const int n_wg = tail_wgrad_workgroups(w, n);
   const char* r = std::getenv("ROCFM_EMB_PLAN_RESERVE");
-  const int reserve = r ? std::max(0, std::atoi(r)) : 0;
+  const int reserve = r ? std::max(0, std::atoi(r)) : 16;
   return std::max(cdiv(n, kTailEntries), tail_cus() - n_wg - reserve);
 }
 

@@ -17,10 +17,13 @@ template <int KP4, bool BT, bool PUSH>
 __global__ __launch_bounds__(kTailThreads) void step_tail_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                  const int n_emb) {
   const int bid = blockIdx.x;
+  unsigned long long* stp = bid < n_emb ? e.stamps : w.stamps;  // (diagnostics: entry / exit stamps 15 / 14)
+  ROCFM_STAMP(stp, 15);
   if (bid < n_emb)
     emb_rows_body<KP4, kTailThreads, BT, PUSH, kTailEntries>(e, bid);  // the longer role first: dispatched first
   else
     wgrad_body<PUSH>(w, bid - n_emb);
+  ROCFM_STAMP(stp, 14);
 }
 
 // planned embedding role (emb_plan_body.h): plan item bid of the side chain's work plan
@@ -28,10 +31,13 @@ template <int KP4, bool BT>
 __global__ __launch_bounds__(kTailThreads) void step_tail_plan_kernel(const WgradParams w, const EmbUpdateParams e,
                                                                       const int n_emb) {
   const int bid = blockIdx.x;
+  unsigned long long* stp = bid < n_emb ? e.stamps : w.stamps;  // (diagnostics: entry / exit stamps 15 / 14)
+  ROCFM_STAMP(stp, 15);
   if (bid < n_emb)
     emb_plan_body<KP4, BT>(e, bid);
   else
     wgrad_body<false>(w, bid - n_emb);
+  ROCFM_STAMP(stp, 14);
 }
 
 struct TailLaunch {

@@ -860,7 +860,9 @@ class FusedDeepFM:
         nw = int(H.tail_plan_workgroups(self.m_params[0][0][1], n))
         self.m_plan_nw = nw
         self.m_plan_beta = int(os.environ.get("ROCFM_EMB_BETA", "4"))
-        self.m_plan_lsplit = int(os.environ.get("ROCFM_EMB_LSPLIT", "128"))
+        # runs longer than this are cut at window boundaries (split runs cost a hand-off; a 512-entry
+        # run in one item costs less than that at B = 1024: profiles/r6_planned_tail.md)
+        self.m_plan_lsplit = int(os.environ.get("ROCFM_EMB_LSPLIT", "512"))
         self.m_pitems = torch.zeros(2, Smax * nw * 4, **i32)
         self.m_pslots = torch.zeros(2, Smax * nw * 4, **i32)
         self.m_pruns = torch.zeros(Smax * (n + 1), **i32)
@@ -1593,8 +1595,13 @@ class FusedDeepFM:
             self.xctr.zero_()  # (the arrival parity is lost with the timed-out launch)
             self.xerr.zero_()
             raise RuntimeError("deepfm_rows: a row-tile split exchange timed out (its steps' layer-1 inputs are invalid)")
-        if getattr(self, "m_eplan", False) and int(self.m_pctr[self.m_plan_nw].item()) != 0:
-            raise RuntimeError("step_tail: a planned embedding item exceeded the plan's bounds (its rows were not updated)")
+        if getattr(self, "m_eplan", False):
+            err = int(self.m_pctr[self.m_plan_nw].item())
+            if err:
+                raise RuntimeError("step_tail (planned embedding role): "
+                                   + ("an item exceeded the plan's bounds " if err & 1 else "")
+                                   + ("a split run's head item timed out waiting for its lead items " if err & 2 else "")
+                                   + "(those rows were not updated)")
         if self.id_guard and int(self.bad_ids.item()) != 0:
             raise ValueError(f"ROCFM_CHECK_IDS: a batch held feature ids outside [0, {self.id_limit}) "
                              "(they were trained as row 0)")

@@ -252,19 +252,24 @@ class StreamPlan:
     ring slot a side graph may still be reading (the event plan's ``copy.wait_event(sevs[j - 3])``).
     """
 
-    def __init__(self):
+    def __init__(self, window: int = 96):
         self.ops: List[Tuple[str, str, List[Tuple[str, int, int, bool]], int]] = []  # stream, label, ranges, deps
-        self._last: Dict[str, int] = {}
-        self._waits: Dict[str, int] = defaultdict(int)  # stream → bitmask of ops its next op waits for
+        self.base = 0  # absolute index of ops[0]: ``check`` prunes to the last ``window`` operations
+        self.window = int(window)
+        self._last: Dict[str, int] = {}  # stream → absolute index of its last op
+        self._waits: Dict[str, int] = defaultdict(int)  # stream → bitmask (relative) of ops its next op waits for
 
     def record(self, stream: str) -> int:
-        """Token of everything issued on ``stream`` so far (an event recorded there)."""
+        """Token of everything issued on ``stream`` so far (an event recorded there): the absolute
+        index of its last operation as one bit, valid across pruning."""
         i = self._last.get(stream)
         return 0 if i is None else (1 << i)
 
     def wait(self, stream: str, token: Optional[int]) -> None:
         if token:
-            self._waits[stream] |= token
+            rel = token >> self.base  # (a token of a pruned op orders nothing left in the window)
+            if rel:
+                self._waits[stream] |= rel
 
     def wait_stream(self, stream: str, other: str) -> None:
         self.wait(stream, self.record(other))
@@ -272,12 +277,28 @@ class StreamPlan:
     def op(self, stream: str, label: str, ranges=()) -> int:
         """One operation on ``stream``; ``ranges`` = [(name, lo, hi, write)] (half-open)."""
         deps = self._waits.pop(stream, 0)
-        if stream in self._last:
-            deps |= 1 << self._last[stream]
-        i = len(self.ops)
+        last = self._last.get(stream)
+        if last is not None and last >= self.base:
+            deps |= 1 << (last - self.base)
+        i = self.base + len(self.ops)
         self.ops.append((stream, label, list(ranges), deps))
         self._last[stream] = i
         return i
+
+    def prune(self, keep: Optional[int] = None) -> None:
+        """Drop all but the last ``keep`` operations.  Exact for the pairs left: happens-before
+        edges only point to older operations, so every path between two kept operations runs
+        through kept operations.  With ``keep`` above the ring's reuse distance in operations (a
+        slot is rewritten every 4 graphs ≈ 16 operations) every access a refill could race is still
+        checked, and ``ROCFM_HAZARD=1`` stays O(keep²) per check over a whole epoch."""
+        keep = self.window if keep is None else int(keep)
+        d = len(self.ops) - keep
+        if d <= 0:
+            return
+        self.ops = [(st, lb, rg, deps >> d) for st, lb, rg, deps in self.ops[d:]]
+        for k in list(self._waits):
+            self._waits[k] >>= d
+        self.base += d
 
     def conflicts(self) -> List[Tuple[str, str, str]]:
         # transitive happens-before: hb[i] = bitmask of every op ordered before op i
@@ -315,3 +336,4 @@ class StreamPlan:
             lines = [f"  {n}: {a}  <->  {b}" for n, a, b in found[:20]]
             raise HazardError(f"stream-plan hazard{(' in ' + tag) if tag else ''}: {len(found)} unordered "
                               "overlapping accesses with a write:\n" + "\n".join(lines))
+        self.prune()

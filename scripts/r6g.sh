@@ -1,0 +1,24 @@
+# Round 6 (g): wave-segmented plan kernel — tests, A/B windows, phases with tail entry/exit stamps,
+# kernel-trace summary; the world-8 node-default DP rehearsal; the N = 2 bench windows (gloo rehearsal)
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6g
+mkdir -p $O
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_emb_plan_gpu.py tests/test_fused_kernels_gpu.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+NB="--embedding_size 32 --feature_size 117581"
+for rep in 1 2 3; do
+  timeout -k 10 150 python bench.py --gpus 1 --no_secondary --steps 20 --warmup 5 > $O/plan_d20_$rep.json 2>/dev/null || exit 1
+  ROCFM_EMB_PLAN=0 timeout -k 10 150 python bench.py --gpus 1 --no_secondary --steps 20 --warmup 5 > $O/noplan_d20_$rep.json 2>/dev/null || exit 1
+  timeout -k 10 150 python bench.py --gpus 1 --no_secondary --steps 20 --warmup 5 $NB > $O/plan_n20_$rep.json 2>/dev/null || exit 1
+done
+timeout -k 10 150 python bench.py --gpus 1 --no_secondary --steps 200 --warmup 20 > $O/plan_d200.json 2>/dev/null || exit 1
+timeout -k 10 150 python bench.py --gpus 1 --no_secondary --steps 200 --warmup 20 $NB > $O/plan_n200.json 2>/dev/null || exit 1
+MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_default.txt 2>&1 || exit 1
+ROCFM_EMB_PLAN=0 MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_default_noplan.txt 2>&1 || exit 1
+MULTI=1 K=32 V=117581 timeout -k 10 200 python tools/diag_phases.py > $O/phases_notebook.txt 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace -d /tmp/p_plan -o run -- python3 $R/bench.py --gpus 1 --steps 200 --warmup 20 --no_secondary > $R/$O/prof_plan.log 2>&1 || exit 1
+python3 $R/tools/rocpd_summary.py $(find /tmp/p_plan -name "*.db" | head -1) > $R/$O/prof_plan.txt 2>&1 || exit 1
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_fused_dp_gpu.py -x -v --timeout 300 --timeout-method thread -k "world8" > $O/dp_world8.log 2>&1 || exit 1
+ROCFM_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/gloo2.json 2> $O/gloo2.err || exit 1

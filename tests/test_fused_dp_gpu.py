@@ -91,7 +91,7 @@ def _worker(rank, world, port, mode, out_path, exchange="rccl", steps=3, spg=0, 
     if rank == 0:
         torch.save({"emb": eng.emb.cpu(), "dense": eng.dense.cpu(), "slots": [x.cpu() for x in eng.emb_slots],
                     "shadow": eng.shadow.status, "exchange": eng.exchange, "consistent": consistent,
-                    "diverged": diverged}, out_path)
+                    "diverged": diverged, "merge_plan": bool(getattr(eng, "m_plan", False))}, out_path)
     eng.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -192,6 +192,19 @@ def test_fused_dp_world8_rehearsal(tmp_path):
     plan-ahead path DP runs from PLAN_MIN_W ranks (the ids exchanged and the plan built on the side
     chain), multi-step graphs; ≡ the single-GPU union batch, replicas bit-identical."""
     _check_dp_vs_single(tmp_path, 8, "dp", "p2p", 11, 4, "sparse", push="0")
+
+
+def test_fused_dp_world8_rehearsal_node_default(tmp_path, monkeypatch):
+    """Eight ranks on one GPU in the 8-GPU node's DEFAULT combination: the fused producer push (every
+    rank's tail stores its gradients straight into the 7 peers' receive slots) together with the
+    plan-ahead merge (PLAN_MIN_W ≤ 8), at 64 examples per rank so that the spinning producers of
+    eight processes cannot starve a lagging peer of CUs; ≡ the single-GPU union batch."""
+    from rocfm.parallel.dp import PLAN_MIN_W
+
+    assert PLAN_MIN_W <= 8
+    monkeypatch.setenv("ROCFM_MERGE", "auto")
+    dp = _check_dp_vs_single(tmp_path, 8, "dp", "p2p", 11, 4, "sparse", push="1")
+    assert dp["merge_plan"]
 
 
 @pytest.mark.parametrize("update", ["sparse", "exact"])

@@ -149,8 +149,11 @@ def test_stream_plan_orders_through_waits_transitively():
         q.check("t")
 
 
-def _simulate_train_stream(S: int, graphs: int, early: bool, skip_init_wait: bool = False):
-    """The event plan of FusedDeepFM.train_stream / _launch_multi on a 4·S-slot ring, in plan ops."""
+def _simulate_train_stream(S: int, graphs: int, early: bool, skip_init_wait: bool = False, early_at: int = 3,
+                           check_every: bool = False):
+    """The event plan of FusedDeepFM.train_stream / _launch_multi on a 4·S-slot ring, in plan ops
+    (``early``: from graph ``early_at`` on, the refill waits one side graph too early;
+    ``check_every``: check — and so prune — after every graph, as the loop does)."""
     from rocfm.utils.hazard import StreamPlan
 
     R = 4 * S
@@ -173,7 +176,7 @@ def _simulate_train_stream(S: int, graphs: int, early: bool, skip_init_wait: boo
     sevs, side_ev, i = [], None, 0
     for j in range(graphs):
         w = sevs[j - 3] if j >= 3 else prime
-        if early and j >= 3:
+        if early and j >= max(3, early_at):
             w = sevs[j - 4] if j >= 4 else prime
         p.wait("copy", w)
         cevs.append(stage(S))
@@ -188,6 +191,8 @@ def _simulate_train_stream(S: int, graphs: int, early: bool, skip_init_wait: boo
         side_ev = p.record("side")
         sevs.append(side_ev)
         i += S
+        if check_every:
+            p.check(f"graph {j}")
     return p
 
 
@@ -209,3 +214,15 @@ def test_train_stream_event_plan_is_race_free_and_an_early_refill_is_caught():
     # the first refill racing the ring's zero fill on the compute stream (no copy.wait_stream(main))
     found = _simulate_train_stream(4, 3, early=False, skip_init_wait=True).conflicts()
     assert any("ring allocation" in a or "ring allocation" in b for _, a, b in found)
+
+
+def test_stream_plan_stays_bounded_over_an_epoch_and_still_catches_a_late_race():
+    """Checked after every graph (as train_stream does), the plan prunes itself to its window: a
+    5,000-graph stream keeps ≤ window operations, and an early refill injected at graph 4,000 is
+    still caught."""
+    from rocfm.utils.hazard import HazardError
+
+    p = _simulate_train_stream(8, 5000, early=False, check_every=True)
+    assert len(p.ops) <= p.window and p.base > 14000
+    with pytest.raises(HazardError, match="copy:stage"):
+        _simulate_train_stream(8, 4100, early=True, early_at=4000, check_every=True)

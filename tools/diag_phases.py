@@ -90,6 +90,18 @@ def main():
         print("   barrier timeouts:", int(sync[2].item()))
     wg = s_wg.view(-1, 16).cpu()
     report("mlp_wgrad (tile WGs)", wg[wg[:, 1] > 0], [0, 1, 2], ["MFMA + LDS reduce", "epilogue (opt+bf16)"])
+    # the fused tail's workgroups from entry to exit (stamps 15 / 14, both roles; multi-step path)
+    em = s_emb.view(-1, 16).cpu()
+    ent = torch.cat([em[em[:, 15] > 0, 15], wg[wg[:, 15] > 0, 15]]).double()
+    ext = torch.cat([em[em[:, 14] > 0, 14], wg[wg[:, 14] > 0, 14]]).double()
+    if ent.numel() and ext.numel():
+        t0 = ent.min()
+        off = ((ent - t0) * 0.01).sort().values
+        ex = ((ext - t0) * 0.01).sort().values
+        q = lambda v, f: float(v[min(v.numel() - 1, int(f * v.numel()))])  # noqa: E731
+        print(f"== step tail (all {ent.numel()} workgroups): first entry → last exit {float(ex[-1]):.2f} us; entry "
+              f"offsets p50 {q(off, .5):.2f} p90 {q(off, .9):.2f} max {float(off[-1]):.2f}; exits p50 {q(ex, .5):.2f} "
+              f"p90 {q(ex, .9):.2f} max {float(ex[-1]):.2f}")
     if getattr(eng, "m_eplan", False) and multi:  # the planned embedding role (emb_plan_body.h)
         st = s_emb.view(-1, 16).cpu()
         report("emb_plan (planned items)", st, [0, 1, 2, 3],

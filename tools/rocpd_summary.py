@@ -8,6 +8,7 @@ import sqlite3
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
     name = re.sub(r"<.*", "", name)
     return name.split("::")[-1][:48]
@@ -24,9 +25,11 @@ def main():
     for n, s, e, st in rows:
         by[short(n)].append((e - s) / 1e3)
     tot = sum(sum(v) for v in by.values())
-    print(f"{'kernel':<50}{'calls':>8}{'total ms':>11}{'mean us':>10}{'share':>8}")
+    print(f"{'kernel':<50}{'calls':>8}{'total ms':>11}{'mean us':>10}{'share':>8}{'p50':>8}{'p90':>8}{'max':>8}")
     for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
-        print(f"{k:<50}{len(v):>8}{sum(v) / 1e3:>11.2f}{sum(v) / len(v):>10.2f}{100 * sum(v) / tot:>7.1f}%")
+        q = sorted(v)
+        print(f"{k:<50}{len(v):>8}{sum(v) / 1e3:>11.2f}{sum(v) / len(v):>10.2f}{100 * sum(v) / tot:>7.1f}%"
+              f"{q[len(q) // 2]:>8.2f}{q[min(len(q) - 1, (9 * len(q)) // 10)]:>8.2f}{q[-1]:>8.2f}")
     # timeline of the last dispatches: busy time (union of kernel intervals) vs wall span
     tail = rows[-a.last:]
     if tail:
