@@ -396,10 +396,11 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
 
     * ``rccl``: the same DP step with the exchange on RCCL (all-gather captured in the graphs), the
       transport A/B of the node;
-    * ``merge_plan`` / ``merge_noplan``: the headline's DP step with the plan-ahead row merge forced
-      on / off (``ROCFM_MERGE``), and ``push_copy``: with the copy push instead of the fused producer
-      push (``ROCFM_DP_PUSH=0``), each with ``phase_ms`` — the A/Bs behind ``dp.PLAN_MIN_W`` and the
-      push default;
+    * ``merge_plan`` (below PLAN_MIN_W ranks) / ``merge_noplan`` (from PLAN_MIN_W): the headline's DP
+      step with the other row merge than the default (``ROCFM_MERGE``), and ``push_copy`` (when the
+      headline used the fused producer push): with the copy push (``ROCFM_DP_PUSH=0``), each with
+      ``phase_ms`` beside the headline's — the A/Bs behind ``dp.PLAN_MIN_W`` and the push default
+      (only with one GPU per rank unless ``ROCFM_BENCH_AB=1``; ``=0`` skips them);
     * ``rowshard``: config 4 — the PS-equivalent row-sharded table at 100M rows
       (``…multiInstance.py:461-521``), p2p all-to-alls.
     Every window reports its own replica check and p2p shadow status."""
@@ -410,6 +411,9 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
 
     def run_window(name, build, env=None, phases=False):
         wd.window = name
+        t_w = time.perf_counter()
+        if rank == 0:
+            print(f"[bench] window {name} ...", file=sys.stderr, flush=True)
         err = None
         res = {}
         eng = None
@@ -465,8 +469,11 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
             out[f"{name}_error"] = err
         for k, v in res.items():
             out[f"{name}_{k}"] = v
+        if rank == 0:
+            print(f"[bench] window {name}: {time.perf_counter() - t_w:.1f} s{' (error)' if err else ''}",
+                  file=sys.stderr, flush=True)
 
-    from rocfm.parallel.dp import FusedDataParallel, pool_exchange_capacity
+    from rocfm.parallel.dp import PLAN_MIN_W, FusedDataParallel, pool_exchange_capacity
     from rocfm.parallel.emb_shard import FusedRowShard
 
     pool_ids = pool[0]
@@ -480,9 +487,18 @@ def multi_gpu_windows(a, spec, hp, params, dev, pool, world, rank, backend, out,
         return FusedDataParallel(spec, hp, B, dev, params=params, mode="dp", seed=a.seed, capacity=cap,
                                  compute_dtype=a.compute_dtype, exchange=a.dp_exchange)
 
-    run_window("merge_plan", dp_default, env={"ROCFM_MERGE": "plan"}, phases=True)
-    run_window("merge_noplan", dp_default, env={"ROCFM_MERGE": "noplan"}, phases=True)
-    run_window("push_copy", dp_default, env={"ROCFM_DP_PUSH": "0"}, phases=True)
+    # (the headline runs the default; each A/B window runs the other choice: the plan-ahead merge
+    # from PLAN_MIN_W ranks, the fused push wherever every rank has a GPU of its own)
+    # (only where every rank has a GPU of its own, or when asked for: on a shared GPU the windows
+    # measure the processes' contention — and the forced fused push of a rehearsal can starve there)
+    ab = os.environ.get("ROCFM_BENCH_AB", "auto")
+    if ab == "1" or (ab == "auto" and torch.cuda.device_count() >= world):
+        if world >= PLAN_MIN_W:
+            run_window("merge_noplan", dp_default, env={"ROCFM_MERGE": "noplan"}, phases=True)
+        else:
+            run_window("merge_plan", dp_default, env={"ROCFM_MERGE": "plan"}, phases=True)
+        if out.get("config", {}).get("fused_push"):
+            run_window("push_copy", dp_default, env={"ROCFM_DP_PUSH": "0"}, phases=True)
     from rocfm.data.synthetic import SyntheticCriteo
     from rocfm.models.deepfm import ModelSpec
 

@@ -107,7 +107,7 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
     """bench.py --gpus 4 relaunches itself under torch.distributed.run; 4 ranks share the GPU (gloo
     bootstrap), the DP exchange is the p2p push through multi-step graphs."""
     j, log = _bench(["--gpus", "4", "--steps", "32", "--warmup", "8", "--steps_per_graph", "16"],
-                    {"ROCFM_BENCH_BACKEND": "gloo"}, timeout=600)
+                    {"ROCFM_BENCH_BACKEND": "gloo", "ROCFM_BENCH_AB": "1"}, timeout=600)
     assert j["n_gpus"] == 4 and j["world_size"] == 4 and j["backend"] == "gloo", j
     # ranks sharing the GPU: the copy push (the fused one is the default with one GPU per rank)
     assert j["config"]["exchange"] == "p2p" and j["config"]["fused_push"] is False, (j, log[-2000:])
@@ -121,8 +121,10 @@ def test_bench_rehearsal_4_ranks_gloo_p2p():
         assert ph[k]["max"] >= ph[k]["min"], (k, ph)
     assert ph["step"]["min"] > 0 and ph["merge_mode"] and ph["cap"] > 0 and ph["push"] == "copy", ph
     assert not [k for k in j if k.endswith("_error")], j
-    for w in ("rccl", "rowshard"):
+    for w in ("rccl", "rowshard", "merge_plan"):
         assert j[f"{w}_examples_per_sec"] > 0 and j[f"{w}_replicas_consistent"] is True, (w, j)
+    # the merge A/B window (forced here on the shared GPU): the plan-ahead merge below PLAN_MIN_W
+    assert j["merge_plan_phase_ms"]["merge_mode"] == "plan" and "merge_noplan_examples_per_sec" not in j, j
     assert j["rowshard_exchange"] == "p2p" and j["rowshard_shadow_exchange"] == "ok", j
     assert j["rowshard_feature_size"] == 100_000_000, j
     # TFRecord-fed DP under the reference's record sharding (each rank reads its records through

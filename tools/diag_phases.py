@@ -41,7 +41,7 @@ def main():
     spec = ModelSpec(V, 39, K, layers, [0.5] * len(layers), l2_reg=1e-4)
     multi = os.environ.get("MULTI", "0") == "1"  # the multi-step graph path (fused step_tail)
     eng = FusedDeepFM(spec, OptHParams("Adam", 5e-4), B, dev, params=init_params(spec, 1), use_graph=multi,
-                      force_generic_kernels=generic)
+                      force_generic_kernels=generic, compute_dtype=os.environ.get("DTYPE", "bf16"))
     gen = SyntheticCriteo(V, 39, seed=1)
     g = torch.Generator(device=dev).manual_seed(1)
     pool = [gen.batch(B, dev, g) for _ in range(8)]
