@@ -12,11 +12,12 @@ Two Python extension modules are produced next to the package sources:
   Built with g++ so it works on CPU-only machines too.
 
 Usage: ``python build.py [--force] [-j N]``.  Incremental: an object is rebuilt only when its source or
-one of the headers it includes (transitively) is newer.
+one of the headers it includes (transitively) changed (content hash).
 """
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import re
 import subprocess
@@ -61,15 +62,27 @@ def _deps(src, seen=None):
     return seen
 
 
-def _newest_header(src):
-    return max((os.path.getmtime(h) for h in _deps(src)), default=0.0)
+def _digest(src):
+    """Content hash of a source and every header it includes (mtimes alone miss a header that a
+    checkout restored with an older time — an object built against another struct layout)."""
+    h = hashlib.sha1()
+    for f in [src] + sorted(_deps(src)):
+        with open(f, "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
 
 
 def _stale(obj, src):
-    if not os.path.exists(obj):
+    stamp = obj + ".sha1"
+    if not os.path.exists(obj) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(obj)
-    return t < os.path.getmtime(src) or t < _newest_header(src)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(src)
+
+
+def _stamp(obj, src):
+    with open(obj + ".sha1", "w") as f:
+        f.write(_digest(src))
 
 
 def _run(cmd):
@@ -97,6 +110,8 @@ def hip_objects(force, jobs):
         for err in ex.map(_run, todo):
             if err and "warning" in err:
                 sys.stderr.write(err)
+    for cmd in todo:
+        _stamp(cmd[-1], cmd[cmd.index("-c") + 1])
     return objs
 
 
@@ -113,6 +128,8 @@ def io_objects(force, jobs):
             todo.append(base + ["-c", s, "-o", o])
     with cf.ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, todo))
+    for cmd in todo:
+        _stamp(cmd[-1], cmd[cmd.index("-c") + 1])
     return objs
 
 
