@@ -1419,7 +1419,15 @@ class FusedDeepFM:
         """``n`` optimisation steps from the attached pool; full step-pairs are replayed from one
         multi-step HIP graph (``steps_per_graph`` steps per launch) to amortise launch overhead."""
         if self.use_graph and not self._ring and self.fuse_dense_opt and steps_per_graph > 1:
-            self._train_steps_multi(n, steps_per_graph)
+            hp = self._main_stream()
+            if hp is None:
+                self._train_steps_multi(n, steps_per_graph)
+                return
+            cur = torch.cuda.current_stream(self.device)
+            hp.wait_stream(cur)
+            with torch.cuda.stream(hp):
+                self._train_steps_multi(n, steps_per_graph)
+            cur.wait_stream(hp)
             return
         S = max(2, steps_per_graph // 2 * 2)
         while n > 0:
@@ -1438,6 +1446,17 @@ class FusedDeepFM:
             else:
                 self.train_step()
                 n -= 1
+
+    def _main_stream(self):
+        """ROCFM_MAIN_PRIORITY=1: the multi-step main graphs run on a high-priority stream (its
+        hardware queue's dispatches are served before the side chain's), or None."""
+        if os.environ.get("ROCFM_MAIN_PRIORITY", "0") != "1":
+            return None
+        st = getattr(self, "_hp_stream", None)
+        if st is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            st = self._hp_stream = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+        return st
 
     def train_step(self) -> None:
         """One optimisation step on the current batch (asynchronous)."""
