@@ -31,6 +31,14 @@
       (ptr)[blockIdx.x * 16 + (i)] = (unsigned long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
+// (diagnostics) where the workgroup runs: XCC id << 32 | HW_ID (CU id bits 8-11, SH bit 12, SE bits 13-15)
+#define ROCFM_STAMP_HWID(ptr, i)                                                                   \
+  do {                                                                                             \
+    if ((ptr) != nullptr && threadIdx.x == 0)                                                      \
+      (ptr)[blockIdx.x * 16 + (i)] = ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) | \
+                                     (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);         \
+  } while (0)
+
 namespace rocfm {
 
 constexpr int kWave = 64;

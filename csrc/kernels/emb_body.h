@@ -33,20 +33,21 @@ __device__ __forceinline__ float4 f4shfl_xor(float4 v, int d) {
 }
 
 // DPP lane moves (VALU, no LDS traffic; __shfl_* compile to ds_bpermute, which shares the LDS
-// pipe with the chunk's row staging): bound_ctrl → lanes without a source read 0
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, true));
-}
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ void dpp_add4(float4& v, bool take) {
-  const float x = dppf<CTRL, ROW_MASK>(v.x), y = dppf<CTRL, ROW_MASK>(v.y), z = dppf<CTRL, ROW_MASK>(v.z),
-              w = dppf<CTRL, ROW_MASK>(v.w);
-  v.x += take ? x : 0.f;
-  v.y += take ? y : 0.f;
-  v.z += take ? z : 0.f;
-  v.w += take ? w : 0.f;
-}
+// pipe with the chunk's row staging).
+// v += take · dpp(v) as ONE v_fmac_f32_dpp per float (m = take ? 1 : 0): the same bits as
+// v + (take ? x : 0) for finite x (x·1 = x exactly, x·0 = ±0 and v ± 0 = v; only a −0 run sum can
+// come out +0 instead).  Written out because the compiler keeps a separate v_mov_b32_dpp and packs
+// the fmas into v_pk_fma_f32 (no DPP form); the leading s_nop 1 is the two wait states a DPP read
+// needs after a VALU write of its source (the hazard recognizer does not see into inline asm).
+// Rows outside ROW_MASK are not written (v unchanged); bound_ctrl zero-fills sources outside the row.
+#define ROCFM_FMAC_DPP4(v, m, MOD)                                                                 \
+  asm volatile("s_nop 1\n\t"                                                                      \
+               "v_fmac_f32_dpp %0, %0, %4 " MOD "\n\t"                                            \
+               "v_fmac_f32_dpp %1, %1, %4 " MOD "\n\t"                                            \
+               "v_fmac_f32_dpp %2, %2, %4 " MOD "\n\t"                                            \
+               "v_fmac_f32_dpp %3, %3, %4 " MOD                                                    \
+               : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)                                         \
+               : "v"(m))
 
 // Inclusive segmented scan over the 64 lanes: v[lane] = Σ v[seg .. lane] (seg = the first lane of
 // this lane's segment, ≤ lane).  Rows of 16 lanes first (row_shr 1, 2, 4, 8), then row 0's last
@@ -59,18 +60,20 @@ __device__ __forceinline__ void seg_scan_dpp(float4 (&v)[N], int lane, int seg) 
   const bool t1 = rl >= 1 && lane - 1 >= seg, t2 = rl >= 2 && lane - 2 >= seg;
   const bool t4 = rl >= 4 && lane - 4 >= seg, t8 = rl >= 8 && lane - 8 >= seg;
   const bool t15 = (row & 1) && seg < (lane & ~15), t31 = row >= 2 && seg <= 31;
+  const float m1 = t1 ? 1.f : 0.f, m2 = t2 ? 1.f : 0.f, m4 = t4 ? 1.f : 0.f, m8 = t8 ? 1.f : 0.f;
+  const float m15 = t15 ? 1.f : 0.f, m31 = t31 ? 1.f : 0.f;
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x111, 0xf>(v[u], t1);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m1, "row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1");
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x112, 0xf>(v[u], t2);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m2, "row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1");
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x114, 0xf>(v[u], t4);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m4, "row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1");
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x118, 0xf>(v[u], t8);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m8, "row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1");
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x142, 0xa>(v[u], t15);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m15, "row_bcast:15 row_mask:0xa bank_mask:0xf");
 #pragma unroll
-  for (int u = 0; u < N; ++u) dpp_add4<0x143, 0xc>(v[u], t31);
+  for (int u = 0; u < N; ++u) ROCFM_FMAC_DPP4(v[u], m31, "row_bcast:31 row_mask:0xc bank_mask:0xf");
 }
 
 }  // namespace

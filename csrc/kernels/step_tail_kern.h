@@ -33,6 +33,7 @@ __global__ __launch_bounds__(kTailThreads) void step_tail_plan_kernel(const Wgra
   const int bid = blockIdx.x;
   unsigned long long* stp = bid < n_emb ? e.stamps : w.stamps;  // (diagnostics: entry / exit stamps 15 / 14)
   ROCFM_STAMP(stp, 15);
+  ROCFM_STAMP_HWID(stp, 13);
   if (bid < n_emb)
     emb_plan_body<KP4, BT>(e, bid);
   else

@@ -1159,8 +1159,25 @@ class FusedDeepFM:
                 and getattr(self, "m_req", None) == steps_per_graph and self._m_primed:
             self._precapture_multi(self._m_graphs, ("m",), n, self._multi_body)
 
-    def train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
-                     ring_batches: int = 0, build=None, run=None, prefix=None) -> int:
+    def train_stream(self, *args, **kwargs) -> int:
+        """``_train_stream``; under ``ROCFM_HAZARD=1`` with every torch write into the batch ring
+        observed on its stream as well (``hazard.ObservedWrites``: a copy the loop does not declare
+        is still checked)."""
+        if self._hazard is None:
+            return self._train_stream(*args, **kwargs)
+
+        def stream_name():
+            return getattr(self, "_plan_names", {}).get(torch.cuda.current_stream(self.device).cuda_stream, "?")
+
+        ring = lambda: {"ring": list(getattr(self, "_stream_ring", None) or ())}  # noqa: E731
+        with hazard.ObservedWrites(lambda: getattr(self, "_plan", None), ring, stream_of=stream_name) as obs:
+            try:
+                return self._train_stream(*args, **kwargs)
+            finally:
+                self.hazard_observed = obs.seen  # torch writes into the ring seen on their streams
+
+    def _train_stream(self, batches, steps_per_graph: int = 16, after_steps=None, hold: int = 1,
+                      ring_batches: int = 0, build=None, run=None, prefix=None) -> int:
         """Train on a stream of host batches (the Estimator's loader) through multi-step graphs.
 
         Batches are copied host → HBM on a copy stream into a device ring of 4·S batch slots, two
@@ -1199,6 +1216,11 @@ class FusedDeepFM:
         # ROCFM_HAZARD=1: every copy / side / main operation of this loop and its event waits go
         # into a happens-before plan, checked after each graph launch (utils/hazard.py StreamPlan)
         self._plan = hazard.StreamPlan() if self._hazard is not None else None
+        names = {}  # stream handle → plan stream name
+        if self._plan is not None:
+            names = {self._copy_stream.cuda_stream: "copy", self.sort_stream.cuda_stream: "side",
+                     torch.cuda.current_stream(dev).cuda_stream: "main"}
+        self._plan_names = names
         ring = getattr(self, "_stream_ring", None)
         if ring is None or ring[0].shape[0] != R:
             ring = (torch.zeros(R, self.B, self.F, dtype=torch.int32, device=dev),
@@ -1229,10 +1251,6 @@ class FusedDeepFM:
             copy.wait_stream(torch.cuda.current_stream(dev))
             if self._plan is not None:
                 self._plan.wait_stream("copy", "main")
-        names = {}  # stream handle → plan stream name
-        if self._plan is not None:
-            names = {copy.cuda_stream: "copy", self.sort_stream.cuda_stream: "side",
-                     torch.cuda.current_stream(dev).cuda_stream: "main"}
 
         def mark(stream):
             e = torch.cuda.Event()

@@ -250,6 +250,13 @@ class StreamPlan:
     streams only through the recorded waits (transitively).  ``check`` raises HazardError for two
     unordered operations whose ranges overlap with at least one write — e.g. a copy that refills a
     ring slot a side graph may still be reading (the event plan's ``copy.wait_event(sevs[j - 3])``).
+
+    Declared ranges are only as good as their annotations: a new write into the ring that the loop
+    does not declare would be invisible.  ``ObservedWrites`` closes that for torch ops: while it is
+    active every aten op that writes into a registered tensor (the ring) becomes an operation of the
+    plan on the stream it was issued on, with the slots it actually touched.  HIP-extension launches
+    (the device parser) are not torch ops; they stay declared (and, inside graph capture, observed by
+    ``Recorder``).
     """
 
     def __init__(self, window: int = 96):
@@ -337,3 +344,85 @@ class StreamPlan:
             raise HazardError(f"stream-plan hazard{(' in ' + tag) if tag else ''}: {len(found)} unordered "
                               "overlapping accesses with a write:\n" + "\n".join(lines))
         self.prune()
+
+
+# ---- observed writes: torch ops into registered tensors become plan operations ----------------------
+class ObservedWrites:
+    """Context manager: while active, every aten op writing (in place, or through ``out=``) into a
+    registered tensor is recorded in ``plan`` as an operation on the stream it was issued on
+    (``stream_of()`` → plan stream name; default: the current CUDA stream through ``names``, a map of
+    ``cuda_stream`` handles), with the range it touched in the tensor's leading-dimension units.
+
+    ``tensors`` = {range name: [tensors]}: e.g. ``{"ring": [ids, vals, labels]}`` — every tensor of
+    a name shares the slot numbering of its leading dimension, as the plan's declared ranges do.
+    ``plan`` and ``tensors`` may be callables, resolved at each write (the engine creates its plan
+    and ring inside the loop this wraps); a ``None`` plan records nothing."""
+
+    def __init__(self, plan, tensors, names=None, stream_of=None):
+        from torch.utils._python_dispatch import TorchDispatchMode
+
+        self._plan = plan if callable(plan) else (lambda: plan)
+        self._tensors = tensors if callable(tensors) else (lambda: tensors)
+        names = names or {}
+        if stream_of is None:
+            def stream_of():
+                return names.get(torch.cuda.current_stream().cuda_stream, "?")
+        self.stream_of = stream_of
+        self.seen = 0
+        outer = self
+
+        class _Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                kwargs = kwargs or {}
+                out = func(*args, **kwargs)
+                outer._note(func, args, kwargs)
+                return out
+
+        self._mode = _Mode()
+
+    def _written(self, func, args, kwargs):
+        schema = func._schema
+        for i, a in enumerate(schema.arguments):
+            if a.alias_info is None or not a.alias_info.is_write:
+                continue
+            v = args[i] if i < len(args) else kwargs.get(a.name)
+            if isinstance(v, torch.Tensor):
+                yield v
+            elif isinstance(v, (list, tuple)):
+                yield from (x for x in v if isinstance(x, torch.Tensor))
+
+    def _regions(self):
+        out = []  # (lo byte, hi byte, unit bytes, name)
+        for name, ts in (self._tensors() or {}).items():
+            for t in ts:
+                if t is not None and t.numel():
+                    lo = t.data_ptr()
+                    out.append((lo, lo + t.numel() * t.element_size(), t.stride(0) * t.element_size(), name))
+        return out
+
+    def _note(self, func, args, kwargs) -> None:
+        plan = self._plan()
+        if plan is None:
+            return
+        regions = self._regions()
+        ranges = []
+        for t in self._written(func, args, kwargs):
+            if t.numel() == 0:
+                continue
+            a = t.data_ptr()
+            e = a + t.numel() * t.element_size()  # (a contiguous view: the ring's slot slices are)
+            for lo, hi, unit, name in regions:
+                if a < hi and lo < e:
+                    s0 = (max(a, lo) - lo) // unit
+                    s1 = (min(e, hi) - lo + unit - 1) // unit
+                    ranges.append((name, int(s0), int(s1), True))
+        if ranges:
+            self.seen += 1
+            plan.op(self.stream_of(), f"observed {func}", ranges)
+
+    def __enter__(self):
+        self._mode.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        return self._mode.__exit__(*exc)

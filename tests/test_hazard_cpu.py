@@ -226,3 +226,31 @@ def test_stream_plan_stays_bounded_over_an_epoch_and_still_catches_a_late_race()
     assert len(p.ops) <= p.window and p.base > 14000
     with pytest.raises(HazardError, match="copy:stage"):
         _simulate_train_stream(8, 4100, early=True, early_at=4000, check_every=True)
+
+
+def test_observed_write_catches_unannotated_copy():
+    """An un-annotated copy into the ring (no ``plan.op`` for it) is still seen: ObservedWrites turns
+    the aten write into a plan operation on the issuing stream, so a refill that races a side-chain
+    read raises, and the same refill behind the side stream's event does not."""
+    import torch
+    from rocfm.utils.hazard import HazardError, ObservedWrites, StreamPlan
+
+    ring = torch.zeros(8, 4, 3)
+    src = torch.ones(2, 4, 3)
+    for ordered in (False, True):
+        plan = StreamPlan()
+        cur = ["side"]
+        plan.op("side", "side graph reads slots 2..5", [("ring", 2, 6, False)])
+        if ordered:
+            plan.wait_stream("copy", "side")
+        cur[0] = "copy"
+        with ObservedWrites(plan, {"ring": [ring]}, stream_of=lambda: cur[0]) as obs:
+            ring[3:5].copy_(src)  # the undeclared refill
+            torch.zeros(3).add_(1.0)  # a write outside the ring: not an operation
+        assert obs.seen == 1
+        assert plan.ops[-1][2] == [("ring", 3, 5, True)]
+        if ordered:
+            plan.check()
+        else:
+            with pytest.raises(HazardError, match="observed"):
+                plan.check()

@@ -108,9 +108,12 @@ def test_train_stream_three_stream_plan(raw, monkeypatch, tmp_path):
         src = ds.raw_groups(4, hold=2) if raw else ds.groups(4, hold=2)
         n = e.train_stream(src, 4, hold=2)
         torch.cuda.synchronize()
+        run.observed = e.hazard_observed
         return n
 
     assert run() == 40
+    if not raw:  # the H2D copies into the ring were also observed as torch writes on the copy stream
+        assert run.observed >= 30
     monkeypatch.setenv("ROCFM_HAZARD_INJECT", "ring")
     with pytest.raises(HazardError, match="ring"):
         run()

@@ -124,9 +124,27 @@ def main():
         stf = st.double()
         tot = (stf[:nw, 3] - stf[:nw, 0]) * 0.01
         order = torch.argsort(tot, descending=True)[:6]
+        # where each tail workgroup ran (stamp 13: XCC << 32 | HW_ID; CU = HW_ID bits 8-15)
+        wgs = wg[wg[:, 15] > 0]
+        hw = torch.cat([st[:nw, 13], wgs[:, 13]]).long()
+        place = [(int(h) >> 32, (int(h) >> 8) & 0xff) for h in hw.tolist()]
+        cnt = {}
+        for pl in place:
+            cnt[pl] = cnt.get(pl, 0) + 1
+        shared = {pl for pl, c in cnt.items() if c > 1}
+        per_xcc = [sum(1 for x, _ in place if x == k) for k in range(8)]
+        print(f"   placement: {len(cnt)} distinct CUs for {len(place)} tail workgroups; CUs holding 2+: {len(shared)}; "
+              f"workgroups per XCC {per_xcc}")
+        t0 = float(torch.cat([st[:nw, 15], wgs[:, 15]]).double().min())
         for w in order.tolist():
-            print(f"   slow item {w:3d}: total {tot[w]:.2f} us, entries {int(ent[w])}, heads {int(hd[w])}, "
-                  f"lead {int(it[w, 2])}, tail {int(it[w, 3])}")
+            ph = [(stf[w, j + 1] - stf[w, j]) * 0.01 for j in range(3)]
+            print(f"   slow item {w:3d}: total {tot[w]:.2f} us (entry +{(stf[w, 15] - t0) * 0.01:.2f}, phases "
+                  f"{ph[0]:.2f} / {ph[1]:.2f} / {ph[2]:.2f}), entries {int(ent[w])}, heads {int(hd[w])}, "
+                  f"lead {int(it[w, 2])}, tail {int(it[w, 3])}, xcc {place[w][0]} cu {place[w][1]:#04x}"
+                  f"{' SHARED' if place[w] in shared else ''}")
+        xt = [[float(tot[w]) for w in range(nw) if ent[w] > 0 and place[w][0] == k] for k in range(8)]
+        print("   item total by XCC (mean / max): " + ", ".join(
+            f"{k}: {sum(v) / len(v):.2f}/{max(v):.2f}" for k, v in enumerate(xt) if v))
         return
     report("emb_rows_update", s_emb.view(-1, 16).cpu(), [0, 1, 2, 3, 4],
            ["keys+rows+scan+heads", "end search", "continuation", "optimizer items"])
