@@ -47,13 +47,18 @@ __device__ __forceinline__ int plan_wave_base(int v, int* s_w) {
 // all (a workgroup-wide rank per 1024-entry tile cost two barriers each: 45 µs per launch).
 __global__ __launch_bounds__(kPlanThreads) void emb_plan_kernel(const EmbPlanParams p) {
   __shared__ int s_w[kPlanWaves + 1];
+  __shared__ int s_r0[kPlanMaxNw], s_r1[kPlanMaxNw];  // per item: first / last run whose head it holds
   const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6, n = p.n;
   const uint32_t* kb = p.skeys + (size_t)k * n;
   int32_t* runs = p.runs + (size_t)k * (n + 1);
   int* it = reinterpret_cast<int*>(p.items + (size_t)k * p.nw);  // {es, ee, lead, tail} per item
   int4* slots = p.slots + (size_t)k * p.nw;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (int j = t; j < p.nw; j += kPlanThreads) p.items[(size_t)k * p.nw + j] = make_int4(0, 0, -1, -1);
+  for (int j = t; j < p.nw; j += kPlanThreads) {
+    p.items[(size_t)k * p.nw + j] = make_int4(0, 0, -1, -1);
+    s_r0[j] = 0x7fffffff;
+    s_r1[j] = -1;
+  }
   // 1. run starts, compacted in order: count per wave segment, prefix over waves, write
   constexpr int kG = 8;  // 64-entry groups loaded before any is ranked
   const int seg = ((n + kPlanWaves - 1) / kPlanWaves + 63) & ~63;
@@ -142,6 +147,8 @@ __global__ __launch_bounds__(kPlanThreads) void emb_plan_kernel(const EmbPlanPar
       slot += __popcll(sm);
       if (!live) continue;
       const int ih = item_of(s, r);
+      atomicMin(&s_r0[ih], r);
+      atomicMax(&s_r1[ih], r);
       const int ip = r > 0 ? item_of(last_cut(sp, s), r - 1) : -1;
       if (ih != ip) {  // a new item starts at this head
         it[4 * ih + 0] = s;
@@ -167,12 +174,36 @@ __global__ __launch_bounds__(kPlanThreads) void emb_plan_kernel(const EmbPlanPar
       if (r == U - 1) it[4 * cur + 1] = n;
     }
   }
+  if (!p.hslab) return;
+  // 3. each item's run-head keys in order, behind its head count (the tail prefetches their rows)
+  __syncthreads();
+  uint32_t* slab = p.hslab + (size_t)k * p.nw * kPlanSlab;
+  for (int j = t; j < p.nw; j += kPlanThreads) slab[(size_t)j * kPlanSlab] = s_r1[j] >= 0 ? (uint32_t)(s_r1[j] - s_r0[j] + 1) : 0u;
+  for (int g0 = q0; g0 < q1; g0 += 64 * kR) {
+    int rs[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int r = g0 + 64 * q + lane;
+      rs[q] = r < q1 ? runs[r] : 0;
+    }
+    uint32_t key[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) key[q] = kb[rs[q]];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int r = g0 + 64 * q + lane;
+      if (r >= q1) continue;
+      const int ih = item_of(rs[q], r), j = r - s_r0[ih];
+      if (j < kPlanSlab - 1) slab[(size_t)ih * kPlanSlab + 1 + j] = key[q];
+    }
+  }
 }
 
 void launch_emb_plan(const EmbPlanParams& p, hipStream_t stream) {
   ROCFM_REQUIRE(p.n > 0 && p.S > 0 && p.nw > 0 && p.beta >= 0 && p.lsplit >= 64, "emb_plan: bad sizes");
   ROCFM_REQUIRE((long long)p.n * (1 + p.beta) + p.nw < (1ll << 31), "emb_plan: cost positions exceed 32 bits");
   ROCFM_REQUIRE(p.skeys && p.runs && p.items && p.slots, "emb_plan: buffers missing");
+  ROCFM_REQUIRE(p.nw <= kPlanMaxNw, "emb_plan: more items than the kernel's head ranges hold");
   // item bounds the planned tail relies on (emb_plan_body.h): heads ≤ Q/(1+beta) + 1 ≤ kPlanHcap
   const long long qmax = ((long long)p.n * (1 + p.beta) + p.nw - 1) / p.nw;
   ROCFM_REQUIRE(qmax / (1 + p.beta) + 2 <= kPlanHcap, "emb_plan: too few items for the batch (raise nw)");

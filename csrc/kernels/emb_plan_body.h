@@ -92,6 +92,35 @@ __device__ __forceinline__ void emb_plan_body(const EmbUpdateParams& p, const in
     if (p.s0) ca = reinterpret_cast<const float4*>(p.s0)[cidx];
     if (p.s1) cb = reinterpret_cast<const float4*>(p.s1)[cidx];
   }
+  // 0. the table / Adam-slot rows of the item's complete runs (first 4·512 (run, float4 column)
+  //    items), loaded now from the plan's head-key slab so they arrive under phase 1's scan; the
+  //    count and the keys are independent loads (one memory latency, then the rows)
+  float4 w[4], a[4], b[4];
+  size_t idx4[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    w[u] = a[u] = b[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    idx4[u] = 0;
+  }
+  int pf_heads = -1;  // the slab's head count (-1: no slab; phase 2 loads the rows itself)
+  if (p.plan_hslab) {
+    const uint32_t* slab = p.plan_hslab + (size_t)bid * kPlanSlab;
+    uint32_t hk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) hk[u] = slab[1 + min((u * kT + t) / KP4, kPlanSlab - 2)];
+    pf_heads = (int)slab[0];
+    const int pf_items = (pf_heads - (tail >= 0 ? 1 : 0)) * KP4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int itm = u * kT + t;
+      idx4[u] = (size_t)((hk[u] - (uint32_t)p.id_offset) / (uint32_t)p.id_stride) * KP4 + (itm % KP4);
+      if (itm < pf_items) {
+        w[u] = tbl_load4<BT>(p.emb, idx4[u]);
+        if (p.s0) a[u] = reinterpret_cast<const float4*>(p.s0)[idx4[u]];
+        if (p.s1) b[u] = reinterpret_cast<const float4*>(p.s1)[idx4[u]];
+      }
+    }
+  }
   ROCFM_STAMP(p.stamps, 0);
   // 1. pieces; the next round's keys and gradient rows are loaded before this round is scanned
   int np = 0, nh = 0;
@@ -175,8 +204,8 @@ __device__ __forceinline__ void emb_plan_body(const EmbUpdateParams& p, const in
   //    the drain of the publish stores runs under them
   const int nfull = nh - (tail >= 0 ? 1 : 0);
   const int nitems = nfull * KP4;
-  float4 w[4], a[4], b[4];
-  size_t idx4[4];
+  if (pf_heads >= 0 && pf_heads != nh && t == 0)  // the slab disagrees with the item's keys: a plan bug
+    atomicOr(reinterpret_cast<int*>(p.plan_ctr) + p.plan_nw, 4);
   auto load_items = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -190,7 +219,7 @@ __device__ __forceinline__ void emb_plan_body(const EmbUpdateParams& p, const in
       b[u] = p.s1 ? reinterpret_cast<const float4*>(p.s1)[idx4[u]] : z;
     }
   };
-  if (nitems > 0) load_items(0);
+  if (nitems > 0 && pf_heads != nh) load_items(0);  // (prefetched at entry when the slab is there)
   if (lead >= 0) {  // arrival: the pieces drained first, then one counter increment
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -76,6 +76,9 @@ struct EmbUpdateParams {
   // [plan_nw] arrival counters (zero between launches: the last arrival resets its slot)
   const int4* plan_items;
   const int4* plan_slots;
+  // nullable: per item [kPlanSlab] words — [0] its run-head count, [1 ..] the heads' keys in order —
+  // so the table / Adam-slot rows of its complete runs are loaded at entry, under the scan
+  const uint32_t* plan_hslab;
   int plan_nw;
   float* plan_win;
   float* plan_head;
@@ -96,11 +99,14 @@ struct EmbPlanParams {
   int32_t* runs;          // scratch [S][n + 1]
   int4* items;            // [S][nw]
   int4* slots;            // [S][nw]
+  uint32_t* hslab;        // nullable: [S][nw][kPlanSlab] run-head count and keys per item
 };
 void launch_emb_plan(const EmbPlanParams& p, hipStream_t stream);
 // the planned tail's bounds (emb_plan_body.h): run heads and window pieces per item
 constexpr int kPlanHcap = 264;
 constexpr int kPlanPcap = kPlanHcap + 64;
+constexpr int kPlanSlab = 272;     // words per item of the head-key slab (≥ kPlanHcap + 1)
+constexpr int kPlanMaxNw = 1024;   // items per batch the plan kernel's LDS head ranges hold
 
 struct EmbDenseParams {
   float* emb;

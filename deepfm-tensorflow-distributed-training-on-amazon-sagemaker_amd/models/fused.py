@@ -866,6 +866,10 @@ class FusedDeepFM:
         self.m_pitems = torch.zeros(2, Smax * nw * 4, **i32)
         self.m_pslots = torch.zeros(2, Smax * nw * 4, **i32)
         self.m_pruns = torch.zeros(Smax * (n + 1), **i32)
+        # per item its run heads' keys (the tail prefetches their table rows at entry); ROCFM_EMB_HSLAB=0: off
+        self.m_hslab_on = os.environ.get("ROCFM_EMB_HSLAB", "1") != "0"
+        slab = int(H.plan_bounds()[2])
+        self.m_phslab = torch.zeros(2, Smax * nw * slab if self.m_hslab_on else 1, **i32)
         self.m_pwin = torch.zeros((n // 64 + 2) * self.Kp, dtype=torch.float32, device=dev)
         self.m_phead = torch.zeros(nw * self.Kp, dtype=torch.float32, device=dev)
         self.m_pctr = torch.zeros(nw + 4, **i32)  # [nw]: sticky "item outside the plan's bounds" flag
@@ -876,6 +880,7 @@ class FusedDeepFM:
                     continue
                 ep.plan_items = self.m_pitems[q, k * nw * 4:].data_ptr()
                 ep.plan_slots = self.m_pslots[q, k * nw * 4:].data_ptr()
+                ep.plan_hslab = self.m_phslab[q, k * nw * slab:].data_ptr() if self.m_hslab_on else 0
                 ep.plan_nw = nw
                 ep.plan_win, ep.plan_head = self.m_pwin.data_ptr(), self.m_phead.data_ptr()
                 ep.plan_ctr = self.m_pctr.data_ptr()
@@ -888,6 +893,7 @@ class FusedDeepFM:
         pp.n, pp.S, pp.nw = self.n_lookup, self.mS, self.m_plan_nw
         pp.beta, pp.lsplit = self.m_plan_beta, self.m_plan_lsplit
         pp.runs, pp.items, pp.slots = self.m_pruns.data_ptr(), self.m_pitems[q].data_ptr(), self.m_pslots[q].data_ptr()
+        pp.hslab = self.m_phslab[q].data_ptr() if self.m_hslab_on else 0
         H.emb_plan(pp, stream.cuda_stream)
 
     def _fetch_multi_params(self, q: int, advance: int):
@@ -1638,6 +1644,8 @@ class FusedDeepFM:
                 raise RuntimeError("step_tail (planned embedding role): "
                                    + ("an item exceeded the plan's bounds " if err & 1 else "")
                                    + ("a split run's head item timed out waiting for its lead items " if err & 2 else "")
+                                   + ("an item's head-key slab disagreed with its keys (rows reloaded; a plan "
+                                      "kernel bug) " if err & 4 else "")
                                    + "(those rows were not updated)")
         if self.id_guard and int(self.bad_ids.item()) != 0:
             raise ValueError(f"ROCFM_CHECK_IDS: a batch held feature ids outside [0, {self.id_limit}) "

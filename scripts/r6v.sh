@@ -1,0 +1,19 @@
+# Round 6 (v): the plan's per-item head-key slab — table / Adam rows prefetched at tail entry (A/B by env)
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6v
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_emb_plan_gpu.py tests/test_fused_kernels_gpu.py tests/test_trajectory_gpu.py tests/test_bf16_table_gpu.py tests/test_hazard_gpu.py -x -q --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+NB="--embedding_size 32 --feature_size 117581"
+B="python bench.py --gpus 1 --no_secondary"
+for rep in 1 2 3; do
+  for v in 1 0; do
+    ROCFM_EMB_HSLAB=$v timeout -k 10 150 $B --steps 20 --warmup 5 > $O/s${v}_d20_$rep.json 2>/dev/null || exit 1
+    ROCFM_EMB_HSLAB=$v timeout -k 10 150 $B --steps 20 --warmup 5 $NB > $O/s${v}_n20_$rep.json 2>/dev/null || exit 1
+  done
+done
+for v in 1 0; do
+  ROCFM_EMB_HSLAB=$v timeout -k 10 150 $B --steps 200 --warmup 20 > $O/s${v}_d200.json 2>/dev/null || exit 1
+  ROCFM_EMB_HSLAB=$v timeout -k 10 150 $B --steps 200 --warmup 20 $NB > $O/s${v}_n200.json 2>/dev/null || exit 1
+  ROCFM_EMB_HSLAB=$v MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_d_s${v}.txt 2>&1 || exit 1
+  ROCFM_EMB_HSLAB=$v K=32 V=117581 MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_n_s${v}.txt 2>&1 || exit 1
+done

@@ -41,9 +41,12 @@ def test_emb_plan_kernel_matches_reference(beta, lsplit):
             items = torch.full((S, nw, 4), 7, dtype=torch.int32, device=dev)
             slots = torch.zeros(S, nw, 4, dtype=torch.int32, device=dev)
             runs = torch.zeros(S * (n + 1), dtype=torch.int32, device=dev)
+            slab_w = H.plan_bounds()[2]
+            hslab = torch.full((S, nw, slab_w), -5, dtype=torch.int32, device=dev)
             pp = H.EmbPlanParams()
             pp.skeys, pp.n, pp.S, pp.nw, pp.beta, pp.lsplit = kd.data_ptr(), n, S, nw, beta, lsplit
             pp.runs, pp.items, pp.slots = runs.data_ptr(), items.data_ptr(), slots.data_ptr()
+            pp.hslab = hslab.data_ptr()
             H.emb_plan(pp, torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             ri, rs = R.emb_plan_reference(keys, nw, beta, lsplit)
@@ -51,6 +54,16 @@ def test_emb_plan_kernel_matches_reference(beta, lsplit):
             for k in range(S):
                 np.testing.assert_array_equal(items[k].cpu().numpy(), ri, err_msg=f"n={n} nw={nw}")
                 np.testing.assert_array_equal(slots[k, :ns].cpu().numpy(), rs[:ns])
+            # the head-key slab: per item its run heads' count, then their keys in order
+            head = np.ones(n, bool)
+            head[1:] = keys[1:] != keys[:-1]
+            hs = hslab.cpu().numpy()
+            for k in range(S):
+                for j in range(nw):
+                    a, b = ri[j, 0], ri[j, 1]
+                    hk = keys[a:b][head[a:b]] if b > a else keys[:0]
+                    assert hs[k, j, 0] == hk.size, f"n={n} nw={nw} item {j}"
+                    np.testing.assert_array_equal(hs[k, j, 1:1 + hk.size], hk.astype(np.int32))
             live = ri[:, 1] > ri[:, 0]
             e = ri[live][:, :2]
             assert e[0, 0] == 0 and e[-1, 1] == n and (e[1:, 0] == e[:-1, 1]).all()  # a partition

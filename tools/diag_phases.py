@@ -102,6 +102,15 @@ def main():
         print(f"== step tail (all {ent.numel()} workgroups): first entry → last exit {float(ex[-1]):.2f} us; entry "
               f"offsets p50 {q(off, .5):.2f} p90 {q(off, .9):.2f} max {float(off[-1]):.2f}; exits p50 {q(ex, .5):.2f} "
               f"p90 {q(ex, .9):.2f} max {float(ex[-1]):.2f}")
+        # the last exits by role (emb: its workgroup index; wgrad: its index among the wgrad workgroups)
+        ne = int((em[:, 15] > 0).sum())
+        rows_ = [("emb", i, float(em[i, 15] - t0) * 0.01, float(em[i, 14] - t0) * 0.01)
+                 for i in range(em.shape[0]) if em[i, 15] > 0]
+        rows_ += [("wgrad", i, float(wg[i, 15] - t0) * 0.01, float(wg[i, 14] - t0) * 0.01)
+                  for i in range(wg.shape[0]) if wg[i, 15] > 0]
+        rows_.sort(key=lambda r: -r[3])
+        print("   last exits: " + "; ".join(f"{r} {i} (entry {a:.2f}, exit {b:.2f})" for r, i, a, b in rows_[:6])
+              + f"  [{ne} emb workgroups]")
     if getattr(eng, "m_eplan", False) and multi:  # the planned embedding role (emb_plan_body.h)
         st = s_emb.view(-1, 16).cpu()
         report("emb_plan (planned items)", st, [0, 1, 2, 3],
