@@ -224,12 +224,13 @@ def main():
 
     if a.steps_per_graph <= 0:
         a.steps_per_graph = max(2, min(64, a.steps))
-    run(a.warmup)
     shadow = getattr(eng, "shadow", None)
-    while shadow is not None and shadow.active:  # p2p self-validation window: always untimed
-        eng.train_step()
-    if hasattr(eng, "precapture"):
-        eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region
+    if not warm_capture_first(eng, run, a.warmup, a.steps, a.steps_per_graph):
+        run(a.warmup)
+        while shadow is not None and shadow.active:  # p2p self-validation window: always untimed
+            eng.train_step()
+        if hasattr(eng, "precapture"):
+            eng.precapture(a.steps, a.steps_per_graph)  # graph captures stay out of the timed region
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
@@ -335,6 +336,24 @@ def main():
 
 
 _CTRL = []
+
+
+def warm_capture_first(eng, run, warmup: int, steps: int, spg: int) -> bool:
+    """Single-GPU fused engine: warm-up step 1 (eager: code objects load), then capture every graph
+    the remaining warm-up AND the timed window will launch, then warm-up steps 2..W — so the timed
+    window starts right behind W-1 graph-replayed warm-up steps instead of behind the capture's
+    idle gap (the GPU's clocks drop while the host captures; profiles/r6_window_fixed_cost.md).
+    Same W untimed steps, same K timed steps.  ROCFM_BENCH_CAPTURE_FIRST=0: capture after the
+    warm-up (the round-5 order).  Returns False when not applicable."""
+    from rocfm.models.fused import FusedDeepFM
+
+    if (type(eng) is not FusedDeepFM or warmup < 2 or spg < 2
+            or os.environ.get("ROCFM_BENCH_CAPTURE_FIRST", "1") != "1"):
+        return False
+    run(1)
+    eng.precapture([warmup - 1, steps], spg)
+    run(warmup - 1)
+    return True
 
 
 def _ctrl_barrier():
@@ -646,8 +665,9 @@ def secondary_windows(a, spec, hp, params, dev, pool):
                       compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
     eng.attach_pool(*pool)
     S = a.steps_per_graph
-    eng.train_steps(a.warmup, S)
-    eng.precapture(a.steps, S)
+    if not warm_capture_first(eng, lambda n: eng.train_steps(n, S), a.warmup, a.steps, S):
+        eng.train_steps(a.warmup, S)
+        eng.precapture(a.steps, S)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     eng.train_steps(a.steps, S)
@@ -675,8 +695,9 @@ def secondary_windows(a, spec, hp, params, dev, pool):
                              compute_dtype=a.compute_dtype, table_dtype=a.table_dtype)
             e2.attach_pool(torch.stack([x[0] for x in pb]), torch.stack([x[1] for x in pb]),
                            torch.stack([x[2] for x in pb]))
-            e2.train_steps(a.warmup, S)
-            e2.precapture(a.steps, S)
+            if not warm_capture_first(e2, lambda n: e2.train_steps(n, S), a.warmup, a.steps, S):
+                e2.train_steps(a.warmup, S)
+                e2.precapture(a.steps, S)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             e2.train_steps(a.steps, S)
@@ -737,8 +758,9 @@ def scale_windows(a, spec, hp, dev):
             build_s = time.perf_counter() - t0
             resident = torch.cuda.memory_allocated(dev)
             eng.attach_pool(*pool)
-            eng.train_steps(a.warmup, S)
-            eng.precapture(a.steps, S)
+            if not warm_capture_first(eng, lambda n: eng.train_steps(n, S), a.warmup, a.steps, S):
+                eng.train_steps(a.warmup, S)
+                eng.precapture(a.steps, S)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             eng.train_steps(a.steps, S)

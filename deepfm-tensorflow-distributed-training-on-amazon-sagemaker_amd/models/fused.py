@@ -296,6 +296,12 @@ class FusedDeepFM:
         from ..utils.streams import engine_streams
 
         self.sort_stream, self.aux_stream, self._copy_stream = engine_streams(dev)
+        # ROCFM_LEAN_LAUNCH (bit mask, multi-step graph launches; profiles/r6_window_fixed_cost.md):
+        # bit 0 preallocated launch events + no wait on a side graph already complete, bit 1 lazy
+        # trailing join of the side chain
+        self._lean_launch = int(os.environ.get("ROCFM_LEAN_LAUNCH", "3"))
+        self._lean_evs = [[torch.cuda.Event(), torch.cuda.Event()] for _ in range(2)]
+        self._side_join_pending = False
         # inference buffers (separate from the training slots)
         self.pred_ids = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
         self.pred_vals = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
@@ -544,6 +550,7 @@ class FusedDeepFM:
 
     def attach_pool(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor, start: int = 0) -> None:
         """Train from a device-resident pool of batches ([NB,B,F] ids/vals, [NB,B] labels), cycling."""
+        self._join_side_chain()
         self._set_pool(ids, vals, labels)
         self._ring = False
         self._build_fetch()
@@ -555,6 +562,7 @@ class FusedDeepFM:
 
     def push_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: torch.Tensor) -> None:
         """Ring mode: enqueue the next batch (must stay exactly one batch ahead of train_step)."""
+        self._join_side_chain()
         if not self._ring:
             raise RuntimeError("push_batch() is for the loader ring; this engine trains from an attached pool")
         n = ids.shape[0]
@@ -571,6 +579,7 @@ class FusedDeepFM:
 
         Non-pipelined (re-primes the input slot); use push_batch/attach_pool for full speed.
         """
+        self._join_side_chain()
         if labels is None:
             labels = torch.zeros(ids.shape[0], device=ids.device)
         if not self._ring:
@@ -601,6 +610,7 @@ class FusedDeepFM:
 
     def set_lr_scale(self, s: float) -> None:
         """Multiply the learning rate (Horovod's lr × world size, HVD:171)."""
+        self._join_side_chain()
         self.lr_scale = float(s)
         for lst in (self.wgrad_params, self.dense_apply_params, self.emb_params, self.emb_dense_params):
             for p, q in enumerate(lst):
@@ -626,6 +636,7 @@ class FusedDeepFM:
 
     def refresh_bf16(self) -> None:
         """Rewrite the bf16 / swizzled (and fp8) weight copies from the f32 master weights."""
+        self._join_side_chain()
         dp = self.dense_apply_params[0]
         dp.apply = 0
         if self.w8 is not None:  # host refresh: the exact max in both slots, no accumulation
@@ -652,6 +663,7 @@ class FusedDeepFM:
 
     def prime(self) -> None:
         """Fetch + sort the current step's batch into its slot (before the first step / after a reset)."""
+        self._join_side_chain()
         p = self._i % 2
         base = 0 if self._ring else getattr(self, "_start_batch", 0)
         self.cursor[p] = base + self._i
@@ -965,6 +977,7 @@ class FusedDeepFM:
             self._m_post(1 - q, stream)
 
     def _prime_multi(self) -> None:
+        self._join_side_chain()
         base = 0 if self._ring else getattr(self, "_start_batch", 0)
         self.m_cur[1] = base + self._i
         self.m_step[1] = self._i
@@ -1054,10 +1067,19 @@ class FusedDeepFM:
             # main graph submitted first: its kernels start while the host is still submitting the
             # side graph (a timed window otherwise begins with the side graph's whole submission);
             # the side graph still waits only for the main work queued BEFORE this main graph
-            before = self._pl_mark(torch.cuda.Event(), "main")
+            lean = self._lean_launch
+            if lean & 1:
+                # (ROCFM_LEAN_LAUNCH bit 0) two preallocated events per parity instead of two
+                # hipEventCreate calls ahead of the replay, and no barrier packet for a side graph the
+                # host already sees complete (the window's first graph after a synchronize)
+                evs = self._lean_evs[q]
+                before = self._pl_mark(evs[0], "main")
+            else:
+                before = self._pl_mark(torch.cuda.Event(), "main")
             before.record(main)
             if self._m_side_ev is not None:
-                main.wait_event(self._m_side_ev)
+                if not (lean & 1) or not self._m_side_ev.query():
+                    main.wait_event(self._m_side_ev)
                 self._pl_wait("main", self._m_side_ev)
             st = getattr(self, "stall_timing", None)  # diagnostics (bench): GPU-side gaps of the main stream
             if st is not None:
@@ -1075,25 +1097,27 @@ class FusedDeepFM:
             if st is not None:
                 t_side.record(side)
                 st.append((t_start, t_end, t_side))
-            ev = self._pl_mark(torch.cuda.Event(), "side")
+            ev = self._pl_mark(evs[1] if lean & 1 else torch.cuda.Event(), "side")
             ev.record(side)
         self._m_side_ev = ev
         self._m_warm += 1
         self._mq ^= 1
         self._i += S
 
-    def _precapture_multi(self, graphs: dict, key: tuple, n: int, body, capture_error_mode: str = "global") -> None:
+    def _precapture_multi(self, graphs: dict, key: tuple, n, body, capture_error_mode: str = "global") -> None:
         """Capture every (parity, S) graph pair that ``n`` more steps will launch, so that no
-        capture lands inside a timed region (e.g. the S < Smax remainder graph)."""
+        capture lands inside a timed region (e.g. the S < Smax remainder graph).  ``n`` may be a
+        list of consecutive ``train_steps`` call lengths (each split into graphs on its own)."""
         if self._m_warm < 1:
             return
         q0 = self._mq
         try:
-            while n > 0:
-                S = min(n, self.mS)
-                self._launch_multi(graphs, key, S, body, capture_error_mode, capture_only=True)
-                self._mq ^= 1
-                n -= S
+            for m in ([n] if isinstance(n, int) else n):
+                while m > 0:
+                    S = min(m, self.mS)
+                    self._launch_multi(graphs, key, S, body, capture_error_mode, capture_only=True)
+                    self._mq ^= 1
+                    m -= S
         finally:
             self._mq = q0
 
@@ -1152,8 +1176,20 @@ class FusedDeepFM:
             S = min(n, self.mS)
             self._run_multi_graph(S)
             n -= S
-        torch.cuda.current_stream(self.device).wait_stream(self.sort_stream)
+        if self._lean_launch & 2:
+            # (ROCFM_LEAN_LAUNCH bit 1) no trailing barrier packet: the side graph only writes the
+            # next graph's batch buffers, which the next main graph already waits for (_m_side_ev);
+            # every other reader joins first (_join_side_chain)
+            self._side_join_pending = True
+        else:
+            torch.cuda.current_stream(self.device).wait_stream(self.sort_stream)
         self._primed = False  # the per-step path re-primes from the global step if used next
+
+    def _join_side_chain(self) -> None:
+        """Order the current stream after the multi-step side chain (lazy trailing join)."""
+        if getattr(self, "_side_join_pending", False):
+            torch.cuda.current_stream(self.device).wait_stream(self.sort_stream)
+            self._side_join_pending = False
 
     def _run_multi_graph(self, S: int) -> None:
         """One multi-step graph of S steps (eager the first time: code objects load outside capture)."""
@@ -1169,6 +1205,7 @@ class FusedDeepFM:
         """``_train_stream``; under ``ROCFM_HAZARD=1`` with every torch write into the batch ring
         observed on its stream as well (``hazard.ObservedWrites``: a copy the loop does not declare
         is still checked)."""
+        self._join_side_chain()
         if self._hazard is None:
             return self._train_stream(*args, **kwargs)
 
@@ -1484,6 +1521,7 @@ class FusedDeepFM:
 
     def train_step(self) -> None:
         """One optimisation step on the current batch (asynchronous)."""
+        self._join_side_chain()
         if not self.fuse_dense_opt:
             raise RuntimeError("train_step() is the single-GPU step; distributed steps live in rocfm.parallel")
         self._m_primed = False
@@ -1507,6 +1545,7 @@ class FusedDeepFM:
     @torch.no_grad()
     def predict_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor] = None):
         """Probabilities (and per-row losses) for any number of rows; no dropout, no update."""
+        self._join_side_chain()
         n = ids.shape[0]
         if n > self.B:
             out = [self.predict_batch(ids[i:i + self.B], vals[i:i + self.B],
@@ -1562,6 +1601,7 @@ class FusedDeepFM:
 
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         """TF-named variables + optimizer slots + global_step (CPU tensors)."""
+        self._join_side_chain()
         torch.cuda.synchronize(self.device)
         self.check()
         sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
@@ -1582,6 +1622,7 @@ class FusedDeepFM:
         return sd
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        self._join_side_chain()
         with torch.no_grad():
             self._load_views(sd, "", self.emb, self.dense, strict)
             for k, view in self._bn_views().items():
@@ -1631,6 +1672,7 @@ class FusedDeepFM:
         """Raise if a batch-norm grid barrier of the row kernel timed out (the step's moments are
         then invalid; a sticky device flag, read with one small copy), or if the device Example
         parser flagged a malformed record (its steps were halted, never trained)."""
+        self._join_side_chain()
         self._check_decode(block=True)
         if self.bn and int(self.bn_error[0].item()) != 0:
             raise RuntimeError("deepfm_rows: a batch_norm grid barrier timed out (not every workgroup was resident)")

@@ -24,6 +24,11 @@ def report(name, st, idx, labels):
     tot = (st[:, -1] - st[:, 0]) * 0.01
     span = (st[:, -1].max() - st[:, 0].min()) * 0.01
     print(f"== {name}: {int(valid.sum())} workgroups, kernel span {span:.2f} us, per-WG total mean {tot.mean():.2f} max {tot.max():.2f}")
+    off = ((st[:, 0] - st[:, 0].min()) * 0.01).sort().values
+    if off.numel():
+        q = lambda f: float(off[min(off.numel() - 1, int(f * off.numel()))])  # noqa: E731
+        print(f"   entry offsets p50 {q(.5):.2f} p90 {q(.9):.2f} p99 {q(.99):.2f} max {float(off[-1]):.2f}; "
+              f"workgroups entering > 2 us late: {int((off > 2).sum())}")
     for i in range(d.shape[1]):
         print(f"   {labels[i]:<28} mean {d[:, i].mean():7.2f}  max {d[:, i].max():7.2f}")
 
