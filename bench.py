@@ -339,20 +339,38 @@ _CTRL = []
 
 
 def warm_capture_first(eng, run, warmup: int, steps: int, spg: int) -> bool:
-    """Single-GPU fused engine: warm-up step 1 (eager: code objects load), then capture every graph
-    the remaining warm-up AND the timed window will launch, then warm-up steps 2..W — so the timed
-    window starts right behind W-1 graph-replayed warm-up steps instead of behind the capture's
-    idle gap (the GPU's clocks drop while the host captures; profiles/r6_window_fixed_cost.md).
-    Same W untimed steps, same K timed steps.  ROCFM_BENCH_CAPTURE_FIRST=0: capture after the
-    warm-up (the round-5 order).  Returns False when not applicable."""
+    """Warm-up order: capture every graph the LAST warm-up steps and the timed window will launch,
+    then run those warm-up steps — so the timed window starts right behind graph-replayed warm-up
+    steps instead of behind the capture's idle gap (a 20-step window measured ≈2 µs/step slower
+    there; profiles/r6_window_fixed_cost.md).  Same W untimed steps, same K timed steps.
+
+    * single-GPU fused engine: warm-up step 1 (eager: code objects load), capture, steps 2..W;
+    * DP / row-shard engines: warm-up steps 1..W-m (p2p shadow-validated steps and the eager first
+      graph among them), capture, the last m = W // 2 steps; if the multi-step path has not
+      launched by then (all of them were shadow steps) the round-5 order is kept.
+    ROCFM_BENCH_CAPTURE_FIRST=0: capture after the warm-up (the round-5 order).  Returns False when
+    not applied (the caller then runs the warm-up and captures itself)."""
     from rocfm.models.fused import FusedDeepFM
 
-    if (type(eng) is not FusedDeepFM or warmup < 2 or spg < 2
+    if (warmup < 2 or spg < 2 or not hasattr(eng, "precapture")
             or os.environ.get("ROCFM_BENCH_CAPTURE_FIRST", "1") != "1"):
         return False
-    run(1)
-    eng.precapture([warmup - 1, steps], spg)
-    run(warmup - 1)
+    if type(eng) is FusedDeepFM:
+        run(1)
+        eng.precapture([warmup - 1, steps], spg)
+        run(warmup - 1)
+        return True
+    m = warmup // 2
+    run(warmup - m)
+    shadow = getattr(eng, "shadow", None)
+    while shadow is not None and shadow.active:  # p2p self-validation window: always untimed
+        eng.train_step()
+    if getattr(getattr(eng, "eng", eng), "_m_warm", 0) < 1:  # the multi-step path has not launched yet
+        run(m)
+        eng.precapture(steps, spg)
+        return True
+    eng.precapture([m, steps], spg)
+    run(m)
     return True
 
 
