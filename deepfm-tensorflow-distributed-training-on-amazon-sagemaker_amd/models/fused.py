@@ -302,6 +302,9 @@ class FusedDeepFM:
         self._lean_launch = int(os.environ.get("ROCFM_LEAN_LAUNCH", "3"))
         self._lean_evs = [[torch.cuda.Event(), torch.cuda.Event()] for _ in range(2)]
         self._side_join_pending = False
+        # ROCFM_SIDE_AFTER_MAIN=1 (diagnostic): serialise each side graph behind its main graph, to
+        # measure what the overlapped side chain costs the main chain
+        self._side_after_main = os.environ.get("ROCFM_SIDE_AFTER_MAIN", "0") == "1"
         # inference buffers (separate from the training slots)
         self.pred_ids = torch.zeros(Bp, F, dtype=torch.int32, device=dev)
         self.pred_vals = torch.zeros(Bp, F, dtype=torch.float32, device=dev)
@@ -1089,7 +1092,12 @@ class FusedDeepFM:
             if st is not None:
                 t_end.record(main)
             self._pl_op("main", f"main graph @{self._i}", main_rng)
-            side.wait_event(before)
+            if self._side_after_main:  # diagnostic: the side graph after the main graph (no overlap)
+                after = torch.cuda.Event()
+                after.record(main)
+                side.wait_event(after)
+            else:
+                side.wait_event(before)
             self._pl_wait("side", before)
             with torch.cuda.stream(side):
                 gs.replay()
