@@ -300,7 +300,7 @@ class FusedDeepFM:
         # bit 0 preallocated launch events + no wait on a side graph already complete, bit 1 lazy
         # trailing join of the side chain
         self._lean_launch = int(os.environ.get("ROCFM_LEAN_LAUNCH", "3"))
-        self._lean_evs = [[torch.cuda.Event(), torch.cuda.Event()] for _ in range(2)]
+        self._lean_evs = [[torch.cuda.Event(), torch.cuda.Event()] for _ in range(8)]
         self._side_join_pending = False
         # ROCFM_SIDE_AFTER_MAIN=1 (diagnostic): serialise each side graph behind its main graph, to
         # measure what the overlapped side chain costs the main chain
@@ -1072,10 +1072,11 @@ class FusedDeepFM:
             # the side graph still waits only for the main work queued BEFORE this main graph
             lean = self._lean_launch
             if lean & 1:
-                # (ROCFM_LEAN_LAUNCH bit 0) two preallocated events per parity instead of two
+                # (ROCFM_LEAN_LAUNCH bit 0) preallocated events instead of two
                 # hipEventCreate calls ahead of the replay, and no barrier packet for a side graph the
                 # host already sees complete (the window's first graph after a synchronize)
-                evs = self._lean_evs[q]
+                # (a ring of 8 launches: train_stream keeps the side events of the last 4 graphs)
+                evs = self._lean_evs[self._m_warm % len(self._lean_evs)]
                 before = self._pl_mark(evs[0], "main")
             else:
                 before = self._pl_mark(torch.cuda.Event(), "main")
