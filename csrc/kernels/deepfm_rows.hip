@@ -67,6 +67,23 @@ __device__ __forceinline__ uint32_t pick4(const Philox4& b, int i) {
   return i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
 }
 
+// lane exchange within DPP rows: v of lane quad_perm / mirror partner (full waves only)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over each 32-lane half of a wave, to every lane of the half: lanes ^1 and ^2 (quad_perm),
+// then the 8- and 16-lane mirrors (after the quad steps every lane of a quad holds its sum, so the
+// mirror partner is a partner of the other quad / half-row), on DPP; then the other 16-lane row by
+// one ds_bpermute — four of the five butterfly levels without an LDS-pipe round trip
+__device__ __forceinline__ float half_wave_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += dpp_f<0x141>(v);  // row_half_mirror: lane i <-> 7 - i within 8
+  v += dpp_f<0x140>(v);  // row_mirror: lane i <-> 15 - i within 16
+  return v + __shfl_xor(v, 16, 64);
+}
+
 // x / F for x < 4096, F <= 64 (host-checked): magic = floor(2^32 / F) + 1
 __device__ __forceinline__ int fdiv(int x, uint32_t magic) { return (int)__umulhi((uint32_t)x, magic); }
 
@@ -547,11 +564,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
       }
     }
     for (int f = q; f < F; f += 32) yw += s_wx[r * F + f];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      cterm += __shfl_xor(cterm, o, 64);
-      yw += __shfl_xor(yw, o, 64);
-    }
+    cterm = half_wave_sum(cterm);  // (each row: one 32-lane half of the wave)
+    yw = half_wave_sum(yw);
     if (q == 0) s_ylin[r] = s_prm[L.prm_fmb] + yw + 0.5f * cterm;
   }
   if (train && !(ablate & 1)) {  // h0ᵀ for dW_0: 8 rows × 1 column per item → one 16-B store
@@ -875,8 +889,8 @@ __global__ __launch_bounds__(kRowThreads) void deepfm_rows_kernel(const RowsPara
     const int r = lane >> 2, q = lane & 3;
     float s = 0.f;
     for (int c = q; c < Dn; c += 4) s += bf2f(H[r * ldh + c]) * s_prm[L.prm_wout + c];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+    s += dpp_f<0xB1>(s);  // lane ^ 1 (quad_perm; the same sums as the xor shuffles)
+    s += dpp_f<0x4E>(s);  // lane ^ 2
     if (q == 0) {
       const int gr = row0 + r;
       const bool valid = r < RT && gr < p.B;

@@ -1,0 +1,13 @@
+# Round 6 (bn): FM / head reductions on DPP (rows kernel phases B and D) — numerics tests, phase
+# stamps, driver-shaped windows
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6bn
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_fused_kernels_gpu.py tests/test_trajectory_gpu.py tests/test_bf16_table_gpu.py -x -v --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_d.txt 2>&1 || exit 1
+K=32 V=117581 MULTI=1 timeout -k 10 200 python tools/diag_phases.py > $O/phases_n.txt 2>&1 || exit 1
+B="python bench.py --gpus 1 --no_secondary --steps 20 --warmup 5"
+for rep in 1 2 3; do
+  timeout -k 10 150 $B > $O/d20_$rep.json 2>/dev/null || exit 1
+  timeout -k 10 150 $B --embedding_size 32 --feature_size 117581 > $O/n20_$rep.json 2>/dev/null || exit 1
+done
