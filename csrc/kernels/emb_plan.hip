@@ -1,8 +1,8 @@
 // The step tail's embedding work plan (EmbPlanParams, emb_update.h), one workgroup per batch, run on
 // the side chain for every batch of the next multi-step graph (fused.py _prepare_multi).
-// 512 threads (48 VGPRs: 2 waves per SIMD): a plan workgroup fits on a CU beside a k = 32 row-tile
-// workgroup, so the 256-workgroup row kernel no longer waits for CUs the plan holds (1,024 threads:
-// up to 4 row tiles entered 14 µs late; profiles/r6_side_overlap.md)
+// 256 threads (48 VGPRs: one wave per SIMD): a plan workgroup fits on a CU beside a k = 32 row-tile
+// workgroup (the split ones included), so the 256-workgroup row kernels no longer wait for CUs the
+// plan holds (1,024 threads: up to 4 row tiles entered 14 µs late; profiles/r6_side_overlap.md)
 //
 // Why: the unplanned tail gives every workgroup 256 consecutive sorted lookups.  A chunk's cost is
 // its gradient rows plus one table / Adam-slot round trip per run head, and heads per chunk range
@@ -22,7 +22,7 @@
 
 namespace rocfm {
 
-constexpr int kPlanThreads = 512;
+constexpr int kPlanThreads = 256;
 
 constexpr int kPlanWaves = kPlanThreads / 64;
 
